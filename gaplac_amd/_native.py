@@ -1,0 +1,109 @@
+"""ctypes binding of libgaplac_hip.so (the C-ABI in include/gaplac.h).
+
+The product path has no fallback: if the HIP library is missing or fails to load this
+module raises, and every logpdf call fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_void_p
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
+LIB_PATH = os.path.join(LIB_DIR, "libgaplac_hip.so")
+
+SQEXP, OU, LINEAR, CAT, NOISE = 1, 2, 3, 4, 5
+KIND_NAMES = {SQEXP: "SQEXP", OU: "OU", LINEAR: "LINEAR", CAT: "CAT", NOISE: "NOISE"}
+MAX_TERMS = 16
+
+E_ARG, E_KIND, E_PARAM, E_COL, E_NODEVICE, E_HIP, E_OOM, E_COMM = -1, -2, -3, -4, -5, -6, -7, -8
+
+# Every symbol include/gaplac.h declares (checked by tests/test_abi.py).
+EXPORTED = (
+    "gaplac_abi_version",
+    "gaplac_last_error",
+    "gaplac_ctx_create",
+    "gaplac_ctx_destroy",
+    "gaplac_logpdf",
+    "gaplac_logpdf_device",
+    "gaplac_logpdf_batch",
+    "gaplac_gram",
+    "gaplac_factor",
+    "gaplac_set_profiling",
+    "gaplac_get_stats",
+    "gaplac_reset_stats",
+)
+
+
+class Term(ctypes.Structure):
+    _fields_ = [
+        ("kind", c_int32),
+        ("col", c_int32),
+        ("param", c_double),
+        ("group", c_int32),
+        ("reserved", c_int32),
+    ]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("evals", c_int64),
+        ("syrk_launches", c_int64),
+        ("syrk_ms", c_double),
+        ("syrk_flops", c_double),
+        ("gram_ms", c_double),
+        ("gram_bytes", c_double),
+        ("gram_launches", c_int64),
+        ("panel_ms", c_double),
+        ("total_ms", c_double),
+    ]
+
+
+_lib = None
+
+_DP = POINTER(c_double)
+
+
+def load() -> ctypes.CDLL:
+    """Load the HIP library once; raise if it is absent (no CPU fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"libgaplac_hip.so not built ({LIB_PATH}); run `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.gaplac_abi_version.restype = c_int
+    lib.gaplac_last_error.restype = c_char_p
+    lib.gaplac_last_error.argtypes = [c_void_p]
+    lib.gaplac_ctx_create.argtypes = [c_int, POINTER(c_void_p)]
+    lib.gaplac_ctx_destroy.argtypes = [c_void_p]
+    common = [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, POINTER(Term), c_double, c_void_p]
+    lib.gaplac_logpdf.argtypes = common + [_DP, _DP, _DP]
+    lib.gaplac_logpdf_device.argtypes = common + [_DP, _DP, _DP]
+    lib.gaplac_logpdf_batch.argtypes = [
+        c_void_p, c_int32, c_int64, c_int32, c_void_p, c_int64, POINTER(c_int32), POINTER(Term),
+        c_double, c_void_p, _DP, POINTER(c_int64),
+    ]
+    lib.gaplac_gram.argtypes = [
+        c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, POINTER(Term), c_double, c_void_p, c_int64,
+    ]
+    lib.gaplac_factor.argtypes = common + [c_void_p, c_int64, c_void_p]
+    lib.gaplac_set_profiling.argtypes = [c_void_p, c_int]
+    lib.gaplac_get_stats.argtypes = [c_void_p, POINTER(Stats)]
+    lib.gaplac_reset_stats.argtypes = [c_void_p]
+    for name in EXPORTED:
+        getattr(lib, name).restype = getattr(lib, name).restype or c_int
+    lib.gaplac_last_error.restype = c_char_p
+    _lib = lib
+    return lib
+
+
+def term_array(terms) -> "ctypes.Array[Term]":
+    """terms: iterable of (kind, col, param, group)."""
+    terms = list(terms)
+    arr = (Term * max(1, len(terms)))()
+    for i, (kind, col, param, group) in enumerate(terms):
+        arr[i] = Term(int(kind), int(col), float(param), int(group), 0)
+    return arr

@@ -1,0 +1,175 @@
+"""Python handle on the HIP backend: a device context and the logpdf entry points.
+
+This is the Python mirror of the `ccall` glue a GaPLAC maintainer would add in Julia
+(INTEGRATION.md); numpy arrays stand in for Julia's GC-owned column-major buffers.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_double, c_int32, c_int64, c_void_p
+
+import numpy as np
+
+from . import _native
+from ._native import Term, term_array
+
+
+class GaplacError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"gaplac error {code}: {msg}")
+        self.code = code
+
+
+class PosDefException(ArithmeticError):
+    """Mirror of Julia's LinearAlgebra.PosDefException(info) (cholesky check=true)."""
+
+    def __init__(self, info: int):
+        super().__init__(f"PosDefException: matrix is not positive definite; Cholesky factorization failed (info={info})")
+        self.info = info
+
+
+class ArgumentError(ValueError):
+    """Mirror of Julia's ArgumentError for invalid kernel parameters / arguments."""
+
+
+def _colmajor(X: np.ndarray) -> np.ndarray:
+    X = np.asarray(X, dtype=np.float64)
+    if X.ndim == 1:
+        X = X[:, None]
+    return np.asfortranarray(X)
+
+
+class Context:
+    """One device, one persistent workspace (gaplac_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _native.load()
+        h = c_void_p()
+        rc = self.lib.gaplac_ctx_create(int(device), byref(h))
+        if rc != 0:
+            raise GaplacError(rc, f"gaplac_ctx_create(device={device}) failed")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gaplac_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ------------------------------------------------------------------ helpers
+    def _check(self, rc: int):
+        if rc == 0:
+            return
+        if rc > 0:
+            raise PosDefException(rc)
+        msg = self.lib.gaplac_last_error(self.h)
+        msg = msg.decode() if msg else ""
+        if rc in (_native.E_PARAM, _native.E_KIND, _native.E_COL, _native.E_ARG):
+            raise ArgumentError(f"gaplac error {rc}: {msg}")
+        raise GaplacError(rc, msg)
+
+    # ------------------------------------------------------------------ entries
+    def logpdf(self, X, terms, noise: float, v, full: bool = False):
+        """logpdf of the zero-mean FiniteGP; full=True returns (logpdf, logdet, quad)."""
+        Xc = _colmajor(X)
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        N, D = Xc.shape
+        if v.shape[0] != N:
+            raise ArgumentError(f"length of v ({v.shape[0]}) != N ({N})")
+        ta = term_array(terms)
+        lp, ld, q = c_double(), c_double(), c_double()
+        rc = self.lib.gaplac_logpdf(
+            self.h, N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), len(list(terms)), ta, float(noise),
+            v.ctypes.data_as(c_void_p), byref(lp), byref(ld), byref(q),
+        )
+        self._check(rc)
+        return (lp.value, ld.value, q.value) if full else lp.value
+
+    def logpdf_device(self, N: int, D: int, dX_ptr: int, ldx: int, terms, noise: float, dv_ptr: int, full=False):
+        ta = term_array(terms)
+        lp, ld, q = c_double(), c_double(), c_double()
+        rc = self.lib.gaplac_logpdf_device(
+            self.h, N, D, c_void_p(dX_ptr), ldx, len(list(terms)), ta, float(noise), c_void_p(dv_ptr),
+            byref(lp), byref(ld), byref(q),
+        )
+        self._check(rc)
+        return (lp.value, ld.value, q.value) if full else lp.value
+
+    def logpdf_batch(self, X, models, noise: float, v):
+        """models: list of term lists. Returns (logpdf array, info array)."""
+        Xc = _colmajor(X)
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        N, D = Xc.shape
+        offs = [0]
+        flat = []
+        for m in models:
+            flat.extend(list(m))
+            offs.append(len(flat))
+        ta = term_array(flat)
+        off_arr = (c_int32 * len(offs))(*offs)
+        out = np.empty(len(models), dtype=np.float64)
+        info = np.zeros(len(models), dtype=np.int64)
+        rc = self.lib.gaplac_logpdf_batch(
+            self.h, len(models), N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), off_arr, ta, float(noise),
+            v.ctypes.data_as(c_void_p), out.ctypes.data_as(ctypes.POINTER(c_double)),
+            info.ctypes.data_as(ctypes.POINTER(c_int64)),
+        )
+        self._check(rc)
+        return out, info
+
+    def gram(self, X, terms, noise: float = 0.0) -> np.ndarray:
+        Xc = _colmajor(X)
+        N, D = Xc.shape
+        out = np.empty((N, N), dtype=np.float64, order="F")
+        ta = term_array(terms)
+        rc = self.lib.gaplac_gram(self.h, N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), len(list(terms)), ta,
+                                  float(noise), out.ctypes.data_as(c_void_p), max(N, 1))
+        self._check(rc)
+        return out
+
+    def factor(self, X, terms, noise: float, v):
+        """(L, z): lower Cholesky factor of C and z = L^{-1} v."""
+        Xc = _colmajor(X)
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        N, D = Xc.shape
+        L = np.empty((N, N), dtype=np.float64, order="F")
+        z = np.empty(N, dtype=np.float64)
+        ta = term_array(terms)
+        rc = self.lib.gaplac_factor(self.h, N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), len(list(terms)), ta,
+                                    float(noise), v.ctypes.data_as(c_void_p), L.ctypes.data_as(c_void_p),
+                                    max(N, 1), z.ctypes.data_as(c_void_p))
+        self._check(rc)
+        return L, z
+
+    def set_profiling(self, on: bool):
+        self.lib.gaplac_set_profiling(self.h, 1 if on else 0)
+
+    def stats(self) -> dict:
+        s = _native.Stats()
+        self.lib.gaplac_get_stats(self.h, byref(s))
+        return {name: getattr(s, name) for name, _ in _native.Stats._fields_}
+
+    def reset_stats(self):
+        self.lib.gaplac_reset_stats(self.h)
+
+
+_default_ctx: Context | None = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx

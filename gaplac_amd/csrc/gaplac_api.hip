@@ -1,0 +1,529 @@
+// Host side of libgaplac_hip.so: the C-ABI declared in include/gaplac.h.
+//
+// One evaluation = Gram build + blocked right-looking Cholesky of the (N+1)-augmented
+// matrix with one-panel lookahead + logdet/quad reduction:
+//
+//   s_main : gram | wait(P0) syrk_col(1) rec(L1) syrk_tri(2..) | wait(P1) syrk_col(2) ...
+//   s_panel:        potrf(0) trsm(0) rec(P0) | wait(L1) potrf(1) trsm(1) rec(P1) | ...
+//
+// The panel stream has the device's highest priority so the factorisation of panel k+1
+// (critical path) overlaps the bulk trailing update of step k.
+#include "gaplac_internal.h"
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace gaplac;
+
+struct gaplac_ctx {
+    int device = 0;
+    hipStream_t s_main = nullptr, s_panel = nullptr;
+    hipEvent_t ev_look = nullptr, ev_panel = nullptr, ev_gram = nullptr;
+    double* A = nullptr;
+    size_t A_elems = 0;
+    double* Linv = nullptr;
+    size_t Linv_elems = 0;
+    double* dX = nullptr;
+    size_t dX_elems = 0;
+    double* dv = nullptr;
+    size_t dv_elems = 0;
+    EvalResult* dres = nullptr;
+    EvalResult* hres = nullptr;  // pinned
+    std::string err;
+    // profiling
+    bool profiling = false;
+    gaplac_stats stats{};
+    std::vector<hipEvent_t> evpool;
+    size_t evused = 0;
+    struct Span {
+        int kind;  // 0 syrk, 1 gram, 2 panel, 3 total
+        hipEvent_t a, b;
+        double work;
+    };
+    std::vector<Span> spans;
+};
+
+namespace {
+
+int set_err(gaplac_ctx* ctx, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+int set_err(gaplac_ctx* ctx, int code, const char* fmt, ...) {
+    if (ctx) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        ctx->err = buf;
+    }
+    return code;
+}
+
+#define HIPCK(ctx, call)                                                                   \
+    do {                                                                                   \
+        hipError_t e_ = (call);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return set_err(ctx, GAPLAC_E_HIP, "%s failed: %s", #call, hipGetErrorString(e_)); \
+    } while (0)
+
+int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+
+// Validate terms and build the kernel-argument pack. Mirrors the argument checks of the
+// KernelFunctions constructors GaPLAC calls (src/abstractgp_translations.jl:8-15):
+// LinearKernel requires c >= 0; ScaleTransform(1/l) requires a positive finite scale.
+int pack_terms(gaplac_ctx* ctx, int32_t D, int32_t T, const gaplac_term* terms, TermPack* tp) {
+    if (T < 0 || T > GAPLAC_MAX_TERMS)
+        return set_err(ctx, GAPLAC_E_KIND, "term count %d outside [0, %d]", T, GAPLAC_MAX_TERMS);
+    if (T > 0 && !terms) return set_err(ctx, GAPLAC_E_ARG, "terms is NULL");
+    std::memset(tp, 0, sizeof *tp);
+    tp->T = T;
+    for (int t = 0; t < T; ++t) {
+        const gaplac_term& x = terms[t];
+        if (x.reserved != 0) return set_err(ctx, GAPLAC_E_ARG, "term %d: reserved field not 0", t);
+        // groups must be contiguous: a group id seen before must be the previous term's
+        for (int u = 0; u + 1 < t; ++u)
+            if (terms[u].group == x.group && terms[t - 1].group != x.group)
+                return set_err(ctx, GAPLAC_E_KIND, "term %d: product group %d not contiguous", t,
+                               x.group);
+        tp->kind[t] = x.kind;
+        tp->col[t] = x.col;
+        switch (x.kind) {
+            case GAPLAC_SQEXP:
+            case GAPLAC_OU:
+                if (!(x.param > 0.0) || !std::isfinite(x.param))
+                    return set_err(ctx, GAPLAC_E_PARAM, "term %d: lengthscale %g must be > 0", t,
+                                   x.param);
+                tp->p[t] = 1.0 / x.param;  // ScaleTransform(inv(l))
+                if (!(tp->p[t] > 0.0))
+                    return set_err(ctx, GAPLAC_E_PARAM, "term %d: scale 1/l underflows", t);
+                break;
+            case GAPLAC_LINEAR:
+                if (!(x.param >= 0.0) || !std::isfinite(x.param))
+                    return set_err(ctx, GAPLAC_E_PARAM, "term %d: c = %g must be >= 0", t, x.param);
+                tp->p[t] = x.param;
+                break;
+            case GAPLAC_CAT:
+                tp->p[t] = 0.0;
+                break;
+            case GAPLAC_NOISE:
+                if (!(x.param >= 0.0) || !std::isfinite(x.param))
+                    return set_err(ctx, GAPLAC_E_PARAM, "term %d: noise variance %g must be >= 0",
+                                   t, x.param);
+                tp->p[t] = x.param;
+                tp->col[t] = 0;
+                break;
+            default:
+                return set_err(ctx, GAPLAC_E_KIND, "term %d: unknown kind %d", t, x.kind);
+        }
+        if (x.kind != GAPLAC_NOISE && (x.col < 0 || x.col >= D))
+            return set_err(ctx, GAPLAC_E_COL, "term %d: column %d outside [0, %d)", t, x.col, D);
+        tp->last_in_group[t] = (t == T - 1 || terms[t + 1].group != x.group) ? 1 : 0;
+    }
+    return 0;
+}
+
+int check_common(gaplac_ctx* ctx, int64_t N, int32_t D, const void* X, int64_t ldx, double noise,
+                 const void* v) {
+    if (!ctx) return GAPLAC_E_ARG;
+    if (N < 0) return set_err(ctx, GAPLAC_E_ARG, "N = %lld < 0", (long long)N);
+    if (N > 0 && D > 0 && (!X || ldx < N))
+        return set_err(ctx, GAPLAC_E_ARG, "X NULL or ldx %lld < N %lld", (long long)ldx,
+                       (long long)N);
+    if (N > 0 && !v) return set_err(ctx, GAPLAC_E_ARG, "v is NULL");
+    if (D < 0) return set_err(ctx, GAPLAC_E_ARG, "D = %d < 0", D);
+    if (!(noise >= 0.0) || !std::isfinite(noise))
+        return set_err(ctx, GAPLAC_E_PARAM, "noise %g must be finite and >= 0", noise);
+    return 0;
+}
+
+template <typename T>
+int ensure(gaplac_ctx* ctx, T** p, size_t* cap, size_t n) {
+    if (*cap >= n) return 0;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T)) != hipSuccess)
+        return set_err(ctx, GAPLAC_E_OOM, "hipMalloc of %zu bytes failed", n * sizeof(T));
+    *cap = n;
+    return 0;
+}
+
+hipEvent_t pool_event(gaplac_ctx* ctx) {
+    if (ctx->evused == ctx->evpool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        ctx->evpool.push_back(e);
+    }
+    return ctx->evpool[ctx->evused++];
+}
+
+struct SpanGuard {
+    gaplac_ctx* ctx;
+    hipStream_t s;
+    int kind;
+    double work;
+    hipEvent_t a = nullptr;
+    SpanGuard(gaplac_ctx* c, hipStream_t st, int k, double w) : ctx(c), s(st), kind(k), work(w) {
+        if (ctx->profiling) {
+            a = pool_event(ctx);
+            if (a) (void)hipEventRecord(a, s);
+        }
+    }
+    ~SpanGuard() {
+        if (ctx->profiling && a) {
+            hipEvent_t b = pool_event(ctx);
+            if (b) {
+                (void)hipEventRecord(b, s);
+                ctx->spans.push_back({kind, a, b, work});
+            }
+        }
+    }
+};
+
+// Algorithmic flops of one trailing-update launch: lower triangle (incl. diagonal) of the
+// updated tiles, 2 flops per multiply-add, K = NB.
+double syrk_flops(int m, int colmode) {
+    const double nbd = NB;
+    if (colmode) {  // one diagonal tile + (m-1) full tiles
+        return 2.0 * nbd * ((m - 1) * nbd * nbd + nbd * (nbd + 1) / 2.0);
+    }
+    const double rows = (double)m * nbd;
+    return 2.0 * nbd * rows * (rows + 1) / 2.0;
+}
+
+void collect_spans(gaplac_ctx* ctx) {
+    for (auto& sp : ctx->spans) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, sp.a, sp.b) != hipSuccess) continue;
+        switch (sp.kind) {
+            case 0:
+                ctx->stats.syrk_ms += ms;
+                ctx->stats.syrk_flops += sp.work;
+                ctx->stats.syrk_launches += 1;
+                break;
+            case 1:
+                ctx->stats.gram_ms += ms;
+                ctx->stats.gram_bytes += sp.work;
+                ctx->stats.gram_launches += 1;
+                break;
+            case 2:
+                ctx->stats.panel_ms += ms;
+                break;
+            default:
+                ctx->stats.total_ms += ms;
+                break;
+        }
+    }
+    ctx->spans.clear();
+    ctx->evused = 0;
+}
+
+// Factor the augmented matrix already built in ctx->A (Gram launched on s_main).
+int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
+    hipStream_t sm = ctx->s_main, sp = ctx->s_panel;
+    HIPCK(ctx, hipEventRecord(ctx->ev_gram, sm));
+    HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_gram, 0));
+    {
+        SpanGuard g(ctx, sp, 2, 0);
+        launch_potrf_diag(sp, ctx->A, lda, N, 0, ctx->Linv, ctx->dres);
+        launch_trsm(sp, ctx->A, lda, nt, 0, ctx->Linv);
+    }
+    HIPCK(ctx, hipEventRecord(ctx->ev_panel, sp));
+    for (int k = 0; k < nt; ++k) {
+        HIPCK(ctx, hipStreamWaitEvent(sm, ctx->ev_panel, 0));
+        if (k + 1 >= nt) break;
+        {
+            SpanGuard g(ctx, sm, 0, syrk_flops(nt - (k + 1), 1));
+            launch_syrk(sm, ctx->A, lda, nt, k, k + 1, 1);
+        }
+        HIPCK(ctx, hipEventRecord(ctx->ev_look, sm));
+        HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_look, 0));
+        {
+            SpanGuard g(ctx, sp, 2, 0);
+            double* Lk = ctx->Linv + (size_t)(k + 1) * NB * NB;
+            if ((int64_t)(k + 1) * NB < N) launch_potrf_diag(sp, ctx->A, lda, N, k + 1, Lk, ctx->dres);
+            launch_trsm(sp, ctx->A, lda, nt, k + 1, Lk);
+        }
+        HIPCK(ctx, hipEventRecord(ctx->ev_panel, sp));
+        if (k + 2 < nt) {
+            SpanGuard g(ctx, sm, 0, syrk_flops(nt - (k + 2), 0));
+            launch_syrk(sm, ctx->A, lda, nt, k, k + 2, 0);
+        }
+    }
+    launch_reduce(sm, ctx->A, lda, N, ctx->dres);
+    HIPCK(ctx, hipGetLastError());
+    return 0;
+}
+
+// Full evaluation with X, v already on the device. Leaves the factor in ctx->A.
+int eval_device(gaplac_ctx* ctx, int64_t N, int32_t D, const double* dX, int64_t ldx,
+                const TermPack& tp, double noise, const double* dv, EvalResult* out) {
+    const int64_t Np = round_up(N + 1, NB);
+    const int nt = (int)(Np / NB);
+    int rc;
+    if ((rc = ensure(ctx, &ctx->A, &ctx->A_elems, (size_t)Np * Np))) return rc;
+    if ((rc = ensure(ctx, &ctx->Linv, &ctx->Linv_elems, (size_t)nt * NB * NB))) return rc;
+    HIPCK(ctx, hipSetDevice(ctx->device));
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    if (ctx->profiling) {
+        t0 = pool_event(ctx);
+        t1 = pool_event(ctx);
+        HIPCK(ctx, hipEventRecord(t0, ctx->s_main));
+    }
+    launch_init_result(ctx->s_main, ctx->dres);
+    {
+        const double bytes = 8.0 * (double)Np * (double)(Np + 1) / 2.0 + 8.0 * (double)N * (D + 1);
+        SpanGuard g(ctx, ctx->s_main, 1, bytes);
+        launch_gram(ctx->s_main, ctx->A, Np, N, nt, dX, ldx, dv, tp, noise);
+    }
+    if ((rc = factor_and_reduce(ctx, N, Np, nt))) return rc;
+    HIPCK(ctx, hipMemcpyAsync(ctx->hres, ctx->dres, sizeof(EvalResult), hipMemcpyDeviceToHost,
+                              ctx->s_main));
+    if (ctx->profiling) {
+        HIPCK(ctx, hipEventRecord(t1, ctx->s_main));
+        ctx->spans.push_back({3, t0, t1, 0});
+    }
+    HIPCK(ctx, hipStreamSynchronize(ctx->s_main));
+    *out = *ctx->hres;
+    if (ctx->profiling) {
+        ctx->stats.evals += 1;
+        collect_spans(ctx);
+    }
+    return 0;
+}
+
+int finish(const EvalResult& r, double* out_logpdf, double* out_logdet, double* out_quad) {
+    if (out_logdet) *out_logdet = r.logdet;
+    if (out_quad) *out_quad = r.quad;
+    if (r.info != ~0ull) {
+        if (out_logpdf) *out_logpdf = NAN;
+        return (int)(r.info > 0x7fffffffull ? 0x7fffffff : r.info);
+    }
+    if (out_logpdf) *out_logpdf = r.logpdf;
+    return 0;
+}
+
+int upload(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx, const double* v) {
+    int rc;
+    const size_t nx = (size_t)N * (size_t)(D > 0 ? D : 1);
+    if ((rc = ensure(ctx, &ctx->dX, &ctx->dX_elems, nx))) return rc;
+    if ((rc = ensure(ctx, &ctx->dv, &ctx->dv_elems, (size_t)N))) return rc;
+    if (D > 0)
+        HIPCK(ctx, hipMemcpy2DAsync(ctx->dX, (size_t)N * 8, X, (size_t)ldx * 8, (size_t)N * 8,
+                                    (size_t)D, hipMemcpyHostToDevice, ctx->s_main));
+    HIPCK(ctx, hipMemcpyAsync(ctx->dv, v, (size_t)N * 8, hipMemcpyHostToDevice, ctx->s_main));
+    return 0;
+}
+
+void nan_out(double* a, double* b, double* c) {
+    if (a) *a = NAN;
+    if (b) *b = NAN;
+    if (c) *c = NAN;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gaplac_abi_version(void) { return GAPLAC_ABI_VERSION; }
+
+const char* gaplac_last_error(const gaplac_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int gaplac_ctx_create(int device, gaplac_ctx** out) {
+    if (!out) return GAPLAC_E_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return GAPLAC_E_NODEVICE;
+    if (device < 0 || device >= n) return GAPLAC_E_NODEVICE;
+    gaplac_ctx* ctx = new gaplac_ctx();
+    ctx->device = device;
+    auto fail = [&](const char* what, hipError_t e) {
+        std::fprintf(stderr, "gaplac_ctx_create: %s: %s\n", what, hipGetErrorString(e));
+        gaplac_ctx_destroy(ctx);
+        return GAPLAC_E_HIP;
+    };
+    hipError_t e;
+    if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
+    int least = 0, greatest = 0;
+    if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess)
+        return fail("priority range", e);
+    if ((e = hipStreamCreateWithPriority(&ctx->s_main, hipStreamNonBlocking, least)) != hipSuccess)
+        return fail("stream", e);
+    if ((e = hipStreamCreateWithPriority(&ctx->s_panel, hipStreamNonBlocking, greatest)) != hipSuccess)
+        return fail("stream", e);
+    if ((e = hipEventCreateWithFlags(&ctx->ev_look, hipEventDisableTiming)) != hipSuccess)
+        return fail("event", e);
+    if ((e = hipEventCreateWithFlags(&ctx->ev_panel, hipEventDisableTiming)) != hipSuccess)
+        return fail("event", e);
+    if ((e = hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming)) != hipSuccess)
+        return fail("event", e);
+    if ((e = hipMalloc(reinterpret_cast<void**>(&ctx->dres), sizeof(EvalResult))) != hipSuccess)
+        return fail("hipMalloc", e);
+    if ((e = hipHostMalloc(reinterpret_cast<void**>(&ctx->hres), sizeof(EvalResult), 0)) != hipSuccess)
+        return fail("hipHostMalloc", e);
+    *out = ctx;
+    return 0;
+}
+
+int gaplac_ctx_destroy(gaplac_ctx* ctx) {
+    if (!ctx) return 0;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->s_main) (void)hipStreamSynchronize(ctx->s_main);
+    if (ctx->s_panel) (void)hipStreamSynchronize(ctx->s_panel);
+    for (auto e : ctx->evpool) (void)hipEventDestroy(e);
+    if (ctx->ev_look) (void)hipEventDestroy(ctx->ev_look);
+    if (ctx->ev_panel) (void)hipEventDestroy(ctx->ev_panel);
+    if (ctx->ev_gram) (void)hipEventDestroy(ctx->ev_gram);
+    if (ctx->A) (void)hipFree(ctx->A);
+    if (ctx->Linv) (void)hipFree(ctx->Linv);
+    if (ctx->dX) (void)hipFree(ctx->dX);
+    if (ctx->dv) (void)hipFree(ctx->dv);
+    if (ctx->dres) (void)hipFree(ctx->dres);
+    if (ctx->hres) (void)hipHostFree(ctx->hres);
+    if (ctx->s_main) (void)hipStreamDestroy(ctx->s_main);
+    if (ctx->s_panel) (void)hipStreamDestroy(ctx->s_panel);
+    delete ctx;
+    return 0;
+}
+
+int gaplac_logpdf_device(gaplac_ctx* ctx, int64_t N, int32_t D, const double* dX, int64_t ldx,
+                         int32_t T, const gaplac_term* terms, double noise, const double* dv,
+                         double* out_logpdf, double* out_logdet, double* out_quad) {
+    nan_out(out_logpdf, out_logdet, out_quad);
+    int rc = check_common(ctx, N, D, dX, ldx, noise, dv);
+    if (rc) return rc;
+    TermPack tp;
+    if ((rc = pack_terms(ctx, D, T, terms, &tp))) return rc;
+    if (N == 0) {  // logpdf of an empty FiniteGP: -(0 + 0 + 0)/2
+        if (out_logpdf) *out_logpdf = -0.0;
+        if (out_logdet) *out_logdet = 0.0;
+        if (out_quad) *out_quad = 0.0;
+        return 0;
+    }
+    EvalResult r;
+    if ((rc = eval_device(ctx, N, D, dX, ldx, tp, noise, dv, &r))) return rc;
+    return finish(r, out_logpdf, out_logdet, out_quad);
+}
+
+int gaplac_logpdf(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx, int32_t T,
+                  const gaplac_term* terms, double noise, const double* v, double* out_logpdf,
+                  double* out_logdet, double* out_quad) {
+    nan_out(out_logpdf, out_logdet, out_quad);
+    int rc = check_common(ctx, N, D, X, ldx, noise, v);
+    if (rc) return rc;
+    TermPack tp;
+    if ((rc = pack_terms(ctx, D, T, terms, &tp))) return rc;
+    if (N == 0) {
+        if (out_logpdf) *out_logpdf = -0.0;
+        if (out_logdet) *out_logdet = 0.0;
+        if (out_quad) *out_quad = 0.0;
+        return 0;
+    }
+    HIPCK(ctx, hipSetDevice(ctx->device));
+    if ((rc = upload(ctx, N, D, X, ldx, v))) return rc;
+    EvalResult r;
+    if ((rc = eval_device(ctx, N, D, ctx->dX, N, tp, noise, ctx->dv, &r))) return rc;
+    return finish(r, out_logpdf, out_logdet, out_quad);
+}
+
+int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D, const double* X,
+                        int64_t ldx, const int32_t* term_offset, const gaplac_term* terms,
+                        double noise, const double* v, double* out_logpdf, int64_t* out_info) {
+    if (!ctx) return GAPLAC_E_ARG;
+    if (nmodels < 0 || (nmodels > 0 && (!term_offset || !out_logpdf || !out_info)))
+        return set_err(ctx, GAPLAC_E_ARG, "bad batch arguments");
+    for (int m = 0; m < nmodels; ++m) {
+        out_logpdf[m] = NAN;
+        out_info[m] = 0;
+    }
+    int rc = check_common(ctx, N, D, X, ldx, noise, v);
+    if (rc) return rc;
+    std::vector<TermPack> packs((size_t)nmodels);
+    for (int m = 0; m < nmodels; ++m) {
+        const int32_t a = term_offset[m], b = term_offset[m + 1];
+        if (a < 0 || b < a) return set_err(ctx, GAPLAC_E_ARG, "model %d: bad term offsets", m);
+        if ((rc = pack_terms(ctx, D, b - a, terms + a, &packs[(size_t)m]))) return rc;
+    }
+    if (N == 0) {
+        for (int m = 0; m < nmodels; ++m) out_logpdf[m] = -0.0;
+        return 0;
+    }
+    HIPCK(ctx, hipSetDevice(ctx->device));
+    if ((rc = upload(ctx, N, D, X, ldx, v))) return rc;
+    for (int m = 0; m < nmodels; ++m) {
+        EvalResult r;
+        if ((rc = eval_device(ctx, N, D, ctx->dX, N, packs[(size_t)m], noise, ctx->dv, &r))) return rc;
+        out_info[m] = finish(r, &out_logpdf[m], nullptr, nullptr);
+    }
+    return 0;
+}
+
+int gaplac_gram(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx, int32_t T,
+                const gaplac_term* terms, double noise, double* out_C, int64_t ldc) {
+    int rc = check_common(ctx, N, D, X, ldx, noise, X /* v unused */);
+    if (rc && N > 0) return rc;
+    if (N == 0) return 0;
+    if (!out_C || ldc < N) return set_err(ctx, GAPLAC_E_ARG, "out_C NULL or ldc < N");
+    TermPack tp;
+    if ((rc = pack_terms(ctx, D, T, terms, &tp))) return rc;
+    HIPCK(ctx, hipSetDevice(ctx->device));
+    std::vector<double> zeros((size_t)N, 0.0);
+    if ((rc = upload(ctx, N, D, X, ldx, zeros.data()))) return rc;
+    const int64_t Np = round_up(N + 1, NB);
+    const int nt = (int)(Np / NB);
+    if ((rc = ensure(ctx, &ctx->A, &ctx->A_elems, (size_t)Np * Np))) return rc;
+    launch_gram(ctx->s_main, ctx->A, Np, N, nt, ctx->dX, N, ctx->dv, tp, noise);
+    HIPCK(ctx, hipGetLastError());
+    HIPCK(ctx, hipMemcpy2DAsync(out_C, (size_t)ldc * 8, ctx->A, (size_t)Np * 8, (size_t)N * 8,
+                                (size_t)N, hipMemcpyDeviceToHost, ctx->s_main));
+    HIPCK(ctx, hipStreamSynchronize(ctx->s_main));
+    // only the lower triangle is built on the device; mirror it
+    for (int64_t j = 0; j < N; ++j)
+        for (int64_t i = 0; i < j; ++i) out_C[j * ldc + i] = out_C[i * ldc + j];
+    return 0;
+}
+
+int gaplac_factor(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx, int32_t T,
+                  const gaplac_term* terms, double noise, const double* v, double* out_L,
+                  int64_t ldl, double* out_z) {
+    int rc = check_common(ctx, N, D, X, ldx, noise, v);
+    if (rc) return rc;
+    if (N == 0) return 0;
+    if (!out_L || ldl < N || !out_z) return set_err(ctx, GAPLAC_E_ARG, "bad output buffers");
+    TermPack tp;
+    if ((rc = pack_terms(ctx, D, T, terms, &tp))) return rc;
+    HIPCK(ctx, hipSetDevice(ctx->device));
+    if ((rc = upload(ctx, N, D, X, ldx, v))) return rc;
+    EvalResult r;
+    if ((rc = eval_device(ctx, N, D, ctx->dX, N, tp, noise, ctx->dv, &r))) return rc;
+    const int64_t Np = round_up(N + 1, NB);
+    HIPCK(ctx, hipMemcpy2D(out_L, (size_t)ldl * 8, ctx->A, (size_t)Np * 8, (size_t)N * 8, (size_t)N,
+                           hipMemcpyDeviceToHost));
+    HIPCK(ctx, hipMemcpy2D(out_z, 8, ctx->A + N, (size_t)Np * 8, 8, (size_t)N, hipMemcpyDeviceToHost));
+    for (int64_t j = 0; j < N; ++j)
+        for (int64_t i = 0; i < j; ++i) out_L[j * ldl + i] = 0.0;
+    return finish(r, nullptr, nullptr, nullptr);
+}
+
+int gaplac_set_profiling(gaplac_ctx* ctx, int on) {
+    if (!ctx) return GAPLAC_E_ARG;
+    ctx->profiling = on != 0;
+    return 0;
+}
+
+int gaplac_get_stats(gaplac_ctx* ctx, gaplac_stats* out) {
+    if (!ctx || !out) return GAPLAC_E_ARG;
+    *out = ctx->stats;
+    return 0;
+}
+
+int gaplac_reset_stats(gaplac_ctx* ctx) {
+    if (!ctx) return GAPLAC_E_ARG;
+    ctx->stats = gaplac_stats{};
+    return 0;
+}
+
+}  // extern "C"

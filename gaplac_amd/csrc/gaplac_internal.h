@@ -1,0 +1,47 @@
+// Internal declarations shared by the HIP kernels (gaplac_kernels.hip) and the host
+// orchestration (gaplac_api.hip). Not part of the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/gaplac.h"
+
+namespace gaplac {
+
+// Panel width of the blocked right-looking Cholesky and edge of every square tile the
+// kernels work on (Gram tiles, diagonal blocks, trailing-update tiles). 128 fp64 x 128 =
+// 128 KiB: a diagonal block (plus its inverse, packed) fits one CU's 160 KiB LDS.
+constexpr int NB = 128;
+
+// Term descriptor in kernel-argument form (passed by value, lands in SGPRs).
+struct TermPack {
+    int32_t T;
+    int32_t kind[GAPLAC_MAX_TERMS];
+    int32_t col[GAPLAC_MAX_TERMS];
+    int32_t last_in_group[GAPLAC_MAX_TERMS];
+    double  p[GAPLAC_MAX_TERMS];  // 1/l for SQEXP/OU, c for LINEAR, variance for NOISE
+};
+
+// Device-side result record of one evaluation.
+struct EvalResult {
+    double logpdf;
+    double logdet;
+    double quad;
+    unsigned long long info;  // min over failing pivots of (j+1); ULLONG_MAX = none
+};
+
+// Launchers (gaplac_kernels.hip). A is the Np x Np column-major augmented matrix
+// (lda = Np, Np = roundup(N+1, NB)): rows/cols 0..N-1 hold C, row N holds v^T.
+void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt,
+                 const double* X, int64_t ldx, const double* v, const TermPack& tp,
+                 double noise);
+void launch_potrf_diag(hipStream_t s, double* A, int64_t lda, int64_t N, int k,
+                       double* Linv, EvalResult* res);
+// TRSM of the panel rows below diagonal block k: A[i,k] <- A[i,k] * Linv_k^T, i>k.
+void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Linv);
+// Trailing update with panel k. colmode=1: only tile column jb (tiles i>=jb);
+// colmode=0: lower triangle of tile blocks jb..nt-1.
+void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int colmode);
+void launch_reduce(hipStream_t s, const double* A, int64_t lda, int64_t N, EvalResult* res);
+void launch_init_result(hipStream_t s, EvalResult* res);
+
+}  // namespace gaplac

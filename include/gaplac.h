@@ -1,0 +1,150 @@
+/*
+ * gaplac.h — C-ABI of libgaplac_hip.so, the MI355X (gfx950) backend for GaPLAC's
+ * per-MCMC-step Gaussian-process log-marginal-likelihood.
+ *
+ * The reference computes, for every evaluation (AbstractGPs 0.5.12 `logpdf(::FiniteGP, v)`,
+ * reached from /root/reference/CLI/src/mcmc.jl:35 and /root/reference/CLI/src/select.jl:49-50):
+ *
+ *     C    = sum_t K_t(X) + noise * I          (kernelmatrix of the tree built by
+ *                                               GaPLAC.kernel, src/abstractgp_translations.jl:45-71)
+ *     U    = chol_upper(C)                     (LAPACK dpotrf('U'))
+ *     logp = -( N*log(2*pi) + 2*sum(log U_ii) + ||U^-T v||^2 ) / 2
+ *
+ * Each entry point below replaces one piece of that chain; all are plain C, plain
+ * pointers and sizes, no device types in the signatures. Host buffers passed in are
+ * copied during the call and never retained.
+ *
+ * Return convention (mirrors LinearAlgebra.cholesky(check=true) and the argument checks
+ * of KernelFunctions constructors):
+ *     0   success
+ *    >0   potrf `info`: 1-based order of the first leading minor that is not positive
+ *         definite (the Julia glue rethrows LinearAlgebra.PosDefException(info));
+ *         *out_logpdf is NaN
+ *    <0   an argument error (GAPLAC_E_*) or a HIP/RCCL runtime error; *out_logpdf is NaN
+ *         and gaplac_last_error() holds the text.
+ */
+#ifndef GAPLAC_H
+#define GAPLAC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GAPLAC_ABI_VERSION 1
+
+/* Kernel-term kinds. Each is the KernelFunctions 0.10.38 kernel that
+ * src/abstractgp_translations.jl:8-15 builds for one GaPLAC formula term. */
+enum gaplac_kind {
+    GAPLAC_SQEXP  = 1, /* SqExp(:x; l)  -> SqExponentialKernel ∘ ScaleTransform(1/l):
+                          k = exp(-((x_i - x_j)/l)^2 / 2)       src/gp_parts.jl:21-27 */
+    GAPLAC_OU     = 2, /* OU(:x; l)     -> ExponentialKernel ∘ ScaleTransform(1/l):
+                          k = exp(-|x_i - x_j|/l)                src/gp_parts.jl:37-43 */
+    GAPLAC_LINEAR = 3, /* Linear(:x; c) -> LinearKernel(c): k = x_i*x_j + c, c >= 0
+                                                                 src/gp_parts.jl:29-35 */
+    GAPLAC_CAT    = 4, /* Cat(:x)       -> CategoricalKernel: k = (x_i == x_j)
+                                                                 src/gp_parts.jl:11-13,45-47 */
+    GAPLAC_NOISE  = 5  /* extension (absent in the reference):
+                          k = param * delta_ij by index; col ignored */
+};
+
+/* One formula term after lowering. `param` is the lengthscale l (SQEXP, OU), the
+ * intercept c (LINEAR) or the variance (NOISE); ignored for CAT.
+ * `group`: terms with equal group multiply, groups add. The reference lowering
+ * (kernel(), abstractgp_translations.jl:45-69) only ever produces sums, so each term has
+ * its own group; shared groups are the true-product extension.
+ * Terms of one group must be contiguous in the array. */
+typedef struct gaplac_term {
+    int32_t kind;
+    int32_t col;     /* 0-based column of X */
+    double  param;
+    int32_t group;
+    int32_t reserved; /* must be 0 */
+} gaplac_term;
+
+#define GAPLAC_MAX_TERMS 16
+
+/* error codes (<0) */
+#define GAPLAC_E_ARG      (-1)  /* N < 0, D < 1 with terms reading X, ldx < N, null pointer */
+#define GAPLAC_E_KIND     (-2)  /* unknown term kind / too many terms / bad group order */
+#define GAPLAC_E_PARAM    (-3)  /* l <= 0 or non-finite, c < 0, noise < 0 */
+#define GAPLAC_E_COL      (-4)  /* column index outside [0, D) */
+#define GAPLAC_E_NODEVICE (-5)  /* no HIP device / device index out of range */
+#define GAPLAC_E_HIP      (-6)  /* HIP runtime failure (text in gaplac_last_error) */
+#define GAPLAC_E_OOM      (-7)  /* device allocation failed */
+#define GAPLAC_E_COMM     (-8)  /* RCCL failure / communicator missing */
+
+typedef struct gaplac_ctx gaplac_ctx;
+
+/* Context: one device, one persistent workspace (the (N+1)-augmented covariance,
+ * grown on demand and reused across MCMC steps), two HIP streams. Not re-entrant;
+ * distinct contexts may be used from distinct threads.
+ * Replaces: nothing in the reference (AbstractGPs allocates ~2T+3 N×N temporaries per
+ * logpdf); needed so repeated MCMC evaluations do not re-allocate. */
+int  gaplac_ctx_create(int device, gaplac_ctx** out);
+int  gaplac_ctx_destroy(gaplac_ctx* ctx);
+const char* gaplac_last_error(const gaplac_ctx* ctx);
+int  gaplac_abi_version(void);
+
+/* The hot path. Host pointers. X is N×D column-major with leading dimension ldx (Julia
+ * `Matrix(df[!, vars])` wrapped as RowVecs: observations are rows), v has N entries
+ * (`y` in select.jl:49-50, the latent `fx` in mcmc.jl:35). noise is the FiniteGP
+ * observation variance (0.1 at every reference call site).
+ * Replaces: AbstractGPs.logpdf(FiniteGP(GP(kernel(formula)), RowVecs(X), noise), v)
+ *           = kernelmatrix (KernelFunctions) + cholesky(Symmetric) (dpotrf 'U')
+ *             + logdet + sum(abs2, U' \ v).
+ * out_logdet / out_quad may be NULL. */
+int gaplac_logpdf(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx,
+                  int32_t T, const gaplac_term* terms, double noise, const double* v,
+                  double* out_logpdf, double* out_logdet, double* out_quad);
+
+/* Same, with X and v already resident in device memory (HBM) on the ctx's device.
+ * This is the entry the throughput benchmark times. */
+int gaplac_logpdf_device(gaplac_ctx* ctx, int64_t N, int32_t D, const double* dX, int64_t ldx,
+                         int32_t T, const gaplac_term* terms, double noise, const double* dv,
+                         double* out_logpdf, double* out_logdet, double* out_quad);
+
+/* Batched select (BASELINE config 5): nmodels independent formulas over the same X and
+ * v; model m uses terms[term_offset[m] .. term_offset[m+1]). Replaces the two (or more)
+ * `logpdf(pr_k, y_k)` calls of CLI/src/select.jl:49-50. out_logpdf / out_info have
+ * nmodels entries; the return value is 0 when the batch ran (per-model PD failures are
+ * reported in out_info[m] > 0 with out_logpdf[m] = NaN) and <0 on argument/runtime
+ * errors. */
+int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D,
+                        const double* X, int64_t ldx, const int32_t* term_offset,
+                        const gaplac_term* terms, double noise, const double* v,
+                        double* out_logpdf, int64_t* out_info);
+
+/* Debug / parity entries (tests only; not on the timed path). */
+/* Gram matrix sum_t K_t(X) + noise*I as a dense N×N column-major host matrix
+ * (replaces KernelFunctions.kernelmatrix + Diagonal(Fill(noise, N))). */
+int gaplac_gram(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx,
+                int32_t T, const gaplac_term* terms, double noise, double* out_C, int64_t ldc);
+/* Lower Cholesky factor L = U^T of the same C (dense N×N column-major, upper part
+ * zeroed) and z = L^{-1} v (replaces cholesky(Symmetric(C)).U' and U' \ v). */
+int gaplac_factor(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx,
+                  int32_t T, const gaplac_term* terms, double noise, const double* v,
+                  double* out_L, int64_t ldl, double* out_z);
+
+/* Per-kernel timing of the last evaluation(s), recorded with hipEvents on the stream
+ * each kernel is launched on, when profiling is on (off by default). */
+typedef struct gaplac_stats {
+    int64_t evals;
+    int64_t syrk_launches;      /* trailing-update launches */
+    double  syrk_ms;            /* summed event time of those launches */
+    double  syrk_flops;         /* algorithmic flops of those launches */
+    double  gram_ms;
+    double  gram_bytes;         /* algorithmic bytes of the Gram launches */
+    int64_t gram_launches;
+    double  panel_ms;           /* diag potrf + panel trsm, summed */
+    double  total_ms;           /* whole evaluation, first kernel to result */
+} gaplac_stats;
+int gaplac_set_profiling(gaplac_ctx* ctx, int on);
+int gaplac_get_stats(gaplac_ctx* ctx, gaplac_stats* out);
+int gaplac_reset_stats(gaplac_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GAPLAC_H */

@@ -1,0 +1,156 @@
+"""CPU restatement of GaPLAC's log-marginal-likelihood path — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module, and only as the checker / the timed CPU baseline — never as the product path.
+
+PARITY STATUS: **parity unpinned** by the reference. The reference (Julia 1.8.5 +
+KernelFunctions 0.10.38 + AbstractGPs 0.5.12 + OpenBLAS 0.3.20) cannot run in this
+container or on the GPU box (no `julia` binary, no depot, no network),
+and its own tests pin no numbers on this path (they cover formula parsing only,
+/root/reference/src/interface.jl:68-100). This restatement follows the documented
+definitions of the pinned packages and is cross-checked (tests/test_oracle.py) against
+scikit-learn's independent GaussianProcessRegressor.log_marginal_likelihood (RBF and
+Matern(nu=1/2) kernels) to ~1e-15 relative, and against a Distances.jl-style
+(`|a|^2+|b|^2-2ab`, clamped) distance computation to <=1e-9 relative logpdf.
+
+What it restates, with the reference lines it follows:
+  * term kernels — src/gp_parts.jl:11-13 (CategoricalKernel: kappa(d) = d > 0 ? 0 : 1 on
+    Euclidean), :21-47 (SqExp/Linear/OU/Cat structs), src/abstractgp_translations.jl:8-15
+    (makekernel: SqExponentialKernel / ExponentialKernel with_lengthscale(l) =
+    k ∘ ScaleTransform(1/l), LinearKernel(c), CategoricalKernel);
+  * term combination — src/abstractgp_translations.jl:45-69 (each term applied to its own
+    column through SelectTransform, terms summed: KernelSum = left fold);
+  * covariance + likelihood — CLI/src/select.jl:43-50 and CLI/src/mcmc.jl:35
+    (FiniteGP(GP(k), RowVecs(X), 0.1): C = K + 0.1 I, zero mean) and AbstractGPs'
+    logpdf = -(N log 2pi + logdet(C) + ||U^-T v||^2) / 2 with U = cholesky(Symmetric(C)).U
+    (LAPACK dpotrf('U'), here scipy's dpotrf) and U' \\ v (dtrtrs/dtrsv).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import scipy.linalg
+from scipy.linalg import lapack
+
+SQEXP, OU, LINEAR, CAT, NOISE = 1, 2, 3, 4, 5
+LOG2PI = 1.8378770664093453  # Julia's log2π as Float64
+
+
+class PosDefException(Exception):
+    """Mirror of LinearAlgebra.PosDefException(info)."""
+
+    def __init__(self, info: int):
+        super().__init__(f"PosDefException: matrix is not positive definite; Cholesky factorization failed (info={info})")
+        self.info = info
+
+
+def _pair(a: np.ndarray, kind: str, distances: str) -> np.ndarray:
+    """Pairwise squared-euclidean ('sq') or euclidean ('eu') distance of a 1-D coordinate.
+
+    distances='direct': (a_i - a_j)^2 — the mathematical definition.
+    distances='gemm'  : max(a_i^2 + a_j^2 - 2 a_i a_j, 0) — the BLAS form Distances.jl
+                        0.10.7 uses for pairwise(SqEuclidean/Euclidean, X; dims=1)
+                        [unverified-in-container, SURVEY.md §2].
+    """
+    if distances == "direct":
+        d = a[:, None] - a[None, :]
+        d2 = d * d
+    elif distances == "gemm":
+        sa = a * a
+        d2 = np.maximum(sa[:, None] + sa[None, :] - 2.0 * np.outer(a, a), 0.0)
+        np.fill_diagonal(d2, 0.0)
+    else:
+        raise ValueError(distances)
+    return d2 if kind == "sq" else np.sqrt(d2)
+
+
+def term_matrix(X: np.ndarray, kind: int, col: int, param: float, distances: str = "direct") -> np.ndarray:
+    """K_t for one term (KernelFunctions kernelmatrix of the term's kernel on its column)."""
+    N = X.shape[0]
+    if kind == NOISE:
+        return param * np.eye(N)
+    x = np.ascontiguousarray(X[:, col], dtype=np.float64)
+    if kind == SQEXP:
+        if not (param > 0) or not math.isfinite(param):
+            raise ValueError("lengthscale must be > 0")
+        s = 1.0 / param  # ScaleTransform(inv(l))
+        d2 = _pair(s * x, "sq", distances)
+        return np.exp(-d2 * 0.5)  # SqExponentialKernel: kappa(d2) = exp(-d2/2)
+    if kind == OU:
+        if not (param > 0) or not math.isfinite(param):
+            raise ValueError("lengthscale must be > 0")
+        s = 1.0 / param
+        d = _pair(s * x, "eu", distances)
+        return np.exp(-d)  # ExponentialKernel: kappa(d) = exp(-d)
+    if kind == LINEAR:
+        if not (param >= 0):
+            raise ValueError("LinearKernel: c >= 0 required")
+        return np.outer(x, x) + param  # kappa(xᵀy) = xᵀy + c
+    if kind == CAT:
+        if distances == "direct":
+            return (x[:, None] == x[None, :]).astype(np.float64)
+        d = _pair(x, "eu", distances)
+        return np.where(d > 0, 0.0, 1.0)
+    raise ValueError(f"unknown term kind {kind}")
+
+
+def gram(X: np.ndarray, terms, noise: float = 0.0, distances: str = "direct") -> np.ndarray:
+    """C = sum over groups of (product over the group's terms) + noise I.
+
+    terms: sequence of (kind, col, param, group); groups contiguous, summed in order.
+    """
+    X = np.asarray(X, dtype=np.float64)
+    if X.ndim == 1:
+        X = X[:, None]
+    N = X.shape[0]
+    total = np.zeros((N, N))
+    prod = None
+    terms = list(terms)
+    for t, (kind, col, param, group) in enumerate(terms):
+        K = term_matrix(X, kind, col, param, distances)
+        prod = K if prod is None else prod * K
+        last = t == len(terms) - 1 or terms[t + 1][3] != group
+        if last:
+            total = total + prod
+            prod = None
+    if noise:
+        total[np.diag_indices(N)] += noise
+    return total
+
+
+def logpdf_from_cov(C: np.ndarray, v: np.ndarray):
+    """AbstractGPs logpdf for zero mean: returns (logpdf, logdet, quad).
+
+    Raises PosDefException(info) like cholesky(check=true)."""
+    N = C.shape[0]
+    if N == 0:
+        return -0.0, 0.0, 0.0
+    U, info = lapack.dpotrf(C, lower=0, clean=1, overwrite_a=0)
+    if info > 0:
+        raise PosDefException(int(info))
+    if info < 0:
+        raise ValueError(f"dpotrf argument error {info}")
+    z = scipy.linalg.solve_triangular(U, v, trans="T", lower=False, check_finite=False)
+    dd = 0.0
+    for u in np.diag(U):  # logdet(::Cholesky): sequential sum of log diag, then dd + dd
+        dd += math.log(u)
+    logdet = dd + dd
+    quad = float(np.sum(z * z))
+    lp = -((N * LOG2PI + logdet) + quad) / 2
+    return float(lp), float(logdet), quad
+
+
+def logpdf(X, terms, noise: float, v, distances: str = "direct"):
+    """Whole path: (logpdf, logdet, quad)."""
+    C = gram(X, terms, noise, distances)
+    return logpdf_from_cov(C, np.asarray(v, dtype=np.float64))
+
+
+def cholesky_lower(X, terms, noise: float):
+    """L = U^T and z = U^-T v-ready factor for small parity checks."""
+    C = gram(X, terms, noise)
+    U, info = lapack.dpotrf(C, lower=0, clean=1)
+    if info > 0:
+        raise PosDefException(int(info))
+    return U.T.copy()
