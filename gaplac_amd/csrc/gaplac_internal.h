@@ -40,7 +40,10 @@ void launch_potrf_diag(hipStream_t s, double* A, int64_t lda, int64_t N, int k,
 void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Linv);
 // Trailing update with panel k. colmode=1: only tile column jb (tiles i>=jb);
 // colmode=0: lower triangle of tile blocks jb..nt-1.
-void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int colmode);
+// tiles: super-tile ordered list for the m x m triangle, m = nt - jb (build_tile_list).
+void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int colmode,
+                 const uint32_t* tiles);
+void build_tile_list(int m, uint32_t* out);
 void launch_reduce(hipStream_t s, const double* A, int64_t lda, int64_t N, EvalResult* res);
 void launch_init_result(hipStream_t s, EvalResult* res);
 

@@ -9,7 +9,7 @@
 //
 // Kernels:
 //   gram_kernel        Gram build, one 128x128 lower tile per workgroup (HBM-write bound)
-//   potrf_diag_kernel  128x128 diagonal block Cholesky + its triangular inverse, in LDS
+//   potrf_diag_kernel  128x128 diagonal block Cholesky + its triangular inverse (registers)
 //   tile_gemm_kernel   fp64 MFMA (v_mfma_f64_16x16x4f64) 128x128 tiles: trailing SYRK
 //                      update (C -= P Q^T) and panel TRSM (P <- P Linv^T)
 //   reduce_kernel      logdet = 2 sum log L_jj, quad = ||z||^2, logpdf
@@ -137,67 +137,114 @@ __global__ __launch_bounds__(256) void gram_kernel(double* __restrict__ A, int64
 }
 
 // ---------------------------------------------------------------------------------
-// Diagonal block: unblocked right-looking Cholesky of the 128x128 block in LDS, fused
-// with the forward elimination that yields Linv = L_kk^{-1} (used to turn the panel
-// TRSM into an MFMA GEMM). LDS packs both triangles into one 128 x 129 array:
-//   A(r,c), r >= c   at S[r*LS + c]
-//   R(r,c), c <= r   at S[c*LS + r + 1]   (R = running right-hand side, starts at I)
-// Iteration j reads column j of A and row j of R and writes columns > j of A and rows
-// > j of R, so one barrier per column suffices. Pivots of padding columns (>= N) are
-// forced to 1. A failing pivot (<= 0 or NaN, LAPACK dpotf2's test) records info = j+1.
+// Diagonal block: right-looking Cholesky of the 128x128 block fused with the forward
+// elimination that yields Linv = L_kk^{-1} (used to turn the panel TRSM into an MFMA
+// GEMM). Runs alone on CUs reserved for it (CU-masked stream, gaplac_api.hip).
+// Register-resident: 1024 threads = a 32 x 32 grid of 4x4 micro-tiles, t = cb*32 + rb:
+//   rb >= cb : A micro-tile (rb, cb)                    (a[][])
+//   cb >= rb : R micro-tile (cb, rb) of the RHS, R0 = I  (w[][]); after the elimination
+//              row j of R scaled by 1/L_jj is row j of L^{-1}.
+// Wave w holds column blocks 2w and 2w+1, so every owner of column j (and of row j of R)
+// sits in wave (j/4)/2 and a wave whose column blocks are finished stops computing.
+// Column j: the owning wave takes the pivot (sqrt, 1/d, LAPACK dpotf2's scaling), scales
+// column j and R's row j and publishes both, zero-padded, in a double-buffered LDS
+// vector; one barrier; every active wave applies the rank-1 update unconditionally
+// (the zero padding masks finished rows/columns). Pivots of padding columns (>= N) are
+// forced to 1; a failing pivot (<= 0 or NaN) records info = j+1.
 // ---------------------------------------------------------------------------------
-constexpr int LS = NB + 1;
-
 __global__ __launch_bounds__(1024) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
                                                           int64_t N, int k,
                                                           double* __restrict__ Linv,
                                                           EvalResult* __restrict__ res) {
-    __shared__ double S[NB * LS];
-    __shared__ double dd[NB];
-    __shared__ double rdd[NB];
-    const int tid = threadIdx.x;
+    __shared__ double colj[2][NB];
+    __shared__ double rowj[2][NB];
+    const int t = threadIdx.x;
+    const int cb = t >> 5, rb = t & 31, lane = t & 63;
+    const bool ownA = rb >= cb, ownR = cb >= rb;
     const int64_t g0 = (int64_t)k * NB;
     double* Ab = A + g0 * lda + g0;
-    for (int idx = tid; idx < NB * NB; idx += 1024) {
-        const int r = idx & (NB - 1), c = idx >> 7;
-        if (r >= c) {
-            S[r * LS + c] = Ab[(int64_t)c * lda + r];
-            S[c * LS + r + 1] = (r == c) ? 1.0 : 0.0;
+    double a[4][4], w[4][4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            a[i][x] = ownA ? Ab[(int64_t)(4 * cb + x) * lda + 4 * rb + i] : 0.0;
+            w[i][x] = (rb == cb && i == x) ? 1.0 : 0.0;
         }
-    }
-    __syncthreads();
-    const int r = tid & (NB - 1);
-    const int g = tid >> 7;  // column group 0..7
     for (int j = 0; j < NB; ++j) {
-        const double piv = S[j * LS + j];
-        double d;
-        if (g0 + j >= N) {
-            d = 1.0;
-        } else {
-            d = sqrt(piv);
-            if (!(piv > 0.0) && tid == 0)
-                atomicMin(&res->info, (unsigned long long)(g0 + j + 1));
-        }
-        const double rd = 1.0 / d;
-        if (tid == 0) {
-            dd[j] = d;
-            rdd[j] = rd;
-        }
-        if (r > j) {
-            const double lrj = S[r * LS + j] * rd;
-            for (int c = j + 1 + ((g - (j + 1)) & 7); c <= r; c += 8)
-                S[r * LS + c] -= lrj * (S[c * LS + j] * rd);
-            for (int c = g; c <= j; c += 8)
-                S[c * LS + r + 1] -= lrj * (S[c * LS + j + 1] * rd);
+        const int jb = j >> 2, jj = j & 3, p = j & 1;
+        if ((t >> 6) == (jb >> 1)) {  // the wave owning column j: pivot, scale, publish
+            const int plane = (jb & 1) * 32 + jb;
+            double piv = 0.0;
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+                if (x == jj) piv = a[x][x];
+            piv = __shfl(piv, plane);
+            double d, rd;
+            if (g0 + j >= N) {
+                d = 1.0;
+                rd = 1.0;
+            } else {
+                if (lane == plane && !(piv > 0.0))
+                    atomicMin(&res->info, (unsigned long long)(g0 + j + 1));
+                d = sqrt(piv);
+                rd = 1.0 / d;
+            }
+            if (cb == jb) {
+#pragma unroll
+                for (int x = 0; x < 4; ++x) {
+                    if (x != jj) continue;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int r = 4 * rb + i;
+                        const double sc = a[i][x] * rd;
+                        colj[p][r] = (r > j) ? sc : 0.0;
+                        a[i][x] = (r > j) ? sc : ((r == j) ? d : a[i][x]);
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (i != jj) continue;
+#pragma unroll
+                    for (int x = 0; x < 4; ++x) {
+                        const double sc = w[i][x] * rd;
+                        w[i][x] = sc;
+                        rowj[p][4 * rb + x] = ownR ? sc : 0.0;
+                    }
+                }
+            }
         }
         __syncthreads();
+        if (2 * (t >> 6) + 1 >= jb) {
+            const double2 r01 = *reinterpret_cast<const double2*>(&colj[p][4 * rb]);
+            const double2 r23 = *reinterpret_cast<const double2*>(&colj[p][4 * rb + 2]);
+            const double2 c01 = *reinterpret_cast<const double2*>(&colj[p][4 * cb]);
+            const double2 c23 = *reinterpret_cast<const double2*>(&colj[p][4 * cb + 2]);
+            const double2 w01 = *reinterpret_cast<const double2*>(&rowj[p][4 * rb]);
+            const double2 w23 = *reinterpret_cast<const double2*>(&rowj[p][4 * rb + 2]);
+            const double cr[4] = {r01.x, r01.y, r23.x, r23.y};
+            const double cc[4] = {c01.x, c01.y, c23.x, c23.y};
+            const double rw[4] = {w01.x, w01.y, w23.x, w23.y};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int x = 0; x < 4; ++x) {
+                    a[i][x] -= cr[i] * cc[x];
+                    w[i][x] -= cc[i] * rw[x];
+                }
+        }
     }
-    for (int idx = tid; idx < NB * NB; idx += 1024) {
-        const int rr = idx & (NB - 1), c = idx >> 7;
-        if (rr >= c) Ab[(int64_t)c * lda + rr] = (rr == c) ? dd[c] : S[rr * LS + c] * rdd[c];
-        // Linv(rr, c), column-major with ld NB
-        Linv[c * NB + rr] = (c <= rr) ? S[c * LS + rr + 1] * rdd[rr] : 0.0;
-    }
+    // L block (lower incl. diagonal) back in place; Linv = R (column-major, ld NB).
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = 4 * rb + i, c = 4 * cb + x;
+            if (ownA && r >= c) Ab[(int64_t)c * lda + r] = a[i][x];
+            // R micro-tile (cb, rb): Linv rows 4cb+i, cols 4rb+x; threads with rb > cb
+            // own no R tile and zero the mirrored upper block instead.
+            Linv[(4 * rb + x) * NB + 4 * cb + i] = ownR ? w[i][x] : 0.0;
+        }
 }
 
 // ---------------------------------------------------------------------------------
@@ -208,7 +255,14 @@ __global__ __launch_bounds__(1024) void potrf_diag_kernel(double* __restrict__ A
 // accumulators. Operands are staged through LDS in 16-deep k-chunks, double-buffered
 // with a register prefetch of the next chunk. The MFMA computes D = Q*P^T (the j-side
 // fragment is the A operand) so that a lane's accumulator column is C's row: stores are
-// 128-byte column segments of the column-major matrix.
+// 128-byte column segments of the column-major matrix. In SYRK mode the C tile is loaded
+// straight into the accumulators before the k-loop and P is staged negated, so the MFMA
+// chain produces C - P Q^T and the epilogue is stores only.
+// Tile placement: a precomputed list (tiles) maps blockIdx -> (bi, bj). For the bulk
+// trailing update the list is ordered so that the blocks one XCD runs (blockIdx % 8,
+// dealt round-robin by the dispatcher) walk one contiguous run of 8x8 super-tiles: the
+// P/Q row blocks of its ~64 resident tiles (2 MiB) stay in that XCD's 4 MiB L2.
+// Placement only affects speed; any blockIdx -> tile bijection is correct.
 // ---------------------------------------------------------------------------------
 constexpr int KB = 16;
 constexpr int LR = NB + 16;  // LDS k-row stride: lanes 16..31 land on banks 32..63
@@ -216,7 +270,9 @@ constexpr int LR = NB + 16;  // LDS k-row stride: lanes 16..31 land on banks 32.
 template <int MODE>
 __global__ __launch_bounds__(256, 2) void tile_gemm_kernel(double* __restrict__ A, int64_t lda,
                                                            int k, int jb, int colmode,
-                                                           const double* __restrict__ Linv) {
+                                                           const double* __restrict__ Linv,
+                                                           const uint32_t* __restrict__ tiles,
+                                                           int ntiles) {
     __shared__ double sm[2][2][KB][LR];
     int bi, bj;
     if (MODE == 1) {
@@ -226,9 +282,13 @@ __global__ __launch_bounds__(256, 2) void tile_gemm_kernel(double* __restrict__ 
         bi = jb + (int)blockIdx.x;
         bj = jb;
     } else {
-        tri_index(blockIdx.x, bi, bj);
-        bi += jb;
-        bj += jb;
+        const int b = (int)blockIdx.x;
+        const int chunk = (ntiles + 7) >> 3;
+        const int idx = (b & 7) * chunk + (b >> 3);
+        if (idx >= ntiles) return;
+        const uint32_t tv = tiles[idx];
+        bi = jb + (int)(tv & 0xffffu);
+        bj = jb + (int)(tv >> 16);
     }
     const int64_t r0 = (int64_t)bi * NB, c0 = (int64_t)bj * NB, k0 = (int64_t)k * NB;
     const double* P = A + k0 * lda + r0;
@@ -244,6 +304,25 @@ __global__ __launch_bounds__(256, 2) void tile_gemm_kernel(double* __restrict__ 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wi = w & 1, wj = w >> 1;
     const bool active = !(MODE == 0 && bi == bj && wj > wi);
+    const int fr = lane >> 4, fc = lane & 15;
+
+    d4 acc[4][4];
+    if (MODE == 0 && active) {
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+            const double* Ci = A + c0 * lda + r0 + 64 * wi + 16 * mi + fc;
+#pragma unroll
+            for (int mj = 0; mj < 4; ++mj)
+#pragma unroll
+                for (int rg = 0; rg < 4; ++rg)
+                    acc[mi][mj][rg] = Ci[(int64_t)(64 * wj + 16 * mj + fr + 4 * rg) * lda];
+        }
+    } else {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    }
 
     double2 pp[4], pq[4];
     const int krow = tid >> 6;  // 0..3
@@ -259,22 +338,20 @@ __global__ __launch_bounds__(256, 2) void tile_gemm_kernel(double* __restrict__ 
 #pragma unroll
         for (int it = 0; it < 4; ++it) {
             const int kk = krow + 4 * it;
-            *reinterpret_cast<double2*>(&sm[buf][0][kk][2 * lane]) = pp[it];
+            double2 v = pp[it];
+            if (MODE == 0) {
+                v.x = -v.x;
+                v.y = -v.y;
+            }
+            *reinterpret_cast<double2*>(&sm[buf][0][kk][2 * lane]) = v;
             *reinterpret_cast<double2*>(&sm[buf][1][kk][2 * lane]) = pq[it];
         }
     };
-
-    d4 acc[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
 
     gload(0);
     lstore(0);
     __syncthreads();
     constexpr int NCH = NB / KB;
-    const int fr = lane >> 4, fc = lane & 15;
     for (int ch = 0; ch < NCH; ++ch) {
         const int buf = ch & 1;
         if (ch + 1 < NCH) gload(ch + 1);
@@ -301,19 +378,12 @@ __global__ __launch_bounds__(256, 2) void tile_gemm_kernel(double* __restrict__ 
     if (!active) return;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
-        const int64_t i = r0 + 64 * wi + 16 * mi + fc;
+        double* Ci = A + c0 * lda + r0 + 64 * wi + 16 * mi + fc;
 #pragma unroll
-        for (int mj = 0; mj < 4; ++mj) {
+        for (int mj = 0; mj < 4; ++mj)
 #pragma unroll
-            for (int rg = 0; rg < 4; ++rg) {
-                const int64_t j = c0 + 64 * wj + 16 * mj + fr + 4 * rg;
-                double* p = A + j * lda + i;
-                if (MODE == 0)
-                    *p -= acc[mi][mj][rg];
-                else
-                    *p = acc[mi][mj][rg];
-            }
-        }
+            for (int rg = 0; rg < 4; ++rg)
+                Ci[(int64_t)(64 * wj + 16 * mj + fr + 4 * rg) * lda] = acc[mi][mj][rg];
     }
 }
 
@@ -375,14 +445,31 @@ void launch_potrf_diag(hipStream_t s, double* A, int64_t lda, int64_t N, int k, 
 void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Linv) {
     const int n = nt - k - 1;
     if (n <= 0) return;
-    tile_gemm_kernel<1><<<dim3(n), dim3(256), 0, s>>>(A, lda, k, 0, 0, Linv);
+    tile_gemm_kernel<1><<<dim3(n), dim3(256), 0, s>>>(A, lda, k, 0, 0, Linv, nullptr, 0);
 }
 
-void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int colmode) {
+void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int colmode,
+                 const uint32_t* tiles) {
     const int m = nt - jb;
     if (m <= 0) return;
-    const int64_t n = colmode ? m : (int64_t)m * (m + 1) / 2;
-    tile_gemm_kernel<0><<<dim3((unsigned)n), dim3(256), 0, s>>>(A, lda, k, jb, colmode, nullptr);
+    if (colmode) {
+        tile_gemm_kernel<0><<<dim3((unsigned)m), dim3(256), 0, s>>>(A, lda, k, jb, 1, nullptr, nullptr, 0);
+        return;
+    }
+    const int ntiles = m * (m + 1) / 2;
+    const int grid = ((ntiles + 7) >> 3) << 3;
+    tile_gemm_kernel<0><<<dim3((unsigned)grid), dim3(256), 0, s>>>(A, lda, k, jb, 0, nullptr, tiles, ntiles);
+}
+
+// Super-tile ordered list of the lower-triangular m x m tile set (entry = bi | bj << 16,
+// relative to the first tile block): 8x8 super-tiles, super-rows outer, tiles row-major.
+void build_tile_list(int m, uint32_t* out) {
+    int n = 0;
+    for (int I = 0; I < (m + 7) / 8; ++I)
+        for (int J = 0; J <= I; ++J)
+            for (int i = 8 * I; i < 8 * I + 8 && i < m; ++i)
+                for (int j = 8 * J; j < 8 * J + 8 && j <= i; ++j)
+                    out[n++] = (uint32_t)i | ((uint32_t)j << 16);
 }
 
 void launch_reduce(hipStream_t s, const double* A, int64_t lda, int64_t N, EvalResult* res) {

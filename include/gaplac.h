@@ -137,7 +137,8 @@ typedef struct gaplac_stats {
     double  gram_ms;
     double  gram_bytes;         /* algorithmic bytes of the Gram launches */
     int64_t gram_launches;
-    double  panel_ms;           /* diag potrf + panel trsm, summed */
+    double  panel_ms;           /* diagonal-block potrf launches, summed */
+    double  trsm_ms;            /* panel TRSM launches, summed */
     double  total_ms;           /* whole evaluation, first kernel to result */
 } gaplac_stats;
 int gaplac_set_profiling(gaplac_ctx* ctx, int on);
