@@ -137,114 +137,215 @@ __global__ __launch_bounds__(256) void gram_kernel(double* __restrict__ A, int64
 }
 
 // ---------------------------------------------------------------------------------
-// Diagonal block: right-looking Cholesky of the 128x128 block fused with the forward
-// elimination that yields Linv = L_kk^{-1} (used to turn the panel TRSM into an MFMA
-// GEMM). Runs alone on CUs reserved for it (CU-masked stream, gaplac_api.hip).
-// Register-resident: 1024 threads = a 32 x 32 grid of 4x4 micro-tiles, t = cb*32 + rb:
-//   rb >= cb : A micro-tile (rb, cb)                    (a[][])
-//   cb >= rb : R micro-tile (cb, rb) of the RHS, R0 = I  (w[][]); after the elimination
-//              row j of R scaled by 1/L_jj is row j of L^{-1}.
-// Wave w holds column blocks 2w and 2w+1, so every owner of column j (and of row j of R)
-// sits in wave (j/4)/2 and a wave whose column blocks are finished stops computing.
-// Column j: the owning wave takes the pivot (sqrt, 1/d, LAPACK dpotf2's scaling), scales
-// column j and R's row j and publishes both, zero-padded, in a double-buffered LDS
-// vector; one barrier; every active wave applies the rank-1 update unconditionally
-// (the zero padding masks finished rows/columns). Pivots of padding columns (>= N) are
-// forced to 1; a failing pivot (<= 0 or NaN) records info = j+1.
+// Diagonal block: Cholesky of the 128x128 block k and its inverse Linv = L_kk^{-1}
+// (Linv turns the panel TRSM into an MFMA GEMM). One workgroup of 8 waves on CUs
+// reserved for it (CU-masked stream, gaplac_api.hip); the whole block lives in LDS as an
+// 8x8 grid of 16x16 blocks (lower triangle packed, 36 blocks each for L and Linv).
+//
+// Blocked right-looking with 16-column panels, 2 barriers per panel s = 0..7:
+//   phase 1: waves 0..7-s apply panel s-1 to the tiles of block column s (one
+//            v_mfma_f64_16x16x4f64 chain of K = 16 each); wave 7 inverts the diagonal
+//            block s-1 (16x16 forward substitution).
+//   phase 2: wave 0 factors panel s (rows 16s..127 x 16 columns) in registers: two rows
+//            per lane, pivots and L values broadcast by v_readlane, LAPACK dpotf2's
+//            sqrt + reciprocal scaling, no barriers; waves 1..7 apply panel s-1 to the
+//            remaining trailing tiles and compute Linv block row s-1,
+//            Linv_sj = -Linv_ss * sum_{k=j}^{s-1} L_sk Linv_kj, on MFMA.
+// Layouts: L blocks column-major (16 rows contiguous), Linv blocks row-major: every MFMA
+// operand read is 16 contiguous doubles per lane group, and the f64 MFMA accumulator
+// (row = lane/16 + 4q, col = lane%16) feeds the next MFMA as its B operand directly.
+// Pivots of padding columns (>= N) are forced to 1; a pivot <= 0 records info = j+1
+// (OpenBLAS potf2's test; NaN pivots propagate, as in the reference).
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
+constexpr int DB = 16;                 // sub-block edge
+constexpr int NDB = NB / DB;           // 8
+constexpr int NPK = NDB * (NDB + 1) / 2;  // 36 packed blocks
+
+__device__ __forceinline__ int bidx(int I, int J) { return I * (I + 1) / 2 + J; }
+
+__device__ __forceinline__ double readlane_d(double x, int l) {
+    const long long v = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readlane((int)(v & 0xffffffffll), l);
+    const int hi = __builtin_amdgcn_readlane((int)(v >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// C_IJ -= L_Ik * L_Jk^T (all three column-major 16x16 blocks in Ab).
+__device__ __forceinline__ void dblk_update(double* Ab, int I, int J, int k, int lane) {
+    double* C = Ab + bidx(I, J) * 256;
+    const double* LI = Ab + bidx(I, k) * 256;
+    const double* LJ = Ab + bidx(J, k) * 256;
+    const int fr = lane >> 4, fc = lane & 15;
+    d4 acc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = C[(fr + 4 * q) * 16 + fc];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-LJ[(4 * kk + fr) * 16 + fc], LI[(4 * kk + fr) * 16 + fc],
+                                                   acc, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) C[(fr + 4 * q) * 16 + fc] = acc[q];
+}
+
+// Linv_ss = L_ss^{-1} (row-major into Lb), 16 lanes each one column, fully unrolled.
+__device__ __forceinline__ void dinv_diag(const double* Ab, double* Lb, const double* rdiag, int s,
+                                          int lane) {
+    const double* Ls = Ab + bidx(s, s) * 256;
+    const int c = lane & 15;
+    double x[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        double acc = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+        for (int m = 0; m < r; ++m) acc -= Ls[m * 16 + r] * x[m];
+        x[r] = (r >= c) ? acc * rdiag[16 * s + r] : 0.0;
+    }
+    if (lane < 16) {
+        double* out = Lb + bidx(s, s) * 256;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) out[r * 16 + c] = x[r];
+    }
+}
+
+// Linv_sj = -Linv_ss * sum_{k=j}^{s-1} L_sk * Linv_kj   (j < s)
+__device__ __forceinline__ void dinv_offdiag(const double* Ab, double* Lb, int s, int j, int lane) {
+    const int fr = lane >> 4, fc = lane & 15;
+    d4 t0 = {0.0, 0.0, 0.0, 0.0}, t1 = {0.0, 0.0, 0.0, 0.0};
+    for (int k = j; k < s; ++k) {
+        const double* Lsk = Ab + bidx(s, k) * 256;  // column-major: A operand [row fc][k]
+        const double* Ikj = Lb + bidx(k, j) * 256;  // row-major:    B operand [k][col fc]
+        d4 acc = (k - j) & 1 ? t1 : t0;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Lsk[(4 * kk + fr) * 16 + fc], Ikj[(4 * kk + fr) * 16 + fc],
+                                                       acc, 0, 0, 0);
+        if ((k - j) & 1)
+            t1 = acc;
+        else
+            t0 = acc;
+    }
+    const d4 T = t0 + t1;
+    const double* Iss = Lb + bidx(s, s) * 256;  // row-major: A operand [row fc][k]
+    d4 o = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+        o = __builtin_amdgcn_mfma_f64_16x16x4f64(-Iss[fc * 16 + 4 * kk + fr], T[kk], o, 0, 0, 0);
+    double* out = Lb + bidx(s, j) * 256;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[(fr + 4 * q) * 16 + fc] = o[q];
+}
+
+// Wave-level factorisation of panel s: rows 16s..127 x 16 columns, two rows per lane.
+__device__ __forceinline__ void dpanel(double* Ab, double* rdiag, int s, int lane, int64_t gcol0,
+                                       int64_t N, EvalResult* res) {
+    const int R0 = 16 * s;
+    const int rel0 = 2 * lane, rel1 = rel0 + 1;
+    const int row0 = R0 + rel0;
+    const bool live = row0 < NB;
+    double v0[16], v1[16];
+    double* blk = Ab + (live ? bidx(row0 >> 4, s) * 256 : 0);
+    const int rr = row0 & 15;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        v0[c] = live ? blk[c * 16 + rr] : 0.0;
+        v1[c] = live ? blk[c * 16 + rr + 1] : 0.0;
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const double piv = readlane_d((c & 1) ? v1[c] : v0[c], c >> 1);
+        double d, rd;
+        if (gcol0 + R0 + c >= N) {
+            d = 1.0;
+            rd = 1.0;
+        } else {
+            // OpenBLAS potf2 (the reference's dpotrf, 0.3.20) tests ajj <= 0 only: a NaN
+            // pivot is not reported and propagates to a NaN logpdf, as in the reference.
+            if (lane == 0 && piv <= 0.0)
+                atomicMin(&res->info, (unsigned long long)(gcol0 + R0 + c + 1));
+            d = sqrt(piv);
+            rd = 1.0 / d;
+        }
+        if (lane == 0) rdiag[R0 + c] = rd;
+        v0[c] = rel0 > c ? v0[c] * rd : (rel0 == c ? d : v0[c]);
+        v1[c] = rel1 > c ? v1[c] * rd : (rel1 == c ? d : v1[c]);
+#pragma unroll
+        for (int c2 = c + 1; c2 < 16; ++c2) {
+            const double lc = readlane_d((c2 & 1) ? v1[c] : v0[c], c2 >> 1);  // L[R0+c2][c]
+            v0[c2] -= v0[c] * lc;
+            v1[c2] -= v1[c] * lc;
+        }
+    }
+    if (live) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            blk[c * 16 + rr] = (rel0 >= c) ? v0[c] : 0.0;  // zero the diagonal block's upper part
+            blk[c * 16 + rr + 1] = (rel1 >= c) ? v1[c] : 0.0;
+        }
+    }
+}
+
+__global__ __launch_bounds__(512) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
                                                           int64_t N, int k,
                                                           double* __restrict__ Linv,
                                                           EvalResult* __restrict__ res) {
-    __shared__ double colj[2][NB];
-    __shared__ double rowj[2][NB];
-    const int t = threadIdx.x;
-    const int cb = t >> 5, rb = t & 31, lane = t & 63;
-    const bool ownA = rb >= cb, ownR = cb >= rb;
+    __shared__ double Ab[NPK * 256];
+    __shared__ double Lb[NPK * 256];
+    __shared__ double rdiag[NB];
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const int64_t g0 = (int64_t)k * NB;
-    double* Ab = A + g0 * lda + g0;
-    double a[4][4], w[4][4];
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            a[i][x] = ownA ? Ab[(int64_t)(4 * cb + x) * lda + 4 * rb + i] : 0.0;
-            w[i][x] = (rb == cb && i == x) ? 1.0 : 0.0;
+    double* Ag = A + g0 * lda + g0;
+    // load the lower block triangle: element (r, c) of block (I, J) <- A(16I+r, 16J+c)
+    for (int idx = t; idx < NPK * 256; idx += 512) {
+        const int b = idx >> 8, e = idx & 255, c = e >> 4, r = e & 15;
+        int I = 0;
+        while ((I + 1) * (I + 2) / 2 <= b) ++I;
+        const int J = b - I * (I + 1) / 2;
+        Ab[idx] = Ag[(int64_t)(16 * J + c) * lda + 16 * I + r];
+    }
+    __syncthreads();
+    for (int s = 0; s < NDB; ++s) {
+        if (s >= 1) {
+            if (wave < NDB - s) dblk_update(Ab, s + wave, s, s - 1, lane);
+            if (wave == 7) dinv_diag(Ab, Lb, rdiag, s - 1, lane);
         }
-    for (int j = 0; j < NB; ++j) {
-        const int jb = j >> 2, jj = j & 3, p = j & 1;
-        if ((t >> 6) == (jb >> 1)) {  // the wave owning column j: pivot, scale, publish
-            const int plane = (jb & 1) * 32 + jb;
-            double piv = 0.0;
-#pragma unroll
-            for (int x = 0; x < 4; ++x)
-                if (x == jj) piv = a[x][x];
-            piv = __shfl(piv, plane);
-            double d, rd;
-            if (g0 + j >= N) {
-                d = 1.0;
-                rd = 1.0;
-            } else {
-                if (lane == plane && !(piv > 0.0))
-                    atomicMin(&res->info, (unsigned long long)(g0 + j + 1));
-                d = sqrt(piv);
-                rd = 1.0 / d;
-            }
-            if (cb == jb) {
-#pragma unroll
-                for (int x = 0; x < 4; ++x) {
-                    if (x != jj) continue;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int r = 4 * rb + i;
-                        const double sc = a[i][x] * rd;
-                        colj[p][r] = (r > j) ? sc : 0.0;
-                        a[i][x] = (r > j) ? sc : ((r == j) ? d : a[i][x]);
+        __syncthreads();
+        if (wave == 0) {
+            dpanel(Ab, rdiag, s, lane, g0, N, res);
+        } else if (s >= 1) {
+            const int ntr = (NDB - 1 - s) * (NDB - s) / 2;  // tiles (I,J), s+1 <= J <= I <= 7
+            const int nli = s >= 2 ? s - 1 : 0;              // Linv row s-1, blocks j < s-1
+            for (int task = wave - 1; task < ntr + nli; task += 7) {
+                if (task < ntr) {
+                    int J = s + 1, rem = task;
+                    while (rem >= NDB - J) {
+                        rem -= NDB - J;
+                        ++J;
                     }
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (i != jj) continue;
-#pragma unroll
-                    for (int x = 0; x < 4; ++x) {
-                        const double sc = w[i][x] * rd;
-                        w[i][x] = sc;
-                        rowj[p][4 * rb + x] = ownR ? sc : 0.0;
-                    }
+                    dblk_update(Ab, J + rem, J, s - 1, lane);
+                } else {
+                    dinv_offdiag(Ab, Lb, s - 1, task - ntr, lane);
                 }
             }
         }
         __syncthreads();
-        if (2 * (t >> 6) + 1 >= jb) {
-            const double2 r01 = *reinterpret_cast<const double2*>(&colj[p][4 * rb]);
-            const double2 r23 = *reinterpret_cast<const double2*>(&colj[p][4 * rb + 2]);
-            const double2 c01 = *reinterpret_cast<const double2*>(&colj[p][4 * cb]);
-            const double2 c23 = *reinterpret_cast<const double2*>(&colj[p][4 * cb + 2]);
-            const double2 w01 = *reinterpret_cast<const double2*>(&rowj[p][4 * rb]);
-            const double2 w23 = *reinterpret_cast<const double2*>(&rowj[p][4 * rb + 2]);
-            const double cr[4] = {r01.x, r01.y, r23.x, r23.y};
-            const double cc[4] = {c01.x, c01.y, c23.x, c23.y};
-            const double rw[4] = {w01.x, w01.y, w23.x, w23.y};
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int x = 0; x < 4; ++x) {
-                    a[i][x] -= cr[i] * cc[x];
-                    w[i][x] -= cc[i] * rw[x];
-                }
+    }
+    if (wave == 7) dinv_diag(Ab, Lb, rdiag, NDB - 1, lane);
+    if (wave >= 1 && wave < NDB - 1) dinv_offdiag(Ab, Lb, NDB - 2, wave - 1, lane);  // row 6, j < 6
+    __syncthreads();
+    if (wave >= 1 && wave < NDB) dinv_offdiag(Ab, Lb, NDB - 1, wave - 1, lane);  // row 7, j < 7
+    __syncthreads();
+    // write L (lower incl. diagonal) in place and Linv (column-major, ld NB, zero upper)
+    for (int idx = t; idx < NB * NB; idx += 512) {
+        const int r = idx & (NB - 1), c = idx >> 7;
+        const int I = r >> 4, J = c >> 4;
+        if (J <= I) {
+            const int b = bidx(I, J) * 256;
+            if (r >= c) Ag[(int64_t)c * lda + r] = Ab[b + (c & 15) * 16 + (r & 15)];
+            Linv[c * NB + r] = Lb[b + (r & 15) * 16 + (c & 15)];
+        } else {
+            Linv[c * NB + r] = 0.0;
         }
     }
-    // L block (lower incl. diagonal) back in place; Linv = R (column-major, ld NB).
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int r = 4 * rb + i, c = 4 * cb + x;
-            if (ownA && r >= c) Ab[(int64_t)c * lda + r] = a[i][x];
-            // R micro-tile (cb, rb): Linv rows 4cb+i, cols 4rb+x; threads with rb > cb
-            // own no R tile and zero the mirrored upper block instead.
-            Linv[(4 * rb + x) * NB + 4 * cb + i] = ownR ? w[i][x] : 0.0;
-        }
 }
 
 // ---------------------------------------------------------------------------------
@@ -439,7 +540,7 @@ void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const
 
 void launch_potrf_diag(hipStream_t s, double* A, int64_t lda, int64_t N, int k, double* Linv,
                        EvalResult* res) {
-    potrf_diag_kernel<<<dim3(1), dim3(1024), 0, s>>>(A, lda, N, k, Linv, res);
+    potrf_diag_kernel<<<dim3(1), dim3(512), 0, s>>>(A, lda, N, k, Linv, res);
 }
 
 void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Linv) {
