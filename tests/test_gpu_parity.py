@@ -146,7 +146,7 @@ def test_batch_matches_individual(ctx):
     for m, lp in zip(models, out):
         assert rel(lp, R.logpdf(X, m, 0.1, v)[0]) <= RTOL
     # a non-PD model inside a batch reports its own info and does not poison the others
-    out, info = ctx.logpdf_batch(X, [[(CAT, 1, 0.0, 0)], [(SQEXP, 0, 1.0, 0)]], 0.0, v)
+    out, info = ctx.logpdf_batch(X, [[(CAT, 1, 0.0, 0)], [(SQEXP, 0, 1.0, 0), (NOISE, -1, 0.1, 1)]], 0.0, v)
     assert info[0] > 0 and np.isnan(out[0]) and info[1] == 0 and np.isfinite(out[1])
 
 
