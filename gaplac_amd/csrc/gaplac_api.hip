@@ -6,9 +6,7 @@
 //   s_main : gram | wait(P0) syrk_tri(2..) rec(R0) | wait(P1) syrk_tri(3..) rec(R1) | ...
 //   s_panel:        potrf(0) trsm(0) rec(P0) | syrk_col(1) potrf(1) trsm(1) rec(P1) |
 //                   wait(R0) syrk_col(2) potrf(2) trsm(2) rec(P2) | ...
-//
-// The panel stream has the device's highest priority so the lookahead panel k+1
-// (critical path) overlaps the bulk trailing update of step k.
+// (details at factor_and_reduce)
 #include "gaplac_internal.h"
 
 #include <cmath>
@@ -23,8 +21,8 @@ using namespace gaplac;
 
 struct gaplac_ctx {
     int device = 0;
-    hipStream_t s_main = nullptr, s_panel = nullptr, s_diag = nullptr;
-    int diag_cus = 0;  // CUs reserved for s_diag (0: CU masks unavailable)
+    hipStream_t s_main = nullptr, s_panel = nullptr;
+    int diag_cus = 0;  // CUs masked out of s_main for the diagonal kernel (0: no mask)
     hipEvent_t ev_P[2] = {}, ev_R[2] = {}, ev_C[2] = {}, ev_D[2] = {}, ev_gram = nullptr;
     double* A = nullptr;
     size_t A_elems = 0;
@@ -236,29 +234,28 @@ void collect_spans(gaplac_ctx* ctx) {
 
 // Factor the augmented matrix already built in ctx->A (Gram launched on s_main).
 //
-// Three streams: s_main (bulk trailing updates), s_panel (lookahead column update and
-// panel TRSM) and s_diag (the 128x128 diagonal factorisations, on CUs reserved for it by
-// a CU mask so the one-workgroup critical-path kernel never queues behind trailing-update
-// workgroups). Step k, panel k factored and solved:
-//   s_panel: wait R(k-1) | syrk_col(k+1) with panel k | rec C(k+1)
-//   s_diag : wait C(k+1) | potrf(k+1)                  | rec D(k+1)
-//   s_panel: wait D(k+1) | trsm(k+1)                   | rec P(k+1)
-//   s_main : wait P(k)   | syrk_tri(columns >= k+2) with panel k | rec R(k)
+// Two streams. s_panel (highest priority, all CUs) runs the critical path in order:
+// the lookahead column update, the 128x128 diagonal factorisation and the panel TRSM.
+// s_main (CU-masked: GAPLAC_DIAG_CUS CUs, default 1, excluded) runs the bulk trailing
+// updates. The excluded CU(s) never hold trailing-update workgroups, and the diagonal
+// kernel starts only after its own stream predecessors finished, so it always finds a
+// free CU (without this it starved ~600 us per step behind trailing-update workgroups).
+// Keeping the whole chain on one stream avoids cross-stream event hops inside it
+// (~25 us each, measured). Step k (panel k factored and solved):
+//   s_panel: wait R(k-1) | syrk_col(k+1) with panel k | potrf(k+1) | trsm(k+1) | rec P(k+1)
+//   s_main : wait P(k)   | syrk_tri(tile columns >= k+2) with panel k          | rec R(k)
 // Column k+1 receives panel k-1's update in R(k-1) and panel k's in syrk_col(k+1); within
 // a step the streams touch disjoint tile columns. Events ping-pong (k & 1) so a record
 // never overtakes a wait that still refers to the previous step.
 int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     hipStream_t sm = ctx->s_main;
     hipStream_t sp = ctx->serial ? sm : ctx->s_panel;
-    hipStream_t sd = ctx->serial ? sm : ctx->s_diag;
     HIPCK(ctx, hipEventRecord(ctx->ev_gram, sm));
-    HIPCK(ctx, hipStreamWaitEvent(sd, ctx->ev_gram, 0));
+    HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_gram, 0));
     {
-        SpanGuard g(ctx, sd, 2, 0);
-        launch_potrf_diag(sd, ctx->A, lda, N, 0, ctx->Linv, ctx->dres);
+        SpanGuard g(ctx, sp, 2, 0);
+        launch_potrf_diag(sp, ctx->A, lda, N, 0, ctx->Linv, ctx->dres);
     }
-    HIPCK(ctx, hipEventRecord(ctx->ev_D[0], sd));
-    HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_D[0], 0));
     {
         SpanGuard g(ctx, sp, 4, 0);
         launch_trsm(sp, ctx->A, lda, nt, 0, ctx->Linv);
@@ -266,26 +263,21 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     HIPCK(ctx, hipEventRecord(ctx->ev_P[0], sp));
     for (int k = 0; k < nt; ++k) {
         if (k + 1 < nt) {
-            const int q = (k + 1) & 1;
             if (k >= 1) HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_R[(k - 1) & 1], 0));
             {
                 SpanGuard g(ctx, sp, 0, syrk_flops(nt - (k + 1), 1));
                 launch_syrk(sp, ctx->A, lda, nt, k, k + 1, 1, nullptr);
             }
-            HIPCK(ctx, hipEventRecord(ctx->ev_C[q], sp));
             double* Lk = ctx->Linv + (size_t)(k + 1) * NB * NB;
-            HIPCK(ctx, hipStreamWaitEvent(sd, ctx->ev_C[q], 0));
             if ((int64_t)(k + 1) * NB < N) {
-                SpanGuard g(ctx, sd, 2, 0);
-                launch_potrf_diag(sd, ctx->A, lda, N, k + 1, Lk, ctx->dres);
+                SpanGuard g(ctx, sp, 2, 0);
+                launch_potrf_diag(sp, ctx->A, lda, N, k + 1, Lk, ctx->dres);
             }
-            HIPCK(ctx, hipEventRecord(ctx->ev_D[q], sd));
-            HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_D[q], 0));
             {
                 SpanGuard g(ctx, sp, 4, 0);
                 launch_trsm(sp, ctx->A, lda, nt, k + 1, Lk);
             }
-            HIPCK(ctx, hipEventRecord(ctx->ev_P[q], sp));
+            HIPCK(ctx, hipEventRecord(ctx->ev_P[(k + 1) & 1], sp));
         }
         HIPCK(ctx, hipStreamWaitEvent(sm, ctx->ev_P[k & 1], 0));
         if (k + 2 < nt) {
@@ -406,42 +398,31 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     };
     hipError_t e;
     if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
-    // Reserve GAPLAC_DIAG_CUS (default 1) CUs for the diagonal factorisation stream and
-    // mask them out of the other two; fall back to stream priorities without CU masks.
+    // s_panel: highest priority, all CUs. s_main: GAPLAC_DIAG_CUS (default 1) CUs masked
+    // out so the critical-path diagonal kernel always finds a free CU; if CU masks are
+    // unavailable, s_main falls back to the lowest priority without a mask.
     int ncu = 0;
     if ((e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
         return fail("attribute", e);
+    int least = 0, greatest = 0;
+    if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess)
+        return fail("priority range", e);
+    if ((e = hipStreamCreateWithPriority(&ctx->s_panel, hipStreamNonBlocking, greatest)) != hipSuccess)
+        return fail("stream", e);
     int want = 1;
     if (const char* s = std::getenv("GAPLAC_DIAG_CUS")) want = std::atoi(s);
-    bool masked = false;
     if (want > 0 && ncu > 2 * want) {
         const int words = (ncu + 31) / 32;
-        std::vector<uint32_t> rest((size_t)words, 0u), diag((size_t)words, 0u);
-        for (int c = 0; c < ncu; ++c) {
-            if (c < want) diag[(size_t)c / 32] |= 1u << (c % 32);
-            else rest[(size_t)c / 32] |= 1u << (c % 32);
-        }
-        masked = hipExtStreamCreateWithCUMask(&ctx->s_main, (uint32_t)words, rest.data()) == hipSuccess &&
-                 hipExtStreamCreateWithCUMask(&ctx->s_panel, (uint32_t)words, rest.data()) == hipSuccess &&
-                 hipExtStreamCreateWithCUMask(&ctx->s_diag, (uint32_t)words, diag.data()) == hipSuccess;
-        if (masked) ctx->diag_cus = want;
+        std::vector<uint32_t> rest((size_t)words, 0u);
+        for (int c = want; c < ncu; ++c) rest[(size_t)c / 32] |= 1u << (c % 32);
+        if (hipExtStreamCreateWithCUMask(&ctx->s_main, (uint32_t)words, rest.data()) == hipSuccess)
+            ctx->diag_cus = want;
+        else
+            ctx->s_main = nullptr;
     }
-    if (!masked) {
-        for (hipStream_t* s : {&ctx->s_main, &ctx->s_panel, &ctx->s_diag})
-            if (*s) {
-                (void)hipStreamDestroy(*s);
-                *s = nullptr;
-            }
-        int least = 0, greatest = 0;
-        if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess)
-            return fail("priority range", e);
-        if ((e = hipStreamCreateWithPriority(&ctx->s_main, hipStreamNonBlocking, least)) != hipSuccess)
-            return fail("stream", e);
-        if ((e = hipStreamCreateWithPriority(&ctx->s_panel, hipStreamNonBlocking, greatest)) != hipSuccess)
-            return fail("stream", e);
-        if ((e = hipStreamCreateWithPriority(&ctx->s_diag, hipStreamNonBlocking, greatest)) != hipSuccess)
-            return fail("stream", e);
-    }
+    if (!ctx->s_main &&
+        (e = hipStreamCreateWithPriority(&ctx->s_main, hipStreamNonBlocking, least)) != hipSuccess)
+        return fail("stream", e);
     for (int q = 0; q < 2; ++q) {
         if ((e = hipEventCreateWithFlags(&ctx->ev_P[q], hipEventDisableTiming)) != hipSuccess)
             return fail("event", e);
@@ -467,7 +448,6 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->s_main) (void)hipStreamSynchronize(ctx->s_main);
     if (ctx->s_panel) (void)hipStreamSynchronize(ctx->s_panel);
-    if (ctx->s_diag) (void)hipStreamSynchronize(ctx->s_diag);
     for (auto e : ctx->evpool) (void)hipEventDestroy(e);
     for (int q = 0; q < 2; ++q) {
         if (ctx->ev_P[q]) (void)hipEventDestroy(ctx->ev_P[q]);
@@ -485,7 +465,6 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     if (ctx->hres) (void)hipHostFree(ctx->hres);
     if (ctx->s_main) (void)hipStreamDestroy(ctx->s_main);
     if (ctx->s_panel) (void)hipStreamDestroy(ctx->s_panel);
-    if (ctx->s_diag) (void)hipStreamDestroy(ctx->s_diag);
     delete ctx;
     return 0;
 }
