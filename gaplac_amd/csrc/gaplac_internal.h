@@ -11,14 +11,17 @@ namespace gaplac {
 // kernels work on (Gram tiles, diagonal blocks, trailing-update tiles). 128 fp64 x 128 =
 // 128 KiB: a diagonal block (plus its inverse, packed) fits one CU's 160 KiB LDS.
 constexpr int NB = 128;
+constexpr int DINV_PER_BLOCK = 8 * 16 * 16;  // Dinv doubles per diagonal block
 
-// Term descriptor in kernel-argument form (passed by value, lands in SGPRs).
+// Term descriptor as the Gram kernel reads it (device memory, one small H2D copy per
+// evaluation, so a captured graph replays with new hyperparameters).
 struct TermPack {
     int32_t T;
     int32_t kind[GAPLAC_MAX_TERMS];
     int32_t col[GAPLAC_MAX_TERMS];
     int32_t last_in_group[GAPLAC_MAX_TERMS];
     double  p[GAPLAC_MAX_TERMS];  // 1/l for SQEXP/OU, c for LINEAR, variance for NOISE
+    double  noise;                 // FiniteGP observation variance (diagonal)
 };
 
 // Device-side result record of one evaluation.
@@ -32,12 +35,13 @@ struct EvalResult {
 // Launchers (gaplac_kernels.hip). A is the Np x Np column-major augmented matrix
 // (lda = Np, Np = roundup(N+1, NB)): rows/cols 0..N-1 hold C, row N holds v^T.
 void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt,
-                 const double* X, int64_t ldx, const double* v, const TermPack& tp,
-                 double noise);
+                 const double* X, int64_t ldx, const double* v, const TermPack* dtp);
+// Diagonal block k: L_kk in place + Dinv (DINV_ELEMS doubles: 8 column-major 16x16
+// inverses of L_kk's diagonal sub-blocks).
 void launch_potrf_diag(hipStream_t s, double* A, int64_t lda, int64_t N, int k,
-                       double* Linv, EvalResult* res);
-// TRSM of the panel rows below diagonal block k: A[i,k] <- A[i,k] * Linv_k^T, i>k.
-void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Linv);
+                       double* Dinv, EvalResult* res);
+// TRSM of the panel rows below diagonal block k: A[i,k] <- A[i,k] * L_kk^{-T}, i>k.
+void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Dinv);
 // Trailing update with panel k. colmode=1: only tile column jb (tiles i>=jb);
 // colmode=0: lower triangle of tile blocks jb..nt-1.
 // tiles: super-tile ordered list for the m x m triangle, m = nt - jb (build_tile_list).

@@ -44,7 +44,9 @@ __device__ __forceinline__ void tri_index(int64_t t, int& bi, int& bj) {
 __global__ __launch_bounds__(256) void gram_kernel(double* __restrict__ A, int64_t lda,
                                                    int64_t N, const double* __restrict__ X,
                                                    int64_t ldx, const double* __restrict__ v,
-                                                   TermPack tp, double noise) {
+                                                   const TermPack* __restrict__ tpp) {
+    const TermPack& tp = *tpp;  // uniform: scalar loads (device copy refreshed per eval)
+    const double noise = tp.noise;
     int bi, bj;
     tri_index(blockIdx.x, bi, bj);
     const int64_t r0 = (int64_t)bi * NB, c0 = (int64_t)bj * NB;
@@ -137,29 +139,27 @@ __global__ __launch_bounds__(256) void gram_kernel(double* __restrict__ A, int64
 }
 
 // ---------------------------------------------------------------------------------
-// Diagonal block: Cholesky of the 128x128 block k and its inverse Linv = L_kk^{-1}
-// (Linv turns the panel TRSM into an MFMA GEMM). One workgroup of 8 waves on CUs
-// reserved for it (CU-masked stream, gaplac_api.hip); the whole block lives in LDS as an
-// 8x8 grid of 16x16 blocks (lower triangle packed, 36 blocks each for L and Linv).
+// Diagonal block: Cholesky of the 128x128 block k, plus the inverses of its eight 16x16
+// diagonal sub-blocks (Dinv, consumed by the panel TRSM's blocked substitution).
+// One 256-thread workgroup using 73 KiB of LDS: the same footprint as a trailing-update
+// workgroup, so it can take any free slot next to them. The block lives in LDS as the
+// lower triangle of an 8x8 grid of 16x16 column-major blocks (36 packed blocks).
 //
 // Blocked right-looking with 16-column panels, 2 barriers per panel s = 0..7:
-//   phase 1: waves 0..7-s apply panel s-1 to the tiles of block column s (one
-//            v_mfma_f64_16x16x4f64 chain of K = 16 each); wave 7 inverts the diagonal
-//            block s-1 (16x16 forward substitution).
+//   phase 1: the four waves apply panel s-1 to the 8-s tiles of block column s
+//            (one v_mfma_f64_16x16x4f64 chain of K = 16 each); wave 3 also inverts
+//            diagonal sub-block s-1 into Dinv.
 //   phase 2: wave 0 factors panel s (rows 16s..127 x 16 columns) in registers: two rows
 //            per lane, pivots and L values broadcast by v_readlane, LAPACK dpotf2's
-//            sqrt + reciprocal scaling, no barriers; waves 1..7 apply panel s-1 to the
-//            remaining trailing tiles and compute Linv block row s-1,
-//            Linv_sj = -Linv_ss * sum_{k=j}^{s-1} L_sk Linv_kj, on MFMA.
-// Layouts: L blocks column-major (16 rows contiguous), Linv blocks row-major: every MFMA
-// operand read is 16 contiguous doubles per lane group, and the f64 MFMA accumulator
-// (row = lane/16 + 4q, col = lane%16) feeds the next MFMA as its B operand directly.
+//            sqrt + reciprocal scaling, no barriers; waves 1..3 apply panel s-1 to the
+//            remaining trailing tiles on MFMA.
 // Pivots of padding columns (>= N) are forced to 1; a pivot <= 0 records info = j+1
 // (OpenBLAS potf2's test; NaN pivots propagate, as in the reference).
 // ---------------------------------------------------------------------------------
-constexpr int DB = 16;                 // sub-block edge
-constexpr int NDB = NB / DB;           // 8
+constexpr int DB = 16;                    // sub-block edge
+constexpr int NDB = NB / DB;              // 8
 constexpr int NPK = NDB * (NDB + 1) / 2;  // 36 packed blocks
+constexpr int DINV_ELEMS = NDB * DB * DB; // per diagonal block: 8 column-major 16x16 inverses
 
 __device__ __forceinline__ int bidx(int I, int J) { return I * (I + 1) / 2 + J; }
 
@@ -187,9 +187,9 @@ __device__ __forceinline__ void dblk_update(double* Ab, int I, int J, int k, int
     for (int q = 0; q < 4; ++q) C[(fr + 4 * q) * 16 + fc] = acc[q];
 }
 
-// Linv_ss = L_ss^{-1} (row-major into Lb), 16 lanes each one column, fully unrolled.
-__device__ __forceinline__ void dinv_diag(const double* Ab, double* Lb, const double* rdiag, int s,
-                                          int lane) {
+// Dinv_s = L_ss^{-1} (column-major 16x16 into global), 16 lanes each one column.
+__device__ __forceinline__ void dinv_diag(const double* Ab, double* __restrict__ Dinv,
+                                          const double* rdiag, int s, int lane) {
     const double* Ls = Ab + bidx(s, s) * 256;
     const int c = lane & 15;
     double x[16];
@@ -201,38 +201,10 @@ __device__ __forceinline__ void dinv_diag(const double* Ab, double* Lb, const do
         x[r] = (r >= c) ? acc * rdiag[16 * s + r] : 0.0;
     }
     if (lane < 16) {
-        double* out = Lb + bidx(s, s) * 256;
+        double* out = Dinv + s * 256;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) out[r * 16 + c] = x[r];
+        for (int r = 0; r < 16; ++r) out[c * 16 + r] = x[r];
     }
-}
-
-// Linv_sj = -Linv_ss * sum_{k=j}^{s-1} L_sk * Linv_kj   (j < s)
-__device__ __forceinline__ void dinv_offdiag(const double* Ab, double* Lb, int s, int j, int lane) {
-    const int fr = lane >> 4, fc = lane & 15;
-    d4 t0 = {0.0, 0.0, 0.0, 0.0}, t1 = {0.0, 0.0, 0.0, 0.0};
-    for (int k = j; k < s; ++k) {
-        const double* Lsk = Ab + bidx(s, k) * 256;  // column-major: A operand [row fc][k]
-        const double* Ikj = Lb + bidx(k, j) * 256;  // row-major:    B operand [k][col fc]
-        d4 acc = (k - j) & 1 ? t1 : t0;
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Lsk[(4 * kk + fr) * 16 + fc], Ikj[(4 * kk + fr) * 16 + fc],
-                                                       acc, 0, 0, 0);
-        if ((k - j) & 1)
-            t1 = acc;
-        else
-            t0 = acc;
-    }
-    const d4 T = t0 + t1;
-    const double* Iss = Lb + bidx(s, s) * 256;  // row-major: A operand [row fc][k]
-    d4 o = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-        o = __builtin_amdgcn_mfma_f64_16x16x4f64(-Iss[fc * 16 + 4 * kk + fr], T[kk], o, 0, 0, 0);
-    double* out = Lb + bidx(s, j) * 256;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) out[(fr + 4 * q) * 16 + fc] = o[q];
 }
 
 // Wave-level factorisation of panel s: rows 16s..127 x 16 columns, two rows per lane.
@@ -284,18 +256,17 @@ __device__ __forceinline__ void dpanel(double* Ab, double* rdiag, int s, int lan
     }
 }
 
-__global__ __launch_bounds__(512) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
-                                                          int64_t N, int k,
-                                                          double* __restrict__ Linv,
-                                                          EvalResult* __restrict__ res) {
+__global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
+                                                         int64_t N, int k,
+                                                         double* __restrict__ Dinv,
+                                                         EvalResult* __restrict__ res) {
     __shared__ double Ab[NPK * 256];
-    __shared__ double Lb[NPK * 256];
     __shared__ double rdiag[NB];
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const int64_t g0 = (int64_t)k * NB;
     double* Ag = A + g0 * lda + g0;
     // load the lower block triangle: element (r, c) of block (I, J) <- A(16I+r, 16J+c)
-    for (int idx = t; idx < NPK * 256; idx += 512) {
+    for (int idx = t; idx < NPK * 256; idx += 256) {
         const int b = idx >> 8, e = idx & 255, c = e >> 4, r = e & 15;
         int I = 0;
         while ((I + 1) * (I + 2) / 2 <= b) ++I;
@@ -305,45 +276,84 @@ __global__ __launch_bounds__(512) void potrf_diag_kernel(double* __restrict__ A,
     __syncthreads();
     for (int s = 0; s < NDB; ++s) {
         if (s >= 1) {
-            if (wave < NDB - s) dblk_update(Ab, s + wave, s, s - 1, lane);
-            if (wave == 7) dinv_diag(Ab, Lb, rdiag, s - 1, lane);
+            for (int I = s + wave; I < NDB; I += 4) dblk_update(Ab, I, s, s - 1, lane);
+            if (wave == 3) dinv_diag(Ab, Dinv, rdiag, s - 1, lane);
         }
         __syncthreads();
         if (wave == 0) {
             dpanel(Ab, rdiag, s, lane, g0, N, res);
         } else if (s >= 1) {
             const int ntr = (NDB - 1 - s) * (NDB - s) / 2;  // tiles (I,J), s+1 <= J <= I <= 7
-            const int nli = s >= 2 ? s - 1 : 0;              // Linv row s-1, blocks j < s-1
-            for (int task = wave - 1; task < ntr + nli; task += 7) {
-                if (task < ntr) {
-                    int J = s + 1, rem = task;
-                    while (rem >= NDB - J) {
-                        rem -= NDB - J;
-                        ++J;
-                    }
-                    dblk_update(Ab, J + rem, J, s - 1, lane);
-                } else {
-                    dinv_offdiag(Ab, Lb, s - 1, task - ntr, lane);
+            for (int task = wave - 1; task < ntr; task += 3) {
+                int J = s + 1, rem = task;
+                while (rem >= NDB - J) {
+                    rem -= NDB - J;
+                    ++J;
                 }
+                dblk_update(Ab, J + rem, J, s - 1, lane);
             }
         }
         __syncthreads();
     }
-    if (wave == 7) dinv_diag(Ab, Lb, rdiag, NDB - 1, lane);
-    if (wave >= 1 && wave < NDB - 1) dinv_offdiag(Ab, Lb, NDB - 2, wave - 1, lane);  // row 6, j < 6
-    __syncthreads();
-    if (wave >= 1 && wave < NDB) dinv_offdiag(Ab, Lb, NDB - 1, wave - 1, lane);  // row 7, j < 7
-    __syncthreads();
-    // write L (lower incl. diagonal) in place and Linv (column-major, ld NB, zero upper)
-    for (int idx = t; idx < NB * NB; idx += 512) {
+    if (wave == 3) dinv_diag(Ab, Dinv, rdiag, NDB - 1, lane);
+    // write L (lower incl. diagonal) in place
+    for (int idx = t; idx < NB * NB; idx += 256) {
         const int r = idx & (NB - 1), c = idx >> 7;
-        const int I = r >> 4, J = c >> 4;
-        if (J <= I) {
-            const int b = bidx(I, J) * 256;
-            if (r >= c) Ag[(int64_t)c * lda + r] = Ab[b + (c & 15) * 16 + (r & 15)];
-            Linv[c * NB + r] = Lb[b + (r & 15) * 16 + (c & 15)];
-        } else {
-            Linv[c * NB + r] = 0.0;
+        if (r >= c) Ag[(int64_t)c * lda + r] = Ab[bidx(r >> 4, c >> 4) * 256 + (c & 15) * 16 + (r & 15)];
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Panel TRSM by blocked substitution: for each 128-row tile i > k of panel column k,
+//   X = B L_kk^{-T}:  X_b = (B_b - sum_{c<b} X_c L_bc^T) Dinv_b^T,  b = 0..7 (16 columns)
+// computed transposed (Y_b = X_b^T = Dinv_b (B_b^T - sum_c L_bc Y_c)) so that every
+// result stays in the f64 MFMA accumulator layout (row = lane/16 + 4q, col = lane%16),
+// which is exactly the B-operand layout of the next MFMA: no LDS, no transposes.
+// 256 threads = 4 waves x 32 rows (two 16-row blocks, two interleaved MFMA chains).
+// L_kk and Dinv_k are read from global (L2-resident; just written by the diag kernel).
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void trsm_subst_kernel(double* __restrict__ A, int64_t lda, int k,
+                                                         const double* __restrict__ Dinv) {
+    const int bi = k + 1 + (int)blockIdx.x;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int fr = lane >> 4, fc = lane & 15;
+    const int64_t k0 = (int64_t)k * NB;
+    const double* L = A + k0 * lda + k0;                  // L_kk, column-major, lda
+    double* B = A + k0 * lda + (int64_t)bi * NB + 32 * wave;  // this wave's 32 rows of tile (bi, k)
+    d4 Y[2][NDB];
+#pragma unroll
+    for (int b = 0; b < NDB; ++b) {
+        d4 s0, s1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // B_b^T in accumulator layout: [j][r] = B[r][16b + j]
+            const int64_t col = (int64_t)(16 * b + fr + 4 * q) * lda;
+            s0[q] = B[col + fc];
+            s1[q] = B[col + 16 + fc];
+        }
+#pragma unroll
+        for (int c = 0; c < b; ++c) {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const double lbc = -L[(int64_t)(16 * c + 4 * kk + fr) * lda + 16 * b + fc];  // L_bc[j][k]
+                s0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[0][c][kk], s0, 0, 0, 0);
+                s1 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[1][c][kk], s1, 0, 0, 0);
+            }
+        }
+        const double* Di = Dinv + b * 256;  // column-major: A operand [j = fc][m = 4kk + fr]
+        d4 y0 = {0.0, 0.0, 0.0, 0.0}, y1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const double di = Di[(4 * kk + fr) * 16 + fc];
+            y0 = __builtin_amdgcn_mfma_f64_16x16x4f64(di, s0[kk], y0, 0, 0, 0);
+            y1 = __builtin_amdgcn_mfma_f64_16x16x4f64(di, s1[kk], y1, 0, 0, 0);
+        }
+        Y[0][b] = y0;
+        Y[1][b] = y1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t col = (int64_t)(16 * b + fr + 4 * q) * lda;
+            B[col + fc] = y0[q];
+            B[col + 16 + fc] = y1[q];
         }
     }
 }
@@ -533,20 +543,20 @@ __global__ void init_result_kernel(EvalResult* res) {
 
 // ------------------------------- launchers ---------------------------------------
 void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const double* X,
-                 int64_t ldx, const double* v, const TermPack& tp, double noise) {
+                 int64_t ldx, const double* v, const TermPack* dtp) {
     const int64_t ntiles = (int64_t)nt * (nt + 1) / 2;
-    gram_kernel<<<dim3((unsigned)ntiles), dim3(256), 0, s>>>(A, lda, N, X, ldx, v, tp, noise);
+    gram_kernel<<<dim3((unsigned)ntiles), dim3(256), 0, s>>>(A, lda, N, X, ldx, v, dtp);
 }
 
-void launch_potrf_diag(hipStream_t s, double* A, int64_t lda, int64_t N, int k, double* Linv,
+void launch_potrf_diag(hipStream_t s, double* A, int64_t lda, int64_t N, int k, double* Dinv,
                        EvalResult* res) {
-    potrf_diag_kernel<<<dim3(1), dim3(512), 0, s>>>(A, lda, N, k, Linv, res);
+    potrf_diag_kernel<<<dim3(1), dim3(256), 0, s>>>(A, lda, N, k, Dinv, res);
 }
 
-void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Linv) {
+void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Dinv) {
     const int n = nt - k - 1;
     if (n <= 0) return;
-    tile_gemm_kernel<1><<<dim3(n), dim3(256), 0, s>>>(A, lda, k, 0, 0, Linv, nullptr, 0);
+    trsm_subst_kernel<<<dim3(n), dim3(256), 0, s>>>(A, lda, k, Dinv);
 }
 
 void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int colmode,
