@@ -56,6 +56,7 @@ class Stats(ctypes.Structure):
         ("gram_launches", c_int64),
         ("panel_ms", c_double),
         ("trsm_ms", c_double),
+        ("colupd_ms", c_double),
         ("total_ms", c_double),
     ]
 

@@ -9,6 +9,7 @@
 // (details at factor_and_reduce)
 #include "gaplac_internal.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -201,13 +202,10 @@ struct SpanGuard {
     }
 };
 
-// Algorithmic flops of one trailing-update launch: lower triangle (incl. diagonal) of the
-// updated tiles, 2 flops per multiply-add, K = NB.
-double syrk_flops(int m, int colmode) {
+// Algorithmic flops of one bulk trailing-update launch per 128 of K: lower triangle
+// (incl. diagonal) of the m x m tile triangle, 2 flops per multiply-add.
+double syrk_flops(int m, int /*colmode*/) {
     const double nbd = NB;
-    if (colmode) {  // one diagonal tile + (m-1) full tiles
-        return 2.0 * nbd * ((m - 1) * nbd * nbd + nbd * (nbd + 1) / 2.0);
-    }
     const double rows = (double)m * nbd;
     return 2.0 * nbd * rows * (rows + 1) / 2.0;
 }
@@ -233,6 +231,9 @@ void collect_spans(gaplac_ctx* ctx) {
             case 4:
                 ctx->stats.trsm_ms += ms;
                 break;
+            case 5:
+                ctx->stats.colupd_ms += ms;
+                break;
             default:
                 ctx->stats.total_ms += ms;
                 break;
@@ -244,57 +245,67 @@ void collect_spans(gaplac_ctx* ctx) {
 
 // Factor the augmented matrix already built in ctx->A (Gram launched on s_main).
 //
-// Two streams. s_panel (highest priority, all CUs) runs the critical path in order:
-// the lookahead column update, the 128x128 diagonal factorisation and the panel TRSM.
-// s_main (CU-masked: GAPLAC_DIAG_CUS CUs, default 1, excluded) runs the bulk trailing
-// updates. The excluded CU(s) never hold trailing-update workgroups, and the diagonal
-// kernel starts only after its own stream predecessors finished, so it always finds a
-// free CU (without this it starved ~600 us per step behind trailing-update workgroups).
-// Keeping the whole chain on one stream avoids cross-stream event hops inside it
-// (~25 us each, measured). Step k (panel k factored and solved):
-//   s_panel: wait R(k-1) | syrk_col(k+1) with panel k | potrf(k+1) | trsm(k+1) | rec P(k+1)
-//   s_main : wait P(k)   | syrk_tri(tile columns >= k+2) with panel k          | rec R(k)
-// Column k+1 receives panel k-1's update in R(k-1) and panel k's in syrk_col(k+1); within
-// a step the streams touch disjoint tile columns. Events ping-pong (k & 1) so a record
-// never overtakes a wait that still refers to the previous step.
+// Super-panels of two 128-wide tile columns (p covers tile columns 2p, 2p+1): the panel
+// chain factors 128-wide blocks, the bulk trailing update applies a whole super-panel at
+// once (K = 256), halving the C-tile read/write traffic and tile prologues per flop.
+//
+// Two streams. s_panel (highest priority, all CUs) runs the critical path in order;
+// s_main (CU-masked when available: GAPLAC_DIAG_CUS CUs, default 1, excluded) runs the
+// bulk updates. In eager mode the excluded CU keeps a free slot for the diagonal kernel;
+// in graph mode (default) the kernels are slot-compatible anyway.
+//   s_panel: wait R(p-1) | col_update(columns of SP p+1, with SP p, K=256)
+//            | potrf(2p+2) trsm(2p+2) col_update(2p+3 with panel 2p+2) potrf(2p+3) trsm(2p+3)
+//            | rec P(p+1)
+//   s_main : wait P(p)   | syrk_tri(tile columns >= 2p+4, with SP p, K=256) | rec R(p)
+// Columns of SP p+1 receive SP p-1 in R(p-1) and SP p in the lookahead col_update; within
+// a step the streams touch disjoint tile columns. Events ping-pong (p & 1).
+void factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, int nt, int p) {
+    const int c0 = 2 * p, c1 = std::min(2 * p + 2, nt);
+    for (int c = c0; c < c1; ++c) {
+        if (c > c0) {
+            SpanGuard g(ctx, sp, 5, 0);
+            launch_col_update(sp, ctx->A, lda, nt, c - 1, c, 1, NB);
+        }
+        double* Dk = ctx->Dinv + (size_t)c * DINV_PER_BLOCK;
+        if ((int64_t)c * NB < N) {
+            SpanGuard g(ctx, sp, 2, 0);
+            launch_potrf_diag(sp, ctx->A, lda, N, c, Dk, ctx->dres);
+        }
+        {
+            SpanGuard g(ctx, sp, 4, 0);
+            launch_trsm(sp, ctx->A, lda, nt, c, Dk);
+        }
+    }
+}
+
 int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     hipStream_t sm = ctx->s_main;
     hipStream_t sp = ctx->serial ? sm : ctx->s_panel;
+    const int nsp = (nt + 1) / 2;
     HIPCK(ctx, hipEventRecord(ctx->ev_gram, sm));
     HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_gram, 0));
-    {
-        SpanGuard g(ctx, sp, 2, 0);
-        launch_potrf_diag(sp, ctx->A, lda, N, 0, ctx->Dinv, ctx->dres);
-    }
-    {
-        SpanGuard g(ctx, sp, 4, 0);
-        launch_trsm(sp, ctx->A, lda, nt, 0, ctx->Dinv);
-    }
+    factor_superpanel(ctx, sp, N, lda, nt, 0);
     HIPCK(ctx, hipEventRecord(ctx->ev_P[0], sp));
-    for (int k = 0; k < nt; ++k) {
-        if (k + 1 < nt) {
-            if (k >= 1) HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_R[(k - 1) & 1], 0));
+    for (int p = 0; p < nsp; ++p) {
+        const int c0 = 2 * p;
+        const int kd = (std::min(2 * p + 2, nt) - c0) * NB;  // depth of super-panel p
+        if (p + 1 < nsp) {
+            if (p >= 1) HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_R[(p - 1) & 1], 0));
+            const int ncols = std::min(2 * p + 4, nt) - (c0 + 2);
             {
-                SpanGuard g(ctx, sp, 0, syrk_flops(nt - (k + 1), 1));
-                launch_syrk(sp, ctx->A, lda, nt, k, k + 1, 1, nullptr);
+                SpanGuard g(ctx, sp, 5, 0);
+                launch_col_update(sp, ctx->A, lda, nt, c0, c0 + 2, ncols, kd);
             }
-            double* Lk = ctx->Dinv + (size_t)(k + 1) * DINV_PER_BLOCK;
-            if ((int64_t)(k + 1) * NB < N) {
-                SpanGuard g(ctx, sp, 2, 0);
-                launch_potrf_diag(sp, ctx->A, lda, N, k + 1, Lk, ctx->dres);
-            }
-            {
-                SpanGuard g(ctx, sp, 4, 0);
-                launch_trsm(sp, ctx->A, lda, nt, k + 1, Lk);
-            }
-            HIPCK(ctx, hipEventRecord(ctx->ev_P[(k + 1) & 1], sp));
+            factor_superpanel(ctx, sp, N, lda, nt, p + 1);
+            HIPCK(ctx, hipEventRecord(ctx->ev_P[(p + 1) & 1], sp));
         }
-        HIPCK(ctx, hipStreamWaitEvent(sm, ctx->ev_P[k & 1], 0));
-        if (k + 2 < nt) {
-            SpanGuard g(ctx, sm, 0, syrk_flops(nt - (k + 2), 0));
-            launch_syrk(sm, ctx->A, lda, nt, k, k + 2, 0, ctx->tiles + ctx->tile_off[(size_t)(nt - (k + 2))]);
+        HIPCK(ctx, hipStreamWaitEvent(sm, ctx->ev_P[p & 1], 0));
+        const int jb = c0 + 4;
+        if (jb < nt) {
+            SpanGuard g(ctx, sm, 0, syrk_flops(nt - jb, 0) * (kd / NB));
+            launch_syrk(sm, ctx->A, lda, nt, c0, jb, kd, ctx->tiles + ctx->tile_off[(size_t)(nt - jb)]);
         }
-        HIPCK(ctx, hipEventRecord(ctx->ev_R[k & 1], sm));
+        HIPCK(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
     }
     launch_reduce(sm, ctx->A, lda, N, ctx->dres);
     HIPCK(ctx, hipGetLastError());

@@ -42,11 +42,15 @@ void launch_potrf_diag(hipStream_t s, double* A, int64_t lda, int64_t N, int k,
                        double* Dinv, EvalResult* res);
 // TRSM of the panel rows below diagonal block k: A[i,k] <- A[i,k] * L_kk^{-T}, i>k.
 void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Dinv);
-// Trailing update with panel k. colmode=1: only tile column jb (tiles i>=jb);
-// colmode=0: lower triangle of tile blocks jb..nt-1.
-// tiles: super-tile ordered list for the m x m triangle, m = nt - jb (build_tile_list).
-void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int colmode,
+// Bulk trailing update: lower triangle of tile blocks jb..nt-1 minus the kdepth columns
+// starting at tile column k (kdepth 128 or 256). tiles: super-tile ordered list for the
+// m x m triangle, m = nt - jb (build_tile_list).
+void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int kdepth,
                  const uint32_t* tiles);
+// Lookahead update of tile columns jb (and jb+1 if ncols == 2) with the kdepth columns
+// starting at tile column k.
+void launch_col_update(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int ncols,
+                       int kdepth);
 void build_tile_list(int m, uint32_t* out);
 void launch_reduce(hipStream_t s, const double* A, int64_t lda, int64_t N, EvalResult* res);
 void launch_init_result(hipStream_t s, EvalResult* res);

@@ -155,6 +155,7 @@ __global__ __launch_bounds__(256) void gram_kernel(double* __restrict__ A, int64
 //            remaining trailing tiles on MFMA.
 // Pivots of padding columns (>= N) are forced to 1; a pivot <= 0 records info = j+1
 // (OpenBLAS potf2's test; NaN pivots propagate, as in the reference).
+// The eight 16x16 inverses are computed after the loop (off the per-panel barriers).
 // ---------------------------------------------------------------------------------
 constexpr int DB = 16;                    // sub-block edge
 constexpr int NDB = NB / DB;              // 8
@@ -234,8 +235,13 @@ __device__ __forceinline__ void dpanel(double* Ab, double* rdiag, int s, int lan
             // pivot is not reported and propagates to a NaN logpdf, as in the reference.
             if (lane == 0 && piv <= 0.0)
                 atomicMin(&res->info, (unsigned long long)(gcol0 + R0 + c + 1));
-            d = sqrt(piv);
-            rd = 1.0 / d;
+            // 1/sqrt by v_rsq_f64 + two Newton steps (full fp64 accuracy, ~1/3 of the
+            // latency of sqrt followed by a correctly rounded divide)
+            double y = __builtin_amdgcn_rsq(piv);
+            y = y * (1.5 - 0.5 * piv * y * y);
+            y = y * (1.5 - 0.5 * piv * y * y);
+            rd = y;
+            d = piv * y;
         }
         if (lane == 0) rdiag[R0 + c] = rd;
         v0[c] = rel0 > c ? v0[c] * rd : (rel0 == c ? d : v0[c]);
@@ -262,22 +268,23 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
                                                          EvalResult* __restrict__ res) {
     __shared__ double Ab[NPK * 256];
     __shared__ double rdiag[NB];
+    __builtin_amdgcn_s_setprio(3);  // critical path: win issue arbitration on shared SIMDs
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const int64_t g0 = (int64_t)k * NB;
     double* Ag = A + g0 * lda + g0;
     // load the lower block triangle: element (r, c) of block (I, J) <- A(16I+r, 16J+c)
-    for (int idx = t; idx < NPK * 256; idx += 256) {
-        const int b = idx >> 8, e = idx & 255, c = e >> 4, r = e & 15;
-        int I = 0;
-        while ((I + 1) * (I + 2) / 2 <= b) ++I;
-        const int J = b - I * (I + 1) / 2;
-        Ab[idx] = Ag[(int64_t)(16 * J + c) * lda + 16 * I + r];
+    {
+        const int c = t >> 4, r = t & 15;
+#pragma unroll
+        for (int I = 0; I < NDB; ++I)
+#pragma unroll
+            for (int J = 0; J <= I; ++J)
+                Ab[bidx(I, J) * 256 + t] = Ag[(int64_t)(16 * J + c) * lda + 16 * I + r];
     }
     __syncthreads();
     for (int s = 0; s < NDB; ++s) {
         if (s >= 1) {
             for (int I = s + wave; I < NDB; I += 4) dblk_update(Ab, I, s, s - 1, lane);
-            if (wave == 3) dinv_diag(Ab, Dinv, rdiag, s - 1, lane);
         }
         __syncthreads();
         if (wave == 0) {
@@ -295,11 +302,16 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
         }
         __syncthreads();
     }
-    if (wave == 3) dinv_diag(Ab, Dinv, rdiag, NDB - 1, lane);
+    dinv_diag(Ab, Dinv, rdiag, wave, lane);
+    dinv_diag(Ab, Dinv, rdiag, wave + 4, lane);
     // write L (lower incl. diagonal) in place
-    for (int idx = t; idx < NB * NB; idx += 256) {
-        const int r = idx & (NB - 1), c = idx >> 7;
-        if (r >= c) Ag[(int64_t)c * lda + r] = Ab[bidx(r >> 4, c >> 4) * 256 + (c & 15) * 16 + (r & 15)];
+    {
+        const int c = t >> 4, r = t & 15;
+#pragma unroll
+        for (int I = 0; I < NDB; ++I)
+#pragma unroll
+            for (int J = 0; J <= I; ++J)
+                if (I != J || r >= c) Ag[(int64_t)(16 * J + c) * lda + 16 * I + r] = Ab[bidx(I, J) * 256 + t];
     }
 }
 
@@ -314,6 +326,7 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void trsm_subst_kernel(double* __restrict__ A, int64_t lda, int k,
                                                          const double* __restrict__ Dinv) {
+    __builtin_amdgcn_s_setprio(2);  // critical path
     const int bi = k + 1 + (int)blockIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int fr = lane >> 4, fc = lane & 15;
@@ -359,8 +372,8 @@ __global__ __launch_bounds__(256) void trsm_subst_kernel(double* __restrict__ A,
 }
 
 // ---------------------------------------------------------------------------------
-// 128x128 fp64 MFMA tile kernel, K = NB = 128 (one panel).
-//   MODE 0 (SYRK): C(bi,bj) -= P_bi * P_bj^T, P = panel block column k.
+// 128x128 fp64 MFMA tile kernel, K = kdepth (128: one panel; 256: a super-panel of two).
+//   MODE 0 (SYRK): C(bi,bj) -= P_bi * P_bj^T, P = the kdepth columns starting at k*NB.
 //   MODE 1 (TRSM): P_bi <- P_bi * Linv^T (in place), bi > k.
 // 256 threads = 4 waves as 2x2, each wave a 64x64 sub-tile = 4x4 v_mfma_f64_16x16x4f64
 // accumulators. Operands are staged through LDS in 16-deep k-chunks, double-buffered
@@ -383,7 +396,7 @@ __global__ __launch_bounds__(256, 2) void tile_gemm_kernel(double* __restrict__ 
                                                            int k, int jb, int colmode,
                                                            const double* __restrict__ Linv,
                                                            const uint32_t* __restrict__ tiles,
-                                                           int ntiles) {
+                                                           int ntiles, int kdepth) {
     __shared__ double sm[2][2][KB][LR];
     int bi, bj;
     if (MODE == 1) {
@@ -462,7 +475,7 @@ __global__ __launch_bounds__(256, 2) void tile_gemm_kernel(double* __restrict__ 
     gload(0);
     lstore(0);
     __syncthreads();
-    constexpr int NCH = NB / KB;
+    const int NCH = kdepth / KB;
     for (int ch = 0; ch < NCH; ++ch) {
         const int buf = ch & 1;
         if (ch + 1 < NCH) gload(ch + 1);
@@ -496,6 +509,61 @@ __global__ __launch_bounds__(256, 2) void tile_gemm_kernel(double* __restrict__ 
             for (int rg = 0; rg < 4; ++rg)
                 Ci[(int64_t)(64 * wj + 16 * mj + fr + 4 * rg) * lda] = acc[mi][mj][rg];
     }
+}
+
+// ---------------------------------------------------------------------------------
+// Lookahead column update (critical path): C(i, jb) -= P_i P_jb^T for the tiles i >= jb
+// of one or two tile columns, K = kdepth (128 or 256), split into 64x64 quadrants so a column of m tiles runs as
+// ~4m short workgroups (the bulk SYRK's 128x128 tiles take ~25 us each alone on a CU;
+// a quadrant ~4x less). 4 waves as 2x2 of 32x32 (2x2 f64 MFMA accumulators each);
+// fragments are read straight from global (the panel column was just written and is
+// L2-resident), no LDS, no barriers. The upper quadrant of the diagonal tile is skipped.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void col_update_kernel(double* __restrict__ A, int64_t lda, int k,
+                                                         int jb0, int m0, int kdepth) {
+    __builtin_amdgcn_s_setprio(2);  // critical path
+    const int q = (int)blockIdx.x & 3;
+    int t = (int)blockIdx.x >> 2, jb = jb0;
+    if (t >= m0) {  // second tile column (super-panel lookahead updates two)
+        t -= m0;
+        jb = jb0 + 1;
+    }
+    const int bi = jb + t;
+    const int qi = q >> 1, qj = q & 1;
+    if (bi == jb && qj > qi) return;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wi = wave & 1, wj = wave >> 1;
+    const int fr = lane >> 4, fc = lane & 15;
+    const int64_t k0 = (int64_t)k * NB;
+    const int64_t ri = (int64_t)bi * NB + 64 * qi + 32 * wi;  // this wave's 32 rows
+    const int64_t cj = (int64_t)jb * NB + 64 * qj + 32 * wj;  // this wave's 32 columns
+    const double* P = A + k0 * lda + ri;
+    const double* Q = A + k0 * lda + cj;
+    d4 acc[2][2];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int mj = 0; mj < 2; ++mj)
+#pragma unroll
+            for (int rg = 0; rg < 4; ++rg)
+                acc[mi][mj][rg] = A[(cj + 16 * mj + fr + 4 * rg) * lda + ri + 16 * mi + fc];
+#pragma unroll 8
+    for (int ks = 0; ks < kdepth; ks += 4) {
+        const int64_t col = (int64_t)(ks + fr) * lda;
+        const double b0 = -P[col + fc], b1 = -P[col + 16 + fc];
+        const double a0 = Q[col + fc], a1 = Q[col + 16 + fc];
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[1][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[0][1], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int mj = 0; mj < 2; ++mj)
+#pragma unroll
+            for (int rg = 0; rg < 4; ++rg)
+                A[(cj + 16 * mj + fr + 4 * rg) * lda + ri + 16 * mi + fc] = acc[mi][mj][rg];
 }
 
 // ---------------------------------------------------------------------------------
@@ -559,17 +627,22 @@ void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const dou
     trsm_subst_kernel<<<dim3(n), dim3(256), 0, s>>>(A, lda, k, Dinv);
 }
 
-void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int colmode,
+void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int kdepth,
                  const uint32_t* tiles) {
     const int m = nt - jb;
     if (m <= 0) return;
-    if (colmode) {
-        tile_gemm_kernel<0><<<dim3((unsigned)m), dim3(256), 0, s>>>(A, lda, k, jb, 1, nullptr, nullptr, 0);
-        return;
-    }
     const int ntiles = m * (m + 1) / 2;
     const int grid = ((ntiles + 7) >> 3) << 3;
-    tile_gemm_kernel<0><<<dim3((unsigned)grid), dim3(256), 0, s>>>(A, lda, k, jb, 0, nullptr, tiles, ntiles);
+    tile_gemm_kernel<0><<<dim3((unsigned)grid), dim3(256), 0, s>>>(A, lda, k, jb, 0, nullptr, tiles, ntiles,
+                                                                    kdepth);
+}
+
+void launch_col_update(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int ncols,
+                       int kdepth) {
+    const int m0 = nt - jb;
+    if (m0 <= 0) return;
+    const int tiles = ncols == 2 && m0 > 1 ? 2 * m0 - 1 : m0;
+    col_update_kernel<<<dim3((unsigned)(4 * tiles)), dim3(256), 0, s>>>(A, lda, k, jb, m0, kdepth);
 }
 
 // Super-tile ordered list of the lower-triangular m x m tile set (entry = bi | bj << 16,

@@ -131,7 +131,7 @@ int gaplac_factor(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_
  * each kernel is launched on, when profiling is on (off by default). */
 typedef struct gaplac_stats {
     int64_t evals;
-    int64_t syrk_launches;      /* trailing-update launches */
+    int64_t syrk_launches;      /* bulk trailing-update launches (tile_gemm_kernel<0>) */
     double  syrk_ms;            /* summed event time of those launches */
     double  syrk_flops;         /* algorithmic flops of those launches */
     double  gram_ms;
@@ -139,6 +139,7 @@ typedef struct gaplac_stats {
     int64_t gram_launches;
     double  panel_ms;           /* diagonal-block potrf launches, summed */
     double  trsm_ms;            /* panel TRSM launches, summed */
+    double  colupd_ms;          /* lookahead column-update launches, summed */
     double  total_ms;           /* whole evaluation, first kernel to result */
 } gaplac_stats;
 int gaplac_set_profiling(gaplac_ctx* ctx, int on);
