@@ -43,27 +43,32 @@ struct gaplac_ctx {
     EvalResult* hres = nullptr;  // pinned
     TermPack* dtp = nullptr;     // device copy of the term descriptor (read by gram_kernel)
     TermPack* htp = nullptr;     // pinned staging for it
+    std::string err;
+    // profiling: per-launch device timestamps (KTime slots), see kt_begin/kt_end
+    bool profiling = false;
+    bool serial = false;  // GAPLAC_SERIAL=1: one stream, no overlap (per-kernel timing)
+    int bulk_valu = 0;    // GAPLAC_BULK=valu: v_fma_f64 bulk-update kernel instead of MFMA
+    gaplac_stats stats{};
+    struct Slot {
+        int kind;  // 0 bulk syrk, 1 gram, 2 diag, 4 trsm, 5 column update
+        double work;
+    };
+    std::vector<Slot> slots;     // slots of the launches being enqueued / of the profiled graph
+    KTime* dkt = nullptr;        // device slot array
+    KTime* hkt = nullptr;        // pinned copy
+    size_t kt_cap = 0;
+    bool recording = false;      // assign slots while enqueuing
     // Captured schedule of one evaluation (hipGraph), replayed while N and the workspace
     // pointers stay the same: removes the per-launch and cross-stream event-hop costs
     // (2.9 us per dependent launch, ~12 us per event hop eager vs ~1.6 us in a graph).
+    // The profiled variant is the same schedule with KTime slots wired in.
     bool use_graph = true;
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t gexec = nullptr;
-    int64_t gN = -1;
+    hipGraph_t graph = nullptr, pgraph = nullptr;
+    hipGraphExec_t gexec = nullptr, pgexec = nullptr;
+    int64_t gN = -1, pgN = -1;
     const void* gptrs[6] = {};
-    std::string err;
-    // profiling
-    bool profiling = false;
-    bool serial = false;  // GAPLAC_SERIAL=1: one stream, no overlap (per-kernel timing)
-    gaplac_stats stats{};
-    std::vector<hipEvent_t> evpool;
-    size_t evused = 0;
-    struct Span {
-        int kind;  // 0 syrk, 1 gram, 2 panel, 3 total
-        hipEvent_t a, b;
-        double work;
-    };
-    std::vector<Span> spans;
+    const void* pgptrs[6] = {};
+    std::vector<Slot> pslots;
 };
 
 namespace {
@@ -170,59 +175,43 @@ int ensure(gaplac_ctx* ctx, T** p, size_t* cap, size_t n) {
     return 0;
 }
 
-hipEvent_t pool_event(gaplac_ctx* ctx) {
-    if (ctx->evused == ctx->evpool.size()) {
-        hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return nullptr;
-        ctx->evpool.push_back(e);
-    }
-    return ctx->evpool[ctx->evused++];
+// Profiling slot for the next launch (nullptr when profiling is off).
+KTime* slot(gaplac_ctx* ctx, int kind, double work) {
+    if (!ctx->recording) return nullptr;
+    const size_t i = ctx->slots.size();
+    if (i >= ctx->kt_cap) return nullptr;
+    ctx->slots.push_back({kind, work});
+    return ctx->dkt + i;
 }
-
-struct SpanGuard {
-    gaplac_ctx* ctx;
-    hipStream_t s;
-    int kind;
-    double work;
-    hipEvent_t a = nullptr;
-    SpanGuard(gaplac_ctx* c, hipStream_t st, int k, double w) : ctx(c), s(st), kind(k), work(w) {
-        if (ctx->profiling) {
-            a = pool_event(ctx);
-            if (a) (void)hipEventRecord(a, s);
-        }
-    }
-    ~SpanGuard() {
-        if (ctx->profiling && a) {
-            hipEvent_t b = pool_event(ctx);
-            if (b) {
-                (void)hipEventRecord(b, s);
-                ctx->spans.push_back({kind, a, b, work});
-            }
-        }
-    }
-};
 
 // Algorithmic flops of one bulk trailing-update launch per 128 of K: lower triangle
 // (incl. diagonal) of the m x m tile triangle, 2 flops per multiply-add.
-double syrk_flops(int m, int /*colmode*/) {
+double syrk_flops(int m) {
     const double nbd = NB;
     const double rows = (double)m * nbd;
     return 2.0 * nbd * rows * (rows + 1) / 2.0;
 }
 
-void collect_spans(gaplac_ctx* ctx) {
-    for (auto& sp : ctx->spans) {
-        float ms = 0.f;
-        if (hipEventElapsedTime(&ms, sp.a, sp.b) != hipSuccess) continue;
-        switch (sp.kind) {
+// Fold the device timestamps of the given slots into ctx->stats (ticks: 100 MHz).
+int accumulate_slots(gaplac_ctx* ctx, const std::vector<gaplac_ctx::Slot>& slots) {
+    if (slots.empty()) return 0;
+    HIPCK(ctx, hipMemcpy(ctx->hkt, ctx->dkt, slots.size() * sizeof(KTime), hipMemcpyDeviceToHost));
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (size_t i = 0; i < slots.size(); ++i) {
+        const KTime& t = ctx->hkt[i];
+        if (t.end < t.start || t.start == ~0ull) continue;
+        const double ms = (double)(t.end - t.start) * 1e-5;
+        t0 = std::min(t0, t.start);
+        t1 = std::max(t1, t.end);
+        switch (slots[i].kind) {
             case 0:
                 ctx->stats.syrk_ms += ms;
-                ctx->stats.syrk_flops += sp.work;
+                ctx->stats.syrk_flops += slots[i].work;
                 ctx->stats.syrk_launches += 1;
                 break;
             case 1:
                 ctx->stats.gram_ms += ms;
-                ctx->stats.gram_bytes += sp.work;
+                ctx->stats.gram_bytes += slots[i].work;
                 ctx->stats.gram_launches += 1;
                 break;
             case 2:
@@ -231,16 +220,14 @@ void collect_spans(gaplac_ctx* ctx) {
             case 4:
                 ctx->stats.trsm_ms += ms;
                 break;
-            case 5:
-                ctx->stats.colupd_ms += ms;
-                break;
             default:
-                ctx->stats.total_ms += ms;
+                ctx->stats.colupd_ms += ms;
                 break;
         }
     }
-    ctx->spans.clear();
-    ctx->evused = 0;
+    if (t1 > t0) ctx->stats.total_ms += (double)(t1 - t0) * 1e-5;
+    ctx->stats.evals += 1;
+    return 0;
 }
 
 // Factor the augmented matrix already built in ctx->A (Gram launched on s_main).
@@ -262,19 +249,10 @@ void collect_spans(gaplac_ctx* ctx) {
 void factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, int nt, int p) {
     const int c0 = 2 * p, c1 = std::min(2 * p + 2, nt);
     for (int c = c0; c < c1; ++c) {
-        if (c > c0) {
-            SpanGuard g(ctx, sp, 5, 0);
-            launch_col_update(sp, ctx->A, lda, nt, c - 1, c, 1, NB);
-        }
+        if (c > c0) launch_col_update(sp, ctx->A, lda, nt, c - 1, c, 1, NB, slot(ctx, 5, 0));
         double* Dk = ctx->Dinv + (size_t)c * DINV_PER_BLOCK;
-        if ((int64_t)c * NB < N) {
-            SpanGuard g(ctx, sp, 2, 0);
-            launch_potrf_diag(sp, ctx->A, lda, N, c, Dk, ctx->dres);
-        }
-        {
-            SpanGuard g(ctx, sp, 4, 0);
-            launch_trsm(sp, ctx->A, lda, nt, c, Dk);
-        }
+        if ((int64_t)c * NB < N) launch_potrf_diag(sp, ctx->A, lda, N, c, Dk, ctx->dres, slot(ctx, 2, 0));
+        launch_trsm(sp, ctx->A, lda, nt, c, Dk, slot(ctx, 4, 0));
     }
 }
 
@@ -292,19 +270,15 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         if (p + 1 < nsp) {
             if (p >= 1) HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_R[(p - 1) & 1], 0));
             const int ncols = std::min(2 * p + 4, nt) - (c0 + 2);
-            {
-                SpanGuard g(ctx, sp, 5, 0);
-                launch_col_update(sp, ctx->A, lda, nt, c0, c0 + 2, ncols, kd);
-            }
+            launch_col_update(sp, ctx->A, lda, nt, c0, c0 + 2, ncols, kd, slot(ctx, 5, 0));
             factor_superpanel(ctx, sp, N, lda, nt, p + 1);
             HIPCK(ctx, hipEventRecord(ctx->ev_P[(p + 1) & 1], sp));
         }
         HIPCK(ctx, hipStreamWaitEvent(sm, ctx->ev_P[p & 1], 0));
         const int jb = c0 + 4;
-        if (jb < nt) {
-            SpanGuard g(ctx, sm, 0, syrk_flops(nt - jb, 0) * (kd / NB));
-            launch_syrk(sm, ctx->A, lda, nt, c0, jb, kd, ctx->tiles + ctx->tile_off[(size_t)(nt - jb)]);
-        }
+        if (jb < nt)
+            launch_syrk(sm, ctx->A, lda, nt, c0, jb, kd, ctx->tiles + ctx->tile_off[(size_t)(nt - jb)],
+                        ctx->bulk_valu, slot(ctx, 0, syrk_flops(nt - jb) * (kd / NB)));
         HIPCK(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
     }
     launch_reduce(sm, ctx->A, lda, N, ctx->dres);
@@ -329,15 +303,14 @@ int ensure_tile_lists(gaplac_ctx* ctx, int nt) {
 }
 
 // Everything one evaluation puts on the streams (eager launch or graph capture): reset
-// the result record, Gram build, factorisation schedule, reduction, result copy to the
-// pinned host record. Inputs: ctx->dX (ld N), ctx->dv, ctx->dtp.
+// the result record (and the profiling slots), Gram build, factorisation schedule,
+// reduction, result copy to the pinned host record. Inputs: ctx->dX (ld N), ctx->dv,
+// ctx->dtp.
 int enqueue_eval(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt) {
     launch_init_result(ctx->s_main, ctx->dres);
-    {
-        const double bytes = 8.0 * (double)Np * (double)(Np + 1) / 2.0 + 8.0 * (double)N * (D + 1);
-        SpanGuard g(ctx, ctx->s_main, 1, bytes);
-        launch_gram(ctx->s_main, ctx->A, Np, N, nt, ctx->dX, N, ctx->dv, ctx->dtp);
-    }
+    if (ctx->recording) launch_kt_reset(ctx->s_main, ctx->dkt, (int)ctx->kt_cap);
+    const double bytes = 8.0 * (double)Np * (double)(Np + 1) / 2.0 + 8.0 * (double)N * (D + 1);
+    launch_gram(ctx->s_main, ctx->A, Np, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, slot(ctx, 1, bytes));
     int rc;
     if ((rc = factor_and_reduce(ctx, N, Np, nt))) return rc;
     HIPCK(ctx, hipMemcpyAsync(ctx->hres, ctx->dres, sizeof(EvalResult), hipMemcpyDeviceToHost,
@@ -345,12 +318,15 @@ int enqueue_eval(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt) {
     return 0;
 }
 
-void drop_graph(gaplac_ctx* ctx) {
-    if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
-    if (ctx->graph) (void)hipGraphDestroy(ctx->graph);
-    ctx->gexec = nullptr;
-    ctx->graph = nullptr;
-    ctx->gN = -1;
+void drop_graph(gaplac_ctx* ctx, bool prof) {
+    hipGraphExec_t& gx = prof ? ctx->pgexec : ctx->gexec;
+    hipGraph_t& g = prof ? ctx->pgraph : ctx->graph;
+    if (gx) (void)hipGraphExecDestroy(gx);
+    if (g) (void)hipGraphDestroy(g);
+    gx = nullptr;
+    g = nullptr;
+    (prof ? ctx->pgN : ctx->gN) = -1;
+    if (prof) ctx->pslots.clear();
 }
 
 // Full evaluation; inputs already in ctx->dX (ld N) / ctx->dv, term pack in tp (host).
@@ -363,15 +339,31 @@ int eval_device(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp, EvalR
     if ((rc = ensure(ctx, &ctx->A, &ctx->A_elems, (size_t)Np * Np))) return rc;
     if ((rc = ensure(ctx, &ctx->Dinv, &ctx->Dinv_elems, (size_t)nt * DINV_PER_BLOCK))) return rc;
     if ((rc = ensure_tile_lists(ctx, nt))) return rc;
+    const bool prof = ctx->profiling;
+    if (prof) {
+        const size_t need = (size_t)nt * 6 + 16;  // launches per evaluation, with margin
+        if (ctx->kt_cap < need) {
+            if ((rc = ensure(ctx, &ctx->dkt, &ctx->kt_cap, need))) return rc;
+            if (ctx->hkt) (void)hipHostFree(ctx->hkt);
+            ctx->hkt = nullptr;
+            HIPCK(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->hkt), ctx->kt_cap * sizeof(KTime), 0));
+        }
+    }
     *ctx->htp = tp;
     HIPCK(ctx, hipMemcpyAsync(ctx->dtp, ctx->htp, sizeof(TermPack), hipMemcpyHostToDevice, ctx->s_main));
-    const bool graph = ctx->use_graph && !ctx->profiling && !ctx->serial;
-    if (graph) {
-        const void* ptrs[6] = {ctx->A, ctx->Dinv, ctx->dX, ctx->dv, ctx->tiles, ctx->dres};
-        if (!ctx->gexec || ctx->gN != N || std::memcmp(ptrs, ctx->gptrs, sizeof ptrs) != 0) {
-            drop_graph(ctx);
+    if (ctx->use_graph && !ctx->serial) {
+        hipGraph_t& G = prof ? ctx->pgraph : ctx->graph;
+        hipGraphExec_t& GX = prof ? ctx->pgexec : ctx->gexec;
+        int64_t& GN = prof ? ctx->pgN : ctx->gN;
+        const void** GP = prof ? ctx->pgptrs : ctx->gptrs;
+        const void* ptrs[6] = {ctx->A, ctx->Dinv, ctx->dX, ctx->dv, ctx->tiles, prof ? (const void*)ctx->dkt : nullptr};
+        if (!GX || GN != N || std::memcmp(ptrs, GP, sizeof ptrs) != 0) {
+            drop_graph(ctx, prof);
+            ctx->slots.clear();
+            ctx->recording = prof;
             HIPCK(ctx, hipStreamBeginCapture(ctx->s_main, hipStreamCaptureModeThreadLocal));
             rc = enqueue_eval(ctx, N, D, Np, nt);
+            ctx->recording = false;
             hipGraph_t g = nullptr;
             const hipError_t ce = hipStreamEndCapture(ctx->s_main, &g);
             if (rc) {
@@ -380,34 +372,31 @@ int eval_device(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp, EvalR
             }
             if (ce != hipSuccess)
                 return set_err(ctx, GAPLAC_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ce));
-            ctx->graph = g;
-            HIPCK(ctx, hipGraphInstantiate(&ctx->gexec, ctx->graph, nullptr, nullptr, 0));
-            ctx->gN = N;
-            std::memcpy(ctx->gptrs, ptrs, sizeof ptrs);
+            G = g;
+            HIPCK(ctx, hipGraphInstantiate(&GX, G, nullptr, nullptr, 0));
+            GN = N;
+            std::memcpy(GP, ptrs, sizeof ptrs);
+            if (prof) ctx->pslots = ctx->slots;
+            ctx->slots.clear();
         }
-        HIPCK(ctx, hipGraphLaunch(ctx->gexec, ctx->s_main));
+        HIPCK(ctx, hipGraphLaunch(GX, ctx->s_main));
         HIPCK(ctx, hipStreamSynchronize(ctx->s_main));
         *out = *ctx->hres;
+        if (prof) return accumulate_slots(ctx, ctx->pslots);
         return 0;
     }
-    hipEvent_t t0 = nullptr, t1 = nullptr;
-    if (ctx->profiling) {
-        t0 = pool_event(ctx);
-        t1 = pool_event(ctx);
-        HIPCK(ctx, hipEventRecord(t0, ctx->s_main));
-    }
-    if ((rc = enqueue_eval(ctx, N, D, Np, nt))) return rc;
-    if (ctx->profiling) {
-        HIPCK(ctx, hipEventRecord(t1, ctx->s_main));
-        ctx->spans.push_back({3, t0, t1, 0});
-    }
+    ctx->slots.clear();
+    ctx->recording = prof;
+    rc = enqueue_eval(ctx, N, D, Np, nt);
+    ctx->recording = false;
+    if (rc) return rc;
     HIPCK(ctx, hipStreamSynchronize(ctx->s_main));
     *out = *ctx->hres;
-    if (ctx->profiling) {
-        ctx->stats.evals += 1;
-        collect_spans(ctx);
+    if (prof) {
+        rc = accumulate_slots(ctx, ctx->slots);
+        ctx->slots.clear();
     }
-    return 0;
+    return rc;
 }
 
 int finish(const EvalResult& r, double* out_logpdf, double* out_logdet, double* out_quad) {
@@ -470,6 +459,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     gaplac_ctx* ctx = new gaplac_ctx();
     ctx->device = device;
     if (const char* s = std::getenv("GAPLAC_SERIAL")) ctx->serial = s[0] == '1';
+    if (const char* s = std::getenv("GAPLAC_BULK")) ctx->bulk_valu = std::strcmp(s, "valu") == 0;
     auto fail = [&](const char* what, hipError_t e) {
         std::fprintf(stderr, "gaplac_ctx_create: %s: %s\n", what, hipGetErrorString(e));
         gaplac_ctx_destroy(ctx);
@@ -532,7 +522,6 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->s_main) (void)hipStreamSynchronize(ctx->s_main);
     if (ctx->s_panel) (void)hipStreamSynchronize(ctx->s_panel);
-    for (auto e : ctx->evpool) (void)hipEventDestroy(e);
     for (int q = 0; q < 2; ++q) {
         if (ctx->ev_P[q]) (void)hipEventDestroy(ctx->ev_P[q]);
         if (ctx->ev_R[q]) (void)hipEventDestroy(ctx->ev_R[q]);
@@ -545,7 +534,10 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     if (ctx->tiles) (void)hipFree(ctx->tiles);
     if (ctx->dX) (void)hipFree(ctx->dX);
     if (ctx->dv) (void)hipFree(ctx->dv);
-    drop_graph(ctx);
+    drop_graph(ctx, false);
+    drop_graph(ctx, true);
+    if (ctx->dkt) (void)hipFree(ctx->dkt);
+    if (ctx->hkt) (void)hipHostFree(ctx->hkt);
     if (ctx->dres) (void)hipFree(ctx->dres);
     if (ctx->dtp) (void)hipFree(ctx->dtp);
     if (ctx->htp) (void)hipHostFree(ctx->htp);
@@ -650,7 +642,7 @@ int gaplac_gram(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t 
     tp.noise = noise;
     *ctx->htp = tp;
     HIPCK(ctx, hipMemcpyAsync(ctx->dtp, ctx->htp, sizeof(TermPack), hipMemcpyHostToDevice, ctx->s_main));
-    launch_gram(ctx->s_main, ctx->A, Np, N, nt, ctx->dX, N, ctx->dv, ctx->dtp);
+    launch_gram(ctx->s_main, ctx->A, Np, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, nullptr);
     HIPCK(ctx, hipGetLastError());
     HIPCK(ctx, hipMemcpy2DAsync(out_C, (size_t)ldc * 8, ctx->A, (size_t)Np * 8, (size_t)N * 8,
                                 (size_t)N, hipMemcpyDeviceToHost, ctx->s_main));

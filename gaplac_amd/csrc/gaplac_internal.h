@@ -32,27 +32,36 @@ struct EvalResult {
     unsigned long long info;  // min over failing pivots of (j+1); ULLONG_MAX = none
 };
 
-// Launchers (gaplac_kernels.hip). A is the Np x Np column-major augmented matrix
+// Per-launch device timestamps (profiling): 100 MHz s_memrealtime ticks.
+struct KTime {
+    unsigned long long start;  // min over workgroups (init ~0)
+    unsigned long long end;    // max over waves (init 0)
+};
+
+// Launchers (gaplac_kernels.hip). Every launcher takes a KTime slot (nullptr = off).
+// A is the Np x Np column-major augmented matrix
 // (lda = Np, Np = roundup(N+1, NB)): rows/cols 0..N-1 hold C, row N holds v^T.
 void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt,
-                 const double* X, int64_t ldx, const double* v, const TermPack* dtp);
+                 const double* X, int64_t ldx, const double* v, const TermPack* dtp, KTime* kt);
 // Diagonal block k: L_kk in place + Dinv (DINV_ELEMS doubles: 8 column-major 16x16
 // inverses of L_kk's diagonal sub-blocks).
 void launch_potrf_diag(hipStream_t s, double* A, int64_t lda, int64_t N, int k,
-                       double* Dinv, EvalResult* res);
+                       double* Dinv, EvalResult* res, KTime* kt);
 // TRSM of the panel rows below diagonal block k: A[i,k] <- A[i,k] * L_kk^{-T}, i>k.
-void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Dinv);
+void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Dinv, KTime* kt);
 // Bulk trailing update: lower triangle of tile blocks jb..nt-1 minus the kdepth columns
 // starting at tile column k (kdepth 128 or 256). tiles: super-tile ordered list for the
 // m x m triangle, m = nt - jb (build_tile_list).
+// valu: 1 = v_fma_f64 register-tile kernel, 0 = fp64 MFMA kernel.
 void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int kdepth,
-                 const uint32_t* tiles);
+                 const uint32_t* tiles, int valu, KTime* kt);
 // Lookahead update of tile columns jb (and jb+1 if ncols == 2) with the kdepth columns
 // starting at tile column k.
 void launch_col_update(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int ncols,
-                       int kdepth);
+                       int kdepth, KTime* kt);
 void build_tile_list(int m, uint32_t* out);
 void launch_reduce(hipStream_t s, const double* A, int64_t lda, int64_t N, EvalResult* res);
+void launch_kt_reset(hipStream_t s, KTime* kt, int n);
 void launch_init_result(hipStream_t s, EvalResult* res);
 
 }  // namespace gaplac

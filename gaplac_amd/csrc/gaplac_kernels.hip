@@ -20,6 +20,17 @@ namespace gaplac {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+// Per-launch device timestamps (profiling only; kt == nullptr in production): first
+// workgroup start / last wave end on the 100 MHz s_memrealtime clock. HIP timing events
+// recorded inside a captured graph do not report elapsed times on ROCm 7.2, so the
+// per-kernel breakdown of a graph replay is measured in the kernels themselves.
+__device__ __forceinline__ void kt_begin(KTime* kt) {
+    if (kt && threadIdx.x == 0) atomicMin(&kt->start, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void kt_end(KTime* kt) {
+    if (kt && (threadIdx.x & 63) == 0) atomicMax(&kt->end, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
 // Row-major triangular tile index: t = bi*(bi+1)/2 + bj, 0 <= bj <= bi.
 __device__ __forceinline__ void tri_index(int64_t t, int& bi, int& bj) {
     int b = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
@@ -41,7 +52,7 @@ __device__ __forceinline__ void tri_index(int64_t t, int& bi, int& bj) {
 // (16-byte stores, a wave writes one 1 KiB column segment per instruction); the tile's
 // column coordinates are staged once in LDS and read as wave-wide broadcasts.
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void gram_kernel(double* __restrict__ A, int64_t lda,
+__device__ __forceinline__ void gram_kernel_body(double* __restrict__ A, int64_t lda,
                                                    int64_t N, const double* __restrict__ X,
                                                    int64_t ldx, const double* __restrict__ v,
                                                    const TermPack* __restrict__ tpp) {
@@ -136,6 +147,16 @@ __global__ __launch_bounds__(256) void gram_kernel(double* __restrict__ A, int64
         }
         *reinterpret_cast<double2*>(A + j * lda + i0) = make_double2(o0, o1);
     }
+}
+
+__global__ __launch_bounds__(256) void gram_kernel(double* __restrict__ A, int64_t lda,
+                                                   int64_t N, const double* __restrict__ X,
+                                                   int64_t ldx, const double* __restrict__ v,
+                                                   const TermPack* __restrict__ tpp,
+        KTime* __restrict__ kt) {
+    kt_begin(kt);
+    gram_kernel_body(A, lda, N, X, ldx, v, tpp);
+    kt_end(kt);
 }
 
 // ---------------------------------------------------------------------------------
@@ -262,7 +283,7 @@ __device__ __forceinline__ void dpanel(double* Ab, double* rdiag, int s, int lan
     }
 }
 
-__global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
+__device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ A, int64_t lda,
                                                          int64_t N, int k,
                                                          double* __restrict__ Dinv,
                                                          EvalResult* __restrict__ res) {
@@ -315,6 +336,16 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
     }
 }
 
+__global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
+                                                         int64_t N, int k,
+                                                         double* __restrict__ Dinv,
+                                                         EvalResult* __restrict__ res,
+        KTime* __restrict__ kt) {
+    kt_begin(kt);
+    potrf_diag_kernel_body(A, lda, N, k, Dinv, res);
+    kt_end(kt);
+}
+
 // ---------------------------------------------------------------------------------
 // Panel TRSM by blocked substitution: for each 128-row tile i > k of panel column k,
 //   X = B L_kk^{-T}:  X_b = (B_b - sum_{c<b} X_c L_bc^T) Dinv_b^T,  b = 0..7 (16 columns)
@@ -324,7 +355,7 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
 // 256 threads = 4 waves x 32 rows (two 16-row blocks, two interleaved MFMA chains).
 // L_kk and Dinv_k are read from global (L2-resident; just written by the diag kernel).
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void trsm_subst_kernel(double* __restrict__ A, int64_t lda, int k,
+__device__ __forceinline__ void trsm_subst_kernel_body(double* __restrict__ A, int64_t lda, int k,
                                                          const double* __restrict__ Dinv) {
     __builtin_amdgcn_s_setprio(2);  // critical path
     const int bi = k + 1 + (int)blockIdx.x;
@@ -371,6 +402,14 @@ __global__ __launch_bounds__(256) void trsm_subst_kernel(double* __restrict__ A,
     }
 }
 
+__global__ __launch_bounds__(256) void trsm_subst_kernel(double* __restrict__ A, int64_t lda, int k,
+                                                         const double* __restrict__ Dinv,
+        KTime* __restrict__ kt) {
+    kt_begin(kt);
+    trsm_subst_kernel_body(A, lda, k, Dinv);
+    kt_end(kt);
+}
+
 // ---------------------------------------------------------------------------------
 // 128x128 fp64 MFMA tile kernel, K = kdepth (128: one panel; 256: a super-panel of two).
 //   MODE 0 (SYRK): C(bi,bj) -= P_bi * P_bj^T, P = the kdepth columns starting at k*NB.
@@ -392,7 +431,7 @@ constexpr int KB = 16;
 constexpr int LR = NB + 16;  // LDS k-row stride: lanes 16..31 land on banks 32..63
 
 template <int MODE>
-__global__ __launch_bounds__(256, 2) void tile_gemm_kernel(double* __restrict__ A, int64_t lda,
+__device__ __forceinline__ void tile_gemm_kernel_body(double* __restrict__ A, int64_t lda,
                                                            int k, int jb, int colmode,
                                                            const double* __restrict__ Linv,
                                                            const uint32_t* __restrict__ tiles,
@@ -511,6 +550,108 @@ __global__ __launch_bounds__(256, 2) void tile_gemm_kernel(double* __restrict__ 
     }
 }
 
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void tile_gemm_kernel(double* __restrict__ A, int64_t lda,
+                                                           int k, int jb, int colmode,
+                                                           const double* __restrict__ Linv,
+                                                           const uint32_t* __restrict__ tiles,
+                                                           int ntiles, int kdepth,
+        KTime* __restrict__ kt) {
+    kt_begin(kt);
+    tile_gemm_kernel_body<MODE>(A, lda, k, jb, colmode, Linv, tiles, ntiles, kdepth);
+    kt_end(kt);
+}
+
+// ---------------------------------------------------------------------------------
+// VALU variant of the bulk trailing update (same tiles, same list, same K): each thread
+// owns an 8x8 register tile (rows tx+16i, columns ty+16j of the 128x128 tile), operands
+// broadcast from LDS (8 + 8 ds_read_b64 per k, conflict-free: 16 consecutive doubles per
+// read), 64 v_fma_f64 per k. Measured fp64 ceilings on MI355X (tools/mfma_f64_rate.hip):
+// v_fma_f64 61.5 TFLOP/s vs v_mfma_f64_16x16x4f64 47.5 TFLOP/s, so the vector pipe is the
+// faster fp64 engine on this part; GAPLAC_BULK selects the kernel.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ void tile_valu_kernel_body(double* __restrict__ A, int64_t lda, int k,
+                                                           int jb, const uint32_t* __restrict__ tiles,
+                                                           int ntiles, int kdepth) {
+    __shared__ double sm[2][2][KB][LR];
+    const int b = (int)blockIdx.x;
+    const int chunk = (ntiles + 7) >> 3;
+    const int idx = (b & 7) * chunk + (b >> 3);
+    if (idx >= ntiles) return;
+    const uint32_t tv = tiles[idx];
+    const int bi = jb + (int)(tv & 0xffffu), bj = jb + (int)(tv >> 16);
+    const int64_t r0 = (int64_t)bi * NB, c0 = (int64_t)bj * NB, k0 = (int64_t)k * NB;
+    const double* P = A + k0 * lda + r0;
+    const double* Q = A + k0 * lda + c0;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int tx = tid & 15, ty = tid >> 4;
+    double acc[8][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const double* Cj = A + (c0 + ty + 16 * j) * lda + r0 + tx;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i][j] = Cj[16 * i];
+    }
+    double2 pp[4], pq[4];
+    const int krow = tid >> 6;
+    auto gload = [&](int ch) {
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int64_t col = (int64_t)ch * KB + krow + 4 * it;
+            pp[it] = *reinterpret_cast<const double2*>(P + col * lda + 2 * lane);
+            pq[it] = *reinterpret_cast<const double2*>(Q + col * lda + 2 * lane);
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int kk = krow + 4 * it;
+            double2 v = pp[it];
+            v.x = -v.x;
+            v.y = -v.y;
+            *reinterpret_cast<double2*>(&sm[buf][0][kk][2 * lane]) = v;
+            *reinterpret_cast<double2*>(&sm[buf][1][kk][2 * lane]) = pq[it];
+        }
+    };
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    const int NCH = kdepth / KB;
+    for (int ch = 0; ch < NCH; ++ch) {
+        const int buf = ch & 1;
+        if (ch + 1 < NCH) gload(ch + 1);
+#pragma unroll 4
+        for (int kk = 0; kk < KB; ++kk) {
+            double a[8], q[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) a[i] = sm[buf][0][kk][tx + 16 * i];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) q[j] = sm[buf][1][kk][ty + 16 * j];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[i][j] = fma(a[i], q[j], acc[i][j]);
+        }
+        if (ch + 1 < NCH) lstore(buf ^ 1);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        double* Cj = A + (c0 + ty + 16 * j) * lda + r0 + tx;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) Cj[16 * i] = acc[i][j];
+    }
+}
+
+__global__ __launch_bounds__(256, 2) void tile_valu_kernel(double* __restrict__ A, int64_t lda, int k,
+                                                           int jb, const uint32_t* __restrict__ tiles,
+                                                           int ntiles, int kdepth,
+        KTime* __restrict__ kt) {
+    kt_begin(kt);
+    tile_valu_kernel_body(A, lda, k, jb, tiles, ntiles, kdepth);
+    kt_end(kt);
+}
+
 // ---------------------------------------------------------------------------------
 // Lookahead column update (critical path): C(i, jb) -= P_i P_jb^T for the tiles i >= jb
 // of one or two tile columns, K = kdepth (128 or 256), split into 64x64 quadrants so a column of m tiles runs as
@@ -519,7 +660,7 @@ __global__ __launch_bounds__(256, 2) void tile_gemm_kernel(double* __restrict__ 
 // fragments are read straight from global (the panel column was just written and is
 // L2-resident), no LDS, no barriers. The upper quadrant of the diagonal tile is skipped.
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void col_update_kernel(double* __restrict__ A, int64_t lda, int k,
+__device__ __forceinline__ void col_update_kernel_body(double* __restrict__ A, int64_t lda, int k,
                                                          int jb0, int m0, int kdepth) {
     __builtin_amdgcn_s_setprio(2);  // critical path
     const int q = (int)blockIdx.x & 3;
@@ -566,6 +707,14 @@ __global__ __launch_bounds__(256) void col_update_kernel(double* __restrict__ A,
                 A[(cj + 16 * mj + fr + 4 * rg) * lda + ri + 16 * mi + fc] = acc[mi][mj][rg];
 }
 
+__global__ __launch_bounds__(256) void col_update_kernel(double* __restrict__ A, int64_t lda, int k,
+                                                         int jb0, int m0, int kdepth,
+        KTime* __restrict__ kt) {
+    kt_begin(kt);
+    col_update_kernel_body(A, lda, k, jb0, m0, kdepth);
+    kt_end(kt);
+}
+
 // ---------------------------------------------------------------------------------
 // logdet / quad / logpdf (AbstractGPs.logpdf: -((N*log2pi + logdet) + quad) / 2).
 // Fixed-order tree reduction: deterministic across runs.
@@ -602,6 +751,18 @@ __global__ __launch_bounds__(1024) void reduce_kernel(const double* __restrict__
     }
 }
 
+__global__ void kt_reset_kernel(KTime* kt, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        kt[i].start = ~0ull;
+        kt[i].end = 0ull;
+    }
+}
+
+void launch_kt_reset(hipStream_t s, KTime* kt, int n) {
+    if (n > 0) kt_reset_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s>>>(kt, n);
+}
+
 __global__ void init_result_kernel(EvalResult* res) {
     res->logpdf = 0.0;
     res->logdet = 0.0;
@@ -611,38 +772,41 @@ __global__ void init_result_kernel(EvalResult* res) {
 
 // ------------------------------- launchers ---------------------------------------
 void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const double* X,
-                 int64_t ldx, const double* v, const TermPack* dtp) {
+                 int64_t ldx, const double* v, const TermPack* dtp, KTime* kt) {
     const int64_t ntiles = (int64_t)nt * (nt + 1) / 2;
-    gram_kernel<<<dim3((unsigned)ntiles), dim3(256), 0, s>>>(A, lda, N, X, ldx, v, dtp);
+    gram_kernel<<<dim3((unsigned)ntiles), dim3(256), 0, s>>>(A, lda, N, X, ldx, v, dtp, kt);
 }
 
 void launch_potrf_diag(hipStream_t s, double* A, int64_t lda, int64_t N, int k, double* Dinv,
-                       EvalResult* res) {
-    potrf_diag_kernel<<<dim3(1), dim3(256), 0, s>>>(A, lda, N, k, Dinv, res);
+                       EvalResult* res, KTime* kt) {
+    potrf_diag_kernel<<<dim3(1), dim3(256), 0, s>>>(A, lda, N, k, Dinv, res, kt);
 }
 
-void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Dinv) {
+void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Dinv, KTime* kt) {
     const int n = nt - k - 1;
     if (n <= 0) return;
-    trsm_subst_kernel<<<dim3(n), dim3(256), 0, s>>>(A, lda, k, Dinv);
+    trsm_subst_kernel<<<dim3(n), dim3(256), 0, s>>>(A, lda, k, Dinv, kt);
 }
 
 void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int kdepth,
-                 const uint32_t* tiles) {
+                 const uint32_t* tiles, int valu, KTime* kt) {
     const int m = nt - jb;
     if (m <= 0) return;
     const int ntiles = m * (m + 1) / 2;
     const int grid = ((ntiles + 7) >> 3) << 3;
-    tile_gemm_kernel<0><<<dim3((unsigned)grid), dim3(256), 0, s>>>(A, lda, k, jb, 0, nullptr, tiles, ntiles,
-                                                                    kdepth);
+    if (valu)
+        tile_valu_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(A, lda, k, jb, tiles, ntiles, kdepth, kt);
+    else
+        tile_gemm_kernel<0><<<dim3((unsigned)grid), dim3(256), 0, s>>>(A, lda, k, jb, 0, nullptr, tiles,
+                                                                        ntiles, kdepth, kt);
 }
 
 void launch_col_update(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int ncols,
-                       int kdepth) {
+                       int kdepth, KTime* kt) {
     const int m0 = nt - jb;
     if (m0 <= 0) return;
     const int tiles = ncols == 2 && m0 > 1 ? 2 * m0 - 1 : m0;
-    col_update_kernel<<<dim3((unsigned)(4 * tiles)), dim3(256), 0, s>>>(A, lda, k, jb, m0, kdepth);
+    col_update_kernel<<<dim3((unsigned)(4 * tiles)), dim3(256), 0, s>>>(A, lda, k, jb, m0, kdepth, kt);
 }
 
 // Super-tile ordered list of the lower-triangular m x m tile set (entry = bi | bj << 16,
