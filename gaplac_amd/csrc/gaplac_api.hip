@@ -24,7 +24,7 @@ struct gaplac_ctx {
     int device = 0;
     hipStream_t s_main = nullptr, s_panel = nullptr;
     int diag_cus = 0;  // CUs masked out of s_main for the diagonal kernel (0: no mask)
-    hipEvent_t ev_P[2] = {}, ev_R[2] = {}, ev_C[2] = {}, ev_D[2] = {}, ev_gram = nullptr;
+    hipEvent_t ev_P[2] = {}, ev_R[2] = {}, ev_C[2] = {}, ev_D[2] = {}, ev_gram = nullptr, ev_gram2 = nullptr;
     double* A = nullptr;
     size_t A_elems = 0;
     double* Dinv = nullptr;  // per diagonal block: 8 inverses of its 16x16 sub-blocks
@@ -48,6 +48,7 @@ struct gaplac_ctx {
     bool profiling = false;
     bool serial = false;  // GAPLAC_SERIAL=1: one stream, no overlap (per-kernel timing)
     int bulk_valu = 0;    // GAPLAC_BULK=valu: v_fma_f64 bulk-update kernel instead of MFMA
+    int spw = 4;          // GAPLAC_SPW: super-panel width in 128-column tiles (bulk K = 128 spw)
     gaplac_stats stats{};
     struct Slot {
         int kind;  // 0 bulk syrk, 1 gram, 2 diag, 4 trsm, 5 column update
@@ -232,24 +233,29 @@ int accumulate_slots(gaplac_ctx* ctx, const std::vector<gaplac_ctx::Slot>& slots
 
 // Factor the augmented matrix already built in ctx->A (Gram launched on s_main).
 //
-// Super-panels of two 128-wide tile columns (p covers tile columns 2p, 2p+1): the panel
-// chain factors 128-wide blocks, the bulk trailing update applies a whole super-panel at
-// once (K = 256), halving the C-tile read/write traffic and tile prologues per flop.
+// Super-panels of W 128-wide tile columns (SP p covers tile columns pW .. pW+W-1,
+// GAPLAC_SPW, default 4): the panel chain factors 128-wide blocks, the bulk trailing
+// update applies a whole super-panel at once (K = 128 W). Measured per 128x128 tile:
+// ~10 us fixed (C load, first staging, epilogue) + K at the MFMA ceiling, so larger K
+// amortises the fixed part (and cuts C-tile HBM traffic per flop by W).
 //
 // Two streams. s_panel (highest priority, all CUs) runs the critical path in order;
 // s_main (CU-masked when available: GAPLAC_DIAG_CUS CUs, default 1, excluded) runs the
 // bulk updates. In eager mode the excluded CU keeps a free slot for the diagonal kernel;
 // in graph mode (default) the kernels are slot-compatible anyway.
-//   s_panel: wait R(p-1) | col_update(columns of SP p+1, with SP p, K=256)
-//            | potrf(2p+2) trsm(2p+2) col_update(2p+3 with panel 2p+2) potrf(2p+3) trsm(2p+3)
+//   s_panel: wait R(p-1) | col_update(columns of SP p+1, with SP p, K=128W)
+//            | for each column c of SP p+1: [col_update(c with c-1..first, K=128)] potrf(c) trsm(c)
 //            | rec P(p+1)
-//   s_main : wait P(p)   | syrk_tri(tile columns >= 2p+4, with SP p, K=256) | rec R(p)
-// Columns of SP p+1 receive SP p-1 in R(p-1) and SP p in the lookahead col_update; within
-// a step the streams touch disjoint tile columns. Events ping-pong (p & 1).
+//   s_main : wait P(p)   | syrk_tri(tile columns >= (p+2)W, with SP p, K=128W) | rec R(p)
+// Within SP p+1 the chain is right-looking with K=128 column updates (each column gets
+// the previous columns of its own super-panel). Columns of SP p+1 receive SP p-1 in
+// R(p-1) and SP p in the lookahead col_update; within a step the streams touch disjoint
+// tile columns. Events ping-pong (p & 1).
 void factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, int nt, int p) {
-    const int c0 = 2 * p, c1 = std::min(2 * p + 2, nt);
+    const int W = ctx->spw;
+    const int c0 = W * p, c1 = std::min(W * p + W, nt);
     for (int c = c0; c < c1; ++c) {
-        if (c > c0) launch_col_update(sp, ctx->A, lda, nt, c - 1, c, 1, NB, slot(ctx, 5, 0));
+        if (c > c0) launch_col_update(sp, ctx->A, lda, nt, c - 1, c, c1 - c, NB, slot(ctx, 5, 0));
         double* Dk = ctx->Dinv + (size_t)c * DINV_PER_BLOCK;
         if ((int64_t)c * NB < N) launch_potrf_diag(sp, ctx->A, lda, N, c, Dk, ctx->dres, slot(ctx, 2, 0));
         launch_trsm(sp, ctx->A, lda, nt, c, Dk, slot(ctx, 4, 0));
@@ -259,23 +265,26 @@ void factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, 
 int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     hipStream_t sm = ctx->s_main;
     hipStream_t sp = ctx->serial ? sm : ctx->s_panel;
-    const int nsp = (nt + 1) / 2;
-    HIPCK(ctx, hipEventRecord(ctx->ev_gram, sm));
-    HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_gram, 0));
+    const int W = ctx->spw;
+    const int nsp = (nt + W - 1) / W;
+    HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_gram, 0));  // first W tile columns built
     factor_superpanel(ctx, sp, N, lda, nt, 0);
     HIPCK(ctx, hipEventRecord(ctx->ev_P[0], sp));
     for (int p = 0; p < nsp; ++p) {
-        const int c0 = 2 * p;
-        const int kd = (std::min(2 * p + 2, nt) - c0) * NB;  // depth of super-panel p
+        const int c0 = W * p;
+        const int kd = (std::min(c0 + W, nt) - c0) * NB;  // depth of super-panel p
         if (p + 1 < nsp) {
-            if (p >= 1) HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_R[(p - 1) & 1], 0));
-            const int ncols = std::min(2 * p + 4, nt) - (c0 + 2);
-            launch_col_update(sp, ctx->A, lda, nt, c0, c0 + 2, ncols, kd, slot(ctx, 5, 0));
+            if (p >= 1)
+                HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_R[(p - 1) & 1], 0));
+            else
+                HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_gram2, 0));  // rest of the Gram built
+            const int ncols = std::min(c0 + 2 * W, nt) - (c0 + W);
+            launch_col_update(sp, ctx->A, lda, nt, c0, c0 + W, ncols, kd, slot(ctx, 5, 0));
             factor_superpanel(ctx, sp, N, lda, nt, p + 1);
             HIPCK(ctx, hipEventRecord(ctx->ev_P[(p + 1) & 1], sp));
         }
         HIPCK(ctx, hipStreamWaitEvent(sm, ctx->ev_P[p & 1], 0));
-        const int jb = c0 + 4;
+        const int jb = c0 + 2 * W;
         if (jb < nt)
             launch_syrk(sm, ctx->A, lda, nt, c0, jb, kd, ctx->tiles + ctx->tile_off[(size_t)(nt - jb)],
                         ctx->bulk_valu, slot(ctx, 0, syrk_flops(nt - jb) * (kd / NB)));
@@ -309,8 +318,16 @@ int ensure_tile_lists(gaplac_ctx* ctx, int nt) {
 int enqueue_eval(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt) {
     launch_init_result(ctx->s_main, ctx->dres);
     if (ctx->recording) launch_kt_reset(ctx->s_main, ctx->dkt, (int)ctx->kt_cap);
+    // Gram in two launches: the first super-panel's tile columns, then the rest (the panel
+    // chain starts on the first part while the second is still being written).
     const double bytes = 8.0 * (double)Np * (double)(Np + 1) / 2.0 + 8.0 * (double)N * (D + 1);
-    launch_gram(ctx->s_main, ctx->A, Np, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, slot(ctx, 1, bytes));
+    const double frac = nt > 0 ? 1.0 - (double)(nt - ctx->spw) * (nt - ctx->spw + 1) / ((double)nt * (nt + 1)) : 1.0;
+    launch_gram(ctx->s_main, ctx->A, Np, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 1, ctx->spw,
+                slot(ctx, 1, bytes * frac));
+    HIPCK(ctx, hipEventRecord(ctx->ev_gram, ctx->s_main));
+    launch_gram(ctx->s_main, ctx->A, Np, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 2, ctx->spw,
+                slot(ctx, 1, bytes * (1.0 - frac)));
+    HIPCK(ctx, hipEventRecord(ctx->ev_gram2, ctx->s_main));
     int rc;
     if ((rc = factor_and_reduce(ctx, N, Np, nt))) return rc;
     HIPCK(ctx, hipMemcpyAsync(ctx->hres, ctx->dres, sizeof(EvalResult), hipMemcpyDeviceToHost,
@@ -460,6 +477,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     ctx->device = device;
     if (const char* s = std::getenv("GAPLAC_SERIAL")) ctx->serial = s[0] == '1';
     if (const char* s = std::getenv("GAPLAC_BULK")) ctx->bulk_valu = std::strcmp(s, "valu") == 0;
+    if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
     auto fail = [&](const char* what, hipError_t e) {
         std::fprintf(stderr, "gaplac_ctx_create: %s: %s\n", what, hipGetErrorString(e));
         gaplac_ctx_destroy(ctx);
@@ -504,6 +522,8 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     }
     if ((e = hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming)) != hipSuccess)
         return fail("event", e);
+    if ((e = hipEventCreateWithFlags(&ctx->ev_gram2, hipEventDisableTiming)) != hipSuccess)
+        return fail("event", e);
     if ((e = hipMalloc(reinterpret_cast<void**>(&ctx->dres), sizeof(EvalResult))) != hipSuccess)
         return fail("hipMalloc", e);
     if ((e = hipHostMalloc(reinterpret_cast<void**>(&ctx->hres), sizeof(EvalResult), 0)) != hipSuccess)
@@ -529,6 +549,7 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
         if (ctx->ev_D[q]) (void)hipEventDestroy(ctx->ev_D[q]);
     }
     if (ctx->ev_gram) (void)hipEventDestroy(ctx->ev_gram);
+    if (ctx->ev_gram2) (void)hipEventDestroy(ctx->ev_gram2);
     if (ctx->A) (void)hipFree(ctx->A);
     if (ctx->Dinv) (void)hipFree(ctx->Dinv);
     if (ctx->tiles) (void)hipFree(ctx->tiles);
@@ -642,7 +663,7 @@ int gaplac_gram(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t 
     tp.noise = noise;
     *ctx->htp = tp;
     HIPCK(ctx, hipMemcpyAsync(ctx->dtp, ctx->htp, sizeof(TermPack), hipMemcpyHostToDevice, ctx->s_main));
-    launch_gram(ctx->s_main, ctx->A, Np, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, nullptr);
+    launch_gram(ctx->s_main, ctx->A, Np, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 0, 0, nullptr);
     HIPCK(ctx, hipGetLastError());
     HIPCK(ctx, hipMemcpy2DAsync(out_C, (size_t)ldc * 8, ctx->A, (size_t)Np * 8, (size_t)N * 8,
                                 (size_t)N, hipMemcpyDeviceToHost, ctx->s_main));

@@ -41,8 +41,11 @@ struct KTime {
 // Launchers (gaplac_kernels.hip). Every launcher takes a KTime slot (nullptr = off).
 // A is the Np x Np column-major augmented matrix
 // (lda = Np, Np = roundup(N+1, NB)): rows/cols 0..N-1 hold C, row N holds v^T.
+// part 0: all lower tiles; part 1: the first w tile columns; part 2: tiles with both
+// block indices >= w (parts 1 + 2 = part 0).
 void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt,
-                 const double* X, int64_t ldx, const double* v, const TermPack* dtp, KTime* kt);
+                 const double* X, int64_t ldx, const double* v, const TermPack* dtp, int part, int w,
+                 KTime* kt);
 // Diagonal block k: L_kk in place + Dinv (DINV_ELEMS doubles: 8 column-major 16x16
 // inverses of L_kk's diagonal sub-blocks).
 void launch_potrf_diag(hipStream_t s, double* A, int64_t lda, int64_t N, int k,

@@ -24,6 +24,22 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // workgroup start / last wave end on the 100 MHz s_memrealtime clock. HIP timing events
 // recorded inside a captured graph do not report elapsed times on ROCm 7.2, so the
 // per-kernel breakdown of a graph replay is measured in the kernels themselves.
+// Diagnostic build only (-DGAPLAC_STAMPS, tools/diag_probe.hip): phase stamps of the
+// diagonal kernel into a debug array; never compiled into the library.
+#ifdef GAPLAC_STAMPS
+__device__ unsigned long long g_stamps[64];
+#define STAMP(i)                                                                        \
+    do {                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        if (threadIdx.x == 0) g_stamps[i] = __builtin_amdgcn_s_memtime();               \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+    } while (0)
+#else
+#define STAMP(i) \
+    do {         \
+    } while (0)
+#endif
+
 __device__ __forceinline__ void kt_begin(KTime* kt) {
     if (kt && threadIdx.x == 0) atomicMin(&kt->start, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
@@ -55,11 +71,24 @@ __device__ __forceinline__ void tri_index(int64_t t, int& bi, int& bj) {
 __device__ __forceinline__ void gram_kernel_body(double* __restrict__ A, int64_t lda,
                                                    int64_t N, const double* __restrict__ X,
                                                    int64_t ldx, const double* __restrict__ v,
-                                                   const TermPack* __restrict__ tpp) {
+                                                   const TermPack* __restrict__ tpp, int nt,
+                                                   int part, int w0) {
     const TermPack& tp = *tpp;  // uniform: scalar loads (device copy refreshed per eval)
     const double noise = tp.noise;
     int bi, bj;
-    tri_index(blockIdx.x, bi, bj);
+    if (part == 1) {  // strip of the first w0 tile columns (the first super-panel)
+        int t = (int)blockIdx.x;
+        bj = 0;
+        while (t >= nt - bj) {
+            t -= nt - bj;
+            ++bj;
+        }
+        bi = bj + t;
+    } else {  // lower triangle of tile blocks w0..nt-1 (part 2), or everything (w0 = 0)
+        tri_index(blockIdx.x, bi, bj);
+        bi += w0;
+        bj += w0;
+    }
     const int64_t r0 = (int64_t)bi * NB, c0 = (int64_t)bj * NB;
     __shared__ double xcol[GAPLAC_MAX_TERMS][NB];
     __shared__ double vcol[NB];
@@ -152,10 +181,10 @@ __device__ __forceinline__ void gram_kernel_body(double* __restrict__ A, int64_t
 __global__ __launch_bounds__(256) void gram_kernel(double* __restrict__ A, int64_t lda,
                                                    int64_t N, const double* __restrict__ X,
                                                    int64_t ldx, const double* __restrict__ v,
-                                                   const TermPack* __restrict__ tpp,
+                                                   const TermPack* __restrict__ tpp, int nt, int part, int w,
         KTime* __restrict__ kt) {
     kt_begin(kt);
-    gram_kernel_body(A, lda, N, X, ldx, v, tpp);
+    gram_kernel_body(A, lda, N, X, ldx, v, tpp, nt, part, w);
     kt_end(kt);
 }
 
@@ -230,8 +259,12 @@ __device__ __forceinline__ void dinv_diag(const double* Ab, double* __restrict__
 }
 
 // Wave-level factorisation of panel s: rows 16s..127 x 16 columns, two rows per lane.
-__device__ __forceinline__ void dpanel(double* Ab, double* rdiag, int s, int lane, int64_t gcol0,
-                                       int64_t N, EvalResult* res) {
+// Per column: the pivot comes from its lane by v_readlane; the owners of the panel's
+// 16 diagonal rows (lanes 0..7) publish the scaled column in a wave-private LDS vector
+// and every lane reads it back with 8 ds_read_b128 (in-order LDS within one wave; the
+// waitcnt orders write and read), then applies the rank-1 update to its two rows.
+__device__ __forceinline__ void dpanel(double* Ab, double* rdiag, double* colbuf, int s, int lane,
+                                       int64_t gcol0, int64_t N, EvalResult* res) {
     const int R0 = 16 * s;
     const int rel0 = 2 * lane, rel1 = rel0 + 1;
     const int row0 = R0 + rel0;
@@ -267,11 +300,22 @@ __device__ __forceinline__ void dpanel(double* Ab, double* rdiag, int s, int lan
         if (lane == 0) rdiag[R0 + c] = rd;
         v0[c] = rel0 > c ? v0[c] * rd : (rel0 == c ? d : v0[c]);
         v1[c] = rel1 > c ? v1[c] * rd : (rel1 == c ? d : v1[c]);
+        if (c < 15) {
+            if (lane < 8) *reinterpret_cast<double2*>(&colbuf[2 * lane]) = make_double2(v0[c], v1[c]);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            double lc[16];
 #pragma unroll
-        for (int c2 = c + 1; c2 < 16; ++c2) {
-            const double lc = readlane_d((c2 & 1) ? v1[c] : v0[c], c2 >> 1);  // L[R0+c2][c]
-            v0[c2] -= v0[c] * lc;
-            v1[c2] -= v1[c] * lc;
+            for (int q = 0; q < 8; ++q) {
+                const double2 w = *reinterpret_cast<const double2*>(&colbuf[2 * q]);
+                lc[2 * q] = w.x;
+                lc[2 * q + 1] = w.y;
+            }
+#pragma unroll
+            for (int c2 = c + 1; c2 < 16; ++c2) {
+                v0[c2] -= v0[c] * lc[c2];
+                v1[c2] -= v1[c] * lc[c2];
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next write
         }
     }
     if (live) {
@@ -289,7 +333,9 @@ __device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ A, i
                                                          EvalResult* __restrict__ res) {
     __shared__ double Ab[NPK * 256];
     __shared__ double rdiag[NB];
+    __shared__ double colbuf[16];
     __builtin_amdgcn_s_setprio(3);  // critical path: win issue arbitration on shared SIMDs
+    STAMP(20);
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const int64_t g0 = (int64_t)k * NB;
     double* Ag = A + g0 * lda + g0;
@@ -303,14 +349,17 @@ __device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ A, i
                 Ab[bidx(I, J) * 256 + t] = Ag[(int64_t)(16 * J + c) * lda + 16 * I + r];
     }
     __syncthreads();
+    STAMP(0);
     for (int s = 0; s < NDB; ++s) {
         if (s >= 1) {
             for (int I = s + wave; I < NDB; I += 4) dblk_update(Ab, I, s, s - 1, lane);
         }
         __syncthreads();
+        STAMP(1 + 2 * s);
         if (wave == 0) {
-            dpanel(Ab, rdiag, s, lane, g0, N, res);
+            dpanel(Ab, rdiag, colbuf, s, lane, g0, N, res);
         } else if (s >= 1) {
+            if (wave == 3) dinv_diag(Ab, Dinv, rdiag, s - 1, lane);  // off the barrier path
             const int ntr = (NDB - 1 - s) * (NDB - s) / 2;  // tiles (I,J), s+1 <= J <= I <= 7
             for (int task = wave - 1; task < ntr; task += 3) {
                 int J = s + 1, rem = task;
@@ -321,10 +370,12 @@ __device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ A, i
                 dblk_update(Ab, J + rem, J, s - 1, lane);
             }
         }
+        if (wave == 0) STAMP(2 + 2 * s);
         __syncthreads();
     }
-    dinv_diag(Ab, Dinv, rdiag, wave, lane);
-    dinv_diag(Ab, Dinv, rdiag, wave + 4, lane);
+    STAMP(17);
+    if (wave == 3) dinv_diag(Ab, Dinv, rdiag, NDB - 1, lane);
+    STAMP(18);
     // write L (lower incl. diagonal) in place
     {
         const int c = t >> 4, r = t & 15;
@@ -334,6 +385,7 @@ __device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ A, i
             for (int J = 0; J <= I; ++J)
                 if (I != J || r >= c) Ag[(int64_t)(16 * J + c) * lda + 16 * I + r] = Ab[bidx(I, J) * 256 + t];
     }
+    STAMP(19);
 }
 
 __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
@@ -653,33 +705,28 @@ __global__ __launch_bounds__(256, 2) void tile_valu_kernel(double* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------
-// Lookahead column update (critical path): C(i, jb) -= P_i P_jb^T for the tiles i >= jb
-// of one or two tile columns, K = kdepth (128 or 256), split into 64x64 quadrants so a column of m tiles runs as
-// ~4m short workgroups (the bulk SYRK's 128x128 tiles take ~25 us each alone on a CU;
-// a quadrant ~4x less). 4 waves as 2x2 of 32x32 (2x2 f64 MFMA accumulators each);
-// fragments are read straight from global (the panel column was just written and is
-// L2-resident), no LDS, no barriers. The upper quadrant of the diagonal tile is skipped.
+// Quadrant update: C_q -= P_q Q_q^T for one 64x64 quadrant (qi, qj) of tile (bi, bj),
+// K = kdepth columns starting at tile column k. 4 waves as 2x2 of 32x32 (2x2 f64 MFMA
+// accumulators each); fragments come straight from global memory (the panel columns are
+// L2-resident), register double-buffered 8 k-steps (32 columns) ahead, no LDS, no
+// barriers. Used where latency matters more than throughput: the lookahead column
+// update on the critical path and the small trailing updates at the end of the
+// factorisation (a 128x128x256 tile alone on a CU takes ~50 us; a quadrant ~4x less).
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ void col_update_kernel_body(double* __restrict__ A, int64_t lda, int k,
-                                                         int jb0, int m0, int kdepth) {
-    __builtin_amdgcn_s_setprio(2);  // critical path
-    const int q = (int)blockIdx.x & 3;
-    int t = (int)blockIdx.x >> 2, jb = jb0;
-    if (t >= m0) {  // second tile column (super-panel lookahead updates two)
-        t -= m0;
-        jb = jb0 + 1;
-    }
-    const int bi = jb + t;
-    const int qi = q >> 1, qj = q & 1;
-    if (bi == jb && qj > qi) return;
+constexpr int QG = 8;  // k-steps per prefetch group
+// Bulk updates with at most this many 128x128 tiles run as quadrants (4 WGs per tile).
+constexpr int QUAD_BULK_MAX_TILES = 512;
+
+__device__ __forceinline__ void quad_update(double* __restrict__ A, int64_t lda, int k, int bi, int bj,
+                                            int qi, int qj, int kdepth) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wi = wave & 1, wj = wave >> 1;
     const int fr = lane >> 4, fc = lane & 15;
     const int64_t k0 = (int64_t)k * NB;
     const int64_t ri = (int64_t)bi * NB + 64 * qi + 32 * wi;  // this wave's 32 rows
-    const int64_t cj = (int64_t)jb * NB + 64 * qj + 32 * wj;  // this wave's 32 columns
-    const double* P = A + k0 * lda + ri;
-    const double* Q = A + k0 * lda + cj;
+    const int64_t cj = (int64_t)bj * NB + 64 * qj + 32 * wj;  // this wave's 32 columns
+    const double* P = A + k0 * lda + ri + fc;
+    const double* Q = A + k0 * lda + cj + fc;
     d4 acc[2][2];
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
@@ -688,15 +735,36 @@ __device__ __forceinline__ void col_update_kernel_body(double* __restrict__ A, i
 #pragma unroll
             for (int rg = 0; rg < 4; ++rg)
                 acc[mi][mj][rg] = A[(cj + 16 * mj + fr + 4 * rg) * lda + ri + 16 * mi + fc];
-#pragma unroll 8
-    for (int ks = 0; ks < kdepth; ks += 4) {
-        const int64_t col = (int64_t)(ks + fr) * lda;
-        const double b0 = -P[col + fc], b1 = -P[col + 16 + fc];
-        const double a0 = Q[col + fc], a1 = Q[col + 16 + fc];
-        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[1][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[0][1], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    double fa[2][QG][2], fb[2][QG][2];  // [buffer][k-step][16-block]
+    auto load = [&](int buf, int g) {
+#pragma unroll
+        for (int s = 0; s < QG; ++s) {
+            const int64_t col = (int64_t)(g * 4 * QG + 4 * s + fr) * lda;
+            fb[buf][s][0] = P[col];
+            fb[buf][s][1] = P[col + 16];
+            fa[buf][s][0] = Q[col];
+            fa[buf][s][1] = Q[col + 16];
+        }
+    };
+    auto compute = [&](int buf) {
+#pragma unroll
+        for (int s = 0; s < QG; ++s) {
+            const double b0 = -fb[buf][s][0], b1 = -fb[buf][s][1];
+            acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][s][0], b0, acc[0][0], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][s][0], b1, acc[1][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][s][1], b0, acc[0][1], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][s][1], b1, acc[1][1], 0, 0, 0);
+        }
+    };
+    const int ng = kdepth / (4 * QG);  // 4 (K=128) or 8 (K=256)
+    load(0, 0);
+    for (int g = 0; g < ng; g += 2) {
+        if (g + 1 < ng) load(1, g + 1);
+        compute(0);
+        if (g + 1 < ng) {
+            if (g + 2 < ng) load(0, g + 2);
+            compute(1);
+        }
     }
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
@@ -707,11 +775,39 @@ __device__ __forceinline__ void col_update_kernel_body(double* __restrict__ A, i
                 A[(cj + 16 * mj + fr + 4 * rg) * lda + ri + 16 * mi + fc] = acc[mi][mj][rg];
 }
 
+// Lookahead column update (critical path): tiles i >= jb of tile columns jb0 .. jb0+ncols-1
+// (the next super-panel's columns), K = kdepth.
 __global__ __launch_bounds__(256) void col_update_kernel(double* __restrict__ A, int64_t lda, int k,
                                                          int jb0, int m0, int kdepth,
-        KTime* __restrict__ kt) {
+                                                         KTime* __restrict__ kt) {
     kt_begin(kt);
-    col_update_kernel_body(A, lda, k, jb0, m0, kdepth);
+    __builtin_amdgcn_s_setprio(2);
+    const int q = (int)blockIdx.x & 3;
+    int t = (int)blockIdx.x >> 2, jb = jb0;
+    for (int mc = m0; t >= mc && mc > 0; --mc) {  // tile column jb0 + c holds m0 - c tiles
+        t -= mc;
+        ++jb;
+    }
+    const int bi = jb + t, qi = q >> 1, qj = q & 1;
+    if (!(bi == jb && qj > qi)) quad_update(A, lda, k, bi, jb, qi, qj, kdepth);
+    kt_end(kt);
+}
+
+// Small bulk trailing updates: the same tile list as tile_gemm_kernel, four quadrant
+// workgroups per tile (XCD-chunked like the tile kernel).
+__global__ __launch_bounds__(256) void quad_bulk_kernel(double* __restrict__ A, int64_t lda, int k, int jb,
+                                                        const uint32_t* __restrict__ tiles, int ntiles,
+                                                        int kdepth, KTime* __restrict__ kt) {
+    kt_begin(kt);
+    const int b = (int)blockIdx.x >> 2, q = (int)blockIdx.x & 3;
+    const int chunk = (ntiles + 7) >> 3;
+    const int idx = (b & 7) * chunk + (b >> 3);
+    if (idx < ntiles) {
+        const uint32_t tv = tiles[idx];
+        const int bi = jb + (int)(tv & 0xffffu), bj = jb + (int)(tv >> 16);
+        const int qi = q >> 1, qj = q & 1;
+        if (!(bi == bj && qj > qi)) quad_update(A, lda, k, bi, bj, qi, qj, kdepth);
+    }
     kt_end(kt);
 }
 
@@ -772,9 +868,19 @@ __global__ void init_result_kernel(EvalResult* res) {
 
 // ------------------------------- launchers ---------------------------------------
 void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const double* X,
-                 int64_t ldx, const double* v, const TermPack* dtp, KTime* kt) {
-    const int64_t ntiles = (int64_t)nt * (nt + 1) / 2;
-    gram_kernel<<<dim3((unsigned)ntiles), dim3(256), 0, s>>>(A, lda, N, X, ldx, v, dtp, kt);
+                 int64_t ldx, const double* v, const TermPack* dtp, int part, int w, KTime* kt) {
+    int64_t ntiles;
+    if (part == 1) {
+        w = w < nt ? w : nt;
+        ntiles = 0;
+        for (int c = 0; c < w; ++c) ntiles += nt - c;
+    } else {
+        if (part == 0) w = 0;
+        const int64_t m = nt - w;
+        ntiles = m * (m + 1) / 2;
+    }
+    if (ntiles <= 0) return;
+    gram_kernel<<<dim3((unsigned)ntiles), dim3(256), 0, s>>>(A, lda, N, X, ldx, v, dtp, nt, part, w, kt);
 }
 
 void launch_potrf_diag(hipStream_t s, double* A, int64_t lda, int64_t N, int k, double* Dinv,
@@ -794,7 +900,9 @@ void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, i
     if (m <= 0) return;
     const int ntiles = m * (m + 1) / 2;
     const int grid = ((ntiles + 7) >> 3) << 3;
-    if (valu)
+    if (ntiles <= QUAD_BULK_MAX_TILES)
+        quad_bulk_kernel<<<dim3((unsigned)(4 * grid)), dim3(256), 0, s>>>(A, lda, k, jb, tiles, ntiles, kdepth, kt);
+    else if (valu)
         tile_valu_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(A, lda, k, jb, tiles, ntiles, kdepth, kt);
     else
         tile_gemm_kernel<0><<<dim3((unsigned)grid), dim3(256), 0, s>>>(A, lda, k, jb, 0, nullptr, tiles,
@@ -805,7 +913,8 @@ void launch_col_update(hipStream_t s, double* A, int64_t lda, int nt, int k, int
                        int kdepth, KTime* kt) {
     const int m0 = nt - jb;
     if (m0 <= 0) return;
-    const int tiles = ncols == 2 && m0 > 1 ? 2 * m0 - 1 : m0;
+    int tiles = 0;
+    for (int c = 0; c < ncols && c < m0; ++c) tiles += m0 - c;
     col_update_kernel<<<dim3((unsigned)(4 * tiles)), dim3(256), 0, s>>>(A, lda, k, jb, m0, kdepth, kt);
 }
 
