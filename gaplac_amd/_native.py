@@ -71,11 +71,12 @@ def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    path = os.environ.get("GAPLAC_LIB_PATH", LIB_PATH)  # developer A/B builds
+    if not os.path.exists(path):
         raise RuntimeError(
-            f"libgaplac_hip.so not built ({LIB_PATH}); run `python -c 'import __graft_entry__ as g; g.build()'`"
+            f"libgaplac_hip.so not built ({path}); run `python -c 'import __graft_entry__ as g; g.build()'`"
         )
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     lib.gaplac_abi_version.restype = c_int
     lib.gaplac_last_error.restype = c_char_p
     lib.gaplac_last_error.argtypes = [c_void_p]

@@ -63,7 +63,8 @@ struct gaplac_ctx {
     // pointers stay the same: removes the per-launch and cross-stream event-hop costs
     // (2.9 us per dependent launch, ~12 us per event hop eager vs ~1.6 us in a graph).
     // The profiled variant is the same schedule with KTime slots wired in.
-    bool use_graph = true;
+    bool use_graph = false;  // GAPLAC_GRAPH=1: capture/replay (loses stream priorities)
+    bool graph_prio = false;  // instantiate with per-node (capture-stream) priorities
     hipGraph_t graph = nullptr, pgraph = nullptr;
     hipGraphExec_t gexec = nullptr, pgexec = nullptr;
     int64_t gN = -1, pgN = -1;
@@ -390,7 +391,10 @@ int eval_device(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp, EvalR
             if (ce != hipSuccess)
                 return set_err(ctx, GAPLAC_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ce));
             G = g;
-            HIPCK(ctx, hipGraphInstantiate(&GX, G, nullptr, nullptr, 0));
+            if (ctx->graph_prio)
+                HIPCK(ctx, hipGraphInstantiateWithFlags(&GX, G, hipGraphInstantiateFlagUseNodePriority));
+            else
+                HIPCK(ctx, hipGraphInstantiate(&GX, G, nullptr, nullptr, 0));
             GN = N;
             std::memcpy(GP, ptrs, sizeof ptrs);
             if (prof) ctx->pslots = ctx->slots;
@@ -485,9 +489,11 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     };
     hipError_t e;
     if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
-    // s_panel: highest priority, all CUs. s_main: GAPLAC_DIAG_CUS (default 1) CUs masked
-    // out so the critical-path diagonal kernel always finds a free CU; if CU masks are
-    // unavailable, s_main falls back to the lowest priority without a mask.
+    // s_panel: highest priority, all CUs; s_main: lowest priority. Optionally
+    // (GAPLAC_DIAG_CUS=n) s_main gets a CU mask that keeps n CUs free for the panel chain
+    // (a masked stream has no priority). Measured at N=16384: priorities alone, eager
+    // launches: 37.0 ms; mask of 1 CU: 38.2 ms; graph replay (priorities are not carried
+    // into graph nodes): 37.9 ms with the mask, 39.4 ms without.
     int ncu = 0;
     if ((e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
         return fail("attribute", e);
@@ -496,7 +502,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
         return fail("priority range", e);
     if ((e = hipStreamCreateWithPriority(&ctx->s_panel, hipStreamNonBlocking, greatest)) != hipSuccess)
         return fail("stream", e);
-    int want = 1;
+    int want = 0;
     if (const char* s = std::getenv("GAPLAC_DIAG_CUS")) want = std::atoi(s);
     if (want > 0 && ncu > 2 * want) {
         const int words = (ncu + 31) / 32;
@@ -532,7 +538,8 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
         return fail("hipMalloc", e);
     if ((e = hipHostMalloc(reinterpret_cast<void**>(&ctx->htp), sizeof(TermPack), 0)) != hipSuccess)
         return fail("hipHostMalloc", e);
-    if (const char* s = std::getenv("GAPLAC_GRAPH")) ctx->use_graph = s[0] != '0';
+    if (const char* s = std::getenv("GAPLAC_GRAPH")) ctx->use_graph = s[0] == '1';
+    if (const char* s = std::getenv("GAPLAC_GRAPH_PRIO")) ctx->graph_prio = s[0] != '0';
     *out = ctx;
     return 0;
 }

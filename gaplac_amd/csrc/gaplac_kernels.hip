@@ -242,6 +242,7 @@ __device__ __forceinline__ void dblk_update(double* Ab, int I, int J, int k, int
 __device__ __forceinline__ void dinv_diag(const double* Ab, double* __restrict__ Dinv,
                                           const double* rdiag, int s, int lane) {
     const double* Ls = Ab + bidx(s, s) * 256;
+    asm volatile("" : "+v"(lane));  // see dpanel
     const int c = lane & 15;
     double x[16];
 #pragma unroll
@@ -259,65 +260,85 @@ __device__ __forceinline__ void dinv_diag(const double* Ab, double* __restrict__
 }
 
 // Wave-level factorisation of panel s: rows 16s..127 x 16 columns, two rows per lane.
-// Per column: the pivot comes from its lane by v_readlane; the owners of the panel's
-// 16 diagonal rows (lanes 0..7) publish the scaled column in a wave-private LDS vector
-// and every lane reads it back with 8 ds_read_b128 (in-order LDS within one wave; the
-// waitcnt orders write and read), then applies the rank-1 update to its two rows.
+// Per column the critical chain is kept short: pivot (v_readlane) -> 1/sqrt (v_rsq_f64
+// + two Goldschmidt steps) -> scale -> update of the NEXT column only (one v_readlane
+// broadcast) -> next pivot. Column c's updates of the later columns (c+2..15) are
+// deferred into iteration c+1, where they fill the latency of that pivot's 1/sqrt chain;
+// their L(c2, c) factors come from an LDS broadcast (lanes 0..7 publish the scaled
+// column, every lane reads it back at the end of iteration c; LDS is in order within a
+// wave). The sweep is branch-free (padding pivots and the info test are selects).
 __device__ __forceinline__ void dpanel(double* Ab, double* rdiag, double* colbuf, int s, int lane,
                                        int64_t gcol0, int64_t N, EvalResult* res) {
+    // opaque copy of the lane id: keeps the lane-dependent masks of the sweep from being
+    // hoisted out of the panel loop (and spilled) by loop-invariant code motion
+    asm volatile("" : "+v"(lane));
     const int R0 = 16 * s;
     const int rel0 = 2 * lane, rel1 = rel0 + 1;
     const int row0 = R0 + rel0;
     const bool live = row0 < NB;
     double v0[16], v1[16];
-    double* blk = Ab + (live ? bidx(row0 >> 4, s) * 256 : 0);
+    // lanes past the last row read (and never store) the panel's diagonal block
+    double* blk = Ab + bidx(live ? (row0 >> 4) : s, s) * 256;
     const int rr = row0 & 15;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
-        v0[c] = live ? blk[c * 16 + rr] : 0.0;
-        v1[c] = live ? blk[c * 16 + rr + 1] : 0.0;
+        v0[c] = blk[c * 16 + rr];
+        v1[c] = blk[c * 16 + rr + 1];
     }
+    const int64_t npiv = N - (gcol0 + R0);  // columns >= npiv are padding (unit pivots)
+    double myrd = 1.0;
+    int bad = 16;
+    double piv = readlane_d(v0[0], 0);
+    double lc[16];  // L(c2, c-1) for c2 >= c+1 (broadcast of the previous column)
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
-        const double piv = readlane_d((c & 1) ? v1[c] : v0[c], c >> 1);
-        double d, rd;
-        if (gcol0 + R0 + c >= N) {
-            d = 1.0;
-            rd = 1.0;
-        } else {
-            // OpenBLAS potf2 (the reference's dpotrf, 0.3.20) tests ajj <= 0 only: a NaN
-            // pivot is not reported and propagates to a NaN logpdf, as in the reference.
-            if (lane == 0 && piv <= 0.0)
-                atomicMin(&res->info, (unsigned long long)(gcol0 + R0 + c + 1));
-            // 1/sqrt by v_rsq_f64 + two Newton steps (full fp64 accuracy, ~1/3 of the
-            // latency of sqrt followed by a correctly rounded divide)
-            double y = __builtin_amdgcn_rsq(piv);
-            y = y * (1.5 - 0.5 * piv * y * y);
-            y = y * (1.5 - 0.5 * piv * y * y);
-            rd = y;
-            d = piv * y;
+        const bool pad = c >= npiv;
+        // OpenBLAS potf2 (the reference's dpotrf, 0.3.20) tests ajj <= 0 only: a NaN
+        // pivot is not reported and propagates to a NaN logpdf, as in the reference.
+        bad = (!pad && piv <= 0.0 && bad == 16) ? c : bad;
+        const double p = pad ? 1.0 : piv;
+        // Goldschmidt from v_rsq_f64: g -> sqrt(p), h -> 1/(2 sqrt(p))
+        const double y = __builtin_amdgcn_rsq(p);
+        double g = p * y, h = 0.5 * y;
+        // deferred updates of columns c+1..15 by column c-1
+        if (c >= 1) {
+#pragma unroll
+            for (int c2 = c + 1; c2 < 16; ++c2) {
+                v0[c2] = fma(-v0[c - 1], lc[c2], v0[c2]);
+                v1[c2] = fma(-v1[c - 1], lc[c2], v1[c2]);
+            }
         }
-        if (lane == 0) rdiag[R0 + c] = rd;
+        double r = fma(-g, h, 0.5);
+        g = fma(g, r, g);
+        h = fma(h, r, h);
+        r = fma(-g, h, 0.5);
+        g = fma(g, r, g);
+        h = fma(h, r, h);
+        const double d = g, rd = h + h;
+        myrd = lane == c ? rd : myrd;
         v0[c] = rel0 > c ? v0[c] * rd : (rel0 == c ? d : v0[c]);
         v1[c] = rel1 > c ? v1[c] * rd : (rel1 == c ? d : v1[c]);
         if (c < 15) {
-            if (lane < 8) *reinterpret_cast<double2*>(&colbuf[2 * lane]) = make_double2(v0[c], v1[c]);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            double lc[16];
+            double* cb = colbuf + 16 * (c & 1);
+            if (c < 14 && lane < 8) *reinterpret_cast<double2*>(&cb[2 * lane]) = make_double2(v0[c], v1[c]);
+            const double ln = readlane_d(((c + 1) & 1) ? v1[c] : v0[c], (c + 1) >> 1);
+            v0[c + 1] = fma(-v0[c], ln, v0[c + 1]);
+            v1[c + 1] = fma(-v1[c], ln, v1[c + 1]);
+            piv = readlane_d(((c + 1) & 1) ? v1[c + 1] : v0[c + 1], (c + 1) >> 1);
+            if (c < 14) {
+                __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const double2 w = *reinterpret_cast<const double2*>(&colbuf[2 * q]);
-                lc[2 * q] = w.x;
-                lc[2 * q + 1] = w.y;
+                for (int q = (c + 2) >> 1; q < 8; ++q) {
+                    const double2 w = *reinterpret_cast<const double2*>(&cb[2 * q]);
+                    lc[2 * q] = w.x;
+                    lc[2 * q + 1] = w.y;
+                }
             }
-#pragma unroll
-            for (int c2 = c + 1; c2 < 16; ++c2) {
-                v0[c2] -= v0[c] * lc[c2];
-                v1[c2] -= v1[c] * lc[c2];
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next write
         }
+        __builtin_amdgcn_sched_barrier(0);
     }
+    if (bad < 16 && lane == 0) atomicMin(&res->info, (unsigned long long)(gcol0 + R0 + bad + 1));
+    if (lane < 16) rdiag[R0 + lane] = myrd;
     if (live) {
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
@@ -331,9 +352,11 @@ __device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ A, i
                                                          int64_t N, int k,
                                                          double* __restrict__ Dinv,
                                                          EvalResult* __restrict__ res) {
-    __shared__ double Ab[NPK * 256];
-    __shared__ double rdiag[NB];
-    __shared__ double colbuf[16];
+    // one LDS array, small buffers first: their addresses fit ds_read's 16-bit offset
+    __shared__ double smem[32 + NB + NPK * 256];
+    double* colbuf = smem;
+    double* rdiag = smem + 32;
+    double* Ab = smem + 32 + NB;
     __builtin_amdgcn_s_setprio(3);  // critical path: win issue arbitration on shared SIMDs
     STAMP(20);
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
@@ -341,12 +364,12 @@ __device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ A, i
     double* Ag = A + g0 * lda + g0;
     // load the lower block triangle: element (r, c) of block (I, J) <- A(16I+r, 16J+c)
     {
-        const int c = t >> 4, r = t & 15;
+        const double* colp = Ag + (int64_t)(t >> 4) * lda + (t & 15);
 #pragma unroll
-        for (int I = 0; I < NDB; ++I)
+        for (int J = 0; J < NDB; ++J)
 #pragma unroll
-            for (int J = 0; J <= I; ++J)
-                Ab[bidx(I, J) * 256 + t] = Ag[(int64_t)(16 * J + c) * lda + 16 * I + r];
+            for (int I = J; I < NDB; ++I)
+                Ab[bidx(I, J) * 256 + t] = colp[(int64_t)(16 * J) * lda + 16 * I];
     }
     __syncthreads();
     STAMP(0);
@@ -379,11 +402,13 @@ __device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ A, i
     // write L (lower incl. diagonal) in place
     {
         const int c = t >> 4, r = t & 15;
+        double* colq = Ag + (int64_t)c * lda + r;
+        asm volatile("" : "+v"(colq));  // recomputed here: no load addresses live across the sweep
 #pragma unroll
-        for (int I = 0; I < NDB; ++I)
+        for (int J = 0; J < NDB; ++J)
 #pragma unroll
-            for (int J = 0; J <= I; ++J)
-                if (I != J || r >= c) Ag[(int64_t)(16 * J + c) * lda + 16 * I + r] = Ab[bidx(I, J) * 256 + t];
+            for (int I = J; I < NDB; ++I)
+                if (I != J || r >= c) colq[(int64_t)(16 * J) * lda + 16 * I] = Ab[bidx(I, J) * 256 + t];
     }
     STAMP(19);
 }
@@ -404,53 +429,75 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
 // computed transposed (Y_b = X_b^T = Dinv_b (B_b^T - sum_c L_bc Y_c)) so that every
 // result stays in the f64 MFMA accumulator layout (row = lane/16 + 4q, col = lane%16),
 // which is exactly the B-operand layout of the next MFMA: no LDS, no transposes.
-// 256 threads = 4 waves x 32 rows (two 16-row blocks, two interleaved MFMA chains).
-// L_kk and Dinv_k are read from global (L2-resident; just written by the diag kernel).
+// Two workgroups per tile, 4 waves x 16 rows each: the substitution is a dependent MFMA
+// chain per wave (sum_b 4b+4 = 144 MFMAs), so its latency scales with rows per wave.
+// The 28 strictly-lower 16x16 blocks of L_kk and the eight Dinv blocks are staged once
+// per workgroup in LDS (72 KiB), column-major per block, so A-operand reads are 16
+// consecutive doubles per lane group.
 // ---------------------------------------------------------------------------------
+constexpr int TRSM_LBLK = NDB * (NDB - 1) / 2;  // 28
+
 __device__ __forceinline__ void trsm_subst_kernel_body(double* __restrict__ A, int64_t lda, int k,
                                                          const double* __restrict__ Dinv) {
+    __shared__ double Ls[(TRSM_LBLK + NDB) * 256];
     __builtin_amdgcn_s_setprio(2);  // critical path
-    const int bi = k + 1 + (int)blockIdx.x;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tid = threadIdx.x;
+    const int bi = k + 1 + (int)(blockIdx.x >> 1);
+    const int wave = tid >> 6, lane = tid & 63;
     const int fr = lane >> 4, fc = lane & 15;
     const int64_t k0 = (int64_t)k * NB;
-    const double* L = A + k0 * lda + k0;                  // L_kk, column-major, lda
-    double* B = A + k0 * lda + (int64_t)bi * NB + 32 * wave;  // this wave's 32 rows of tile (bi, k)
-    d4 Y[2][NDB];
+    const double* L = A + k0 * lda + k0;  // L_kk, column-major, lda
+    // this wave's 16 rows of tile (bi, k); all of them are loaded up front (the stores of
+    // block b would otherwise order the loads of block b+1 behind them)
+    double* B = A + k0 * lda + (int64_t)bi * NB + 64 * (blockIdx.x & 1) + 16 * wave;
+    d4 Bt[NDB];
+#pragma unroll
+    for (int b = 0; b < NDB; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)  // B_b^T in accumulator layout: [j][r] = B[r][16b + j]
+            Bt[b][q] = B[(int64_t)(16 * b + fr + 4 * q) * lda + fc];
+    {
+        // block (b, c), c < b, at p = b(b-1)/2 + c: Ls[p*256 + m*16 + j] = L(16b + j, 16c + m)
+        const double* Lt = L + (int64_t)(tid >> 4) * lda + (tid & 15);
+        double lv[TRSM_LBLK], dv[NDB];
+#pragma unroll
+        for (int b = 1; b < NDB; ++b)
+#pragma unroll
+            for (int c = 0; c < b; ++c) lv[b * (b - 1) / 2 + c] = Lt[(int64_t)(16 * c) * lda + 16 * b];
+#pragma unroll
+        for (int q = 0; q < NDB; ++q) dv[q] = Dinv[q * 256 + tid];
+#pragma unroll
+        for (int p = 0; p < TRSM_LBLK; ++p) Ls[p * 256 + tid] = lv[p];
+#pragma unroll
+        for (int q = 0; q < NDB; ++q) Ls[(TRSM_LBLK + q) * 256 + tid] = dv[q];
+    }
+    __syncthreads();
+    d4 Y[NDB];
 #pragma unroll
     for (int b = 0; b < NDB; ++b) {
-        d4 s0, s1;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {  // B_b^T in accumulator layout: [j][r] = B[r][16b + j]
-            const int64_t col = (int64_t)(16 * b + fr + 4 * q) * lda;
-            s0[q] = B[col + fc];
-            s1[q] = B[col + 16 + fc];
-        }
+        d4 s0 = Bt[b], s1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int c = 0; c < b; ++c) {
+            const double* Lbc = Ls + (b * (b - 1) / 2 + c) * 256;
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
-                const double lbc = -L[(int64_t)(16 * c + 4 * kk + fr) * lda + 16 * b + fc];  // L_bc[j][k]
-                s0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[0][c][kk], s0, 0, 0, 0);
-                s1 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[1][c][kk], s1, 0, 0, 0);
+                const double lbc = -Lbc[(4 * kk + fr) * 16 + fc];  // L_bc[j][m], m = 4kk + fr
+                // two partial sums (even / odd c): halves the dependent-accumulator chain
+                if (c & 1)
+                    s1 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s1, 0, 0, 0);
+                else
+                    s0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s0, 0, 0, 0);
             }
         }
-        const double* Di = Dinv + b * 256;  // column-major: A operand [j = fc][m = 4kk + fr]
-        d4 y0 = {0.0, 0.0, 0.0, 0.0}, y1 = {0.0, 0.0, 0.0, 0.0};
+        s0 += s1;
+        const double* Di = Ls + (TRSM_LBLK + b) * 256;  // column-major: A operand [j = fc][m = 4kk + fr]
+        d4 y = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const double di = Di[(4 * kk + fr) * 16 + fc];
-            y0 = __builtin_amdgcn_mfma_f64_16x16x4f64(di, s0[kk], y0, 0, 0, 0);
-            y1 = __builtin_amdgcn_mfma_f64_16x16x4f64(di, s1[kk], y1, 0, 0, 0);
-        }
-        Y[0][b] = y0;
-        Y[1][b] = y1;
+        for (int kk = 0; kk < 4; ++kk)
+            y = __builtin_amdgcn_mfma_f64_16x16x4f64(Di[(4 * kk + fr) * 16 + fc], s0[kk], y, 0, 0, 0);
+        Y[b] = y;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int64_t col = (int64_t)(16 * b + fr + 4 * q) * lda;
-            B[col + fc] = y0[q];
-            B[col + 16 + fc] = y1[q];
-        }
+        for (int q = 0; q < 4; ++q) B[(int64_t)(16 * b + fr + 4 * q) * lda + fc] = y[q];
     }
 }
 
@@ -820,10 +867,20 @@ __global__ __launch_bounds__(1024) void reduce_kernel(const double* __restrict__
     __shared__ double s1[1024], s2[1024];
     const int tid = threadIdx.x;
     double ld = 0.0, q = 0.0;
-    for (int64_t j = tid; j < N; j += 1024) {
-        ld += log(A[j * lda + j]);
-        const double z = A[j * lda + N];
-        q += z * z;
+    // 8 strided loads in flight per thread per round (one memory latency per round)
+    for (int64_t j0 = tid; j0 < N; j0 += 8 * 1024) {
+        double dg[8], zz[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t j = j0 + (int64_t)u * 1024;
+            dg[u] = j < N ? A[j * lda + j] : 1.0;
+            zz[u] = j < N ? A[j * lda + N] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            ld += log(dg[u]);
+            q += zz[u] * zz[u];
+        }
     }
     s1[tid] = ld;
     s2[tid] = q;
@@ -891,7 +948,7 @@ void launch_potrf_diag(hipStream_t s, double* A, int64_t lda, int64_t N, int k, 
 void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Dinv, KTime* kt) {
     const int n = nt - k - 1;
     if (n <= 0) return;
-    trsm_subst_kernel<<<dim3(n), dim3(256), 0, s>>>(A, lda, k, Dinv, kt);
+    trsm_subst_kernel<<<dim3(2 * n), dim3(256), 0, s>>>(A, lda, k, Dinv, kt);
 }
 
 void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int kdepth,
