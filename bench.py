@@ -90,8 +90,13 @@ def cpu_baseline(N: int, budget_s: float = 25.0):
     }
 
 
+# PMC traffic of the dominant kernel (tools/profile_round.sh: FETCH_SIZE / WRITE_SIZE
+# passes over the same command, corrected per MI355X_MICROARCH.md; per launch).
+TRAFFIC_FILE = os.path.join("profiles", "r01b_traffic_syrk.json")
+
+
 def load_traffic():
-    path = os.path.join(HERE, "profiles", "traffic_syrk.json")
+    path = os.path.join(HERE, TRAFFIC_FILE)
     try:
         with open(path) as f:
             d = json.load(f)
@@ -187,13 +192,14 @@ def main():
         traffic, traffic_src = load_traffic()
         roofline = {
             "bound": "mfma",
-            "kernel": "tile_gemm_kernel<0> (bulk trailing SYRK, K=256, fp64 MFMA 16x16x4)",
+            "kernel": "tile_gemm_kernel<0> (bulk trailing SYRK, K=512, fp64 MFMA 16x16x4)",
             "achieved": round(achieved, 3),
             "peak": PEAK_F64_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_F64_TFLOPS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
+            "traffic_algorithmic": st["syrk_bytes"] / st["syrk_launches"],
             "flops_per_launch": flops_per_launch,
             "avg_launch_ms": st["syrk_ms"] / st["syrk_launches"],
             "launches": st["syrk_launches"],
@@ -220,6 +226,7 @@ def main():
         extra["trsm_ms_per_eval"] = st["trsm_ms"] / st["evals"]
         extra["colupd_ms_per_eval"] = st["colupd_ms"] / st["evals"]
         extra["syrk_ms_per_eval"] = st["syrk_ms"] / st["evals"]
+        extra["small_update_ms_per_eval"] = st["small_ms"] / st["evals"]
 
     cpu = None
     if world == 1 and not args.skip_cpu:

@@ -58,6 +58,9 @@ class Stats(ctypes.Structure):
         ("trsm_ms", c_double),
         ("colupd_ms", c_double),
         ("total_ms", c_double),
+        ("syrk_bytes", c_double),
+        ("small_launches", c_int64),
+        ("small_ms", c_double),
     ]
 
 

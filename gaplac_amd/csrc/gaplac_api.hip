@@ -51,8 +51,9 @@ struct gaplac_ctx {
     int spw = 4;          // GAPLAC_SPW: super-panel width in 128-column tiles (bulk K = 128 spw)
     gaplac_stats stats{};
     struct Slot {
-        int kind;  // 0 bulk syrk, 1 gram, 2 diag, 4 trsm, 5 column update
+        int kind;  // 0 bulk syrk, 1 gram, 2 diag, 4 trsm, 5 column update, 6 small bulk
         double work;
+        double bytes;  // kind 0: algorithmic HBM bytes
     };
     std::vector<Slot> slots;     // slots of the launches being enqueued / of the profiled graph
     KTime* dkt = nullptr;        // device slot array
@@ -178,11 +179,11 @@ int ensure(gaplac_ctx* ctx, T** p, size_t* cap, size_t n) {
 }
 
 // Profiling slot for the next launch (nullptr when profiling is off).
-KTime* slot(gaplac_ctx* ctx, int kind, double work) {
+KTime* slot(gaplac_ctx* ctx, int kind, double work, double bytes = 0.0) {
     if (!ctx->recording) return nullptr;
     const size_t i = ctx->slots.size();
     if (i >= ctx->kt_cap) return nullptr;
-    ctx->slots.push_back({kind, work});
+    ctx->slots.push_back({kind, work, bytes});
     return ctx->dkt + i;
 }
 
@@ -192,6 +193,13 @@ double syrk_flops(int m) {
     const double nbd = NB;
     const double rows = (double)m * nbd;
     return 2.0 * nbd * rows * (rows + 1) / 2.0;
+}
+
+// Algorithmic HBM bytes of one bulk trailing-update launch over the m x m tile triangle
+// with K = kd: every C tile read and written once, the m*NB panel rows read once.
+double syrk_bytes(int m, int kd) {
+    const double tiles = (double)m * (m + 1) / 2.0;
+    return tiles * NB * NB * 8.0 * 2.0 + (double)m * NB * kd * 8.0;
 }
 
 // Fold the device timestamps of the given slots into ctx->stats (ticks: 100 MHz).
@@ -210,6 +218,11 @@ int accumulate_slots(gaplac_ctx* ctx, const std::vector<gaplac_ctx::Slot>& slots
                 ctx->stats.syrk_ms += ms;
                 ctx->stats.syrk_flops += slots[i].work;
                 ctx->stats.syrk_launches += 1;
+                ctx->stats.syrk_bytes += slots[i].bytes;
+                break;
+            case 6:
+                ctx->stats.small_ms += ms;
+                ctx->stats.small_launches += 1;
                 break;
             case 1:
                 ctx->stats.gram_ms += ms;
@@ -286,9 +299,12 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         }
         HIPCK(ctx, hipStreamWaitEvent(sm, ctx->ev_P[p & 1], 0));
         const int jb = c0 + 2 * W;
-        if (jb < nt)
-            launch_syrk(sm, ctx->A, lda, nt, c0, jb, kd, ctx->tiles + ctx->tile_off[(size_t)(nt - jb)],
-                        ctx->bulk_valu, slot(ctx, 0, syrk_flops(nt - jb) * (kd / NB)));
+        if (jb < nt) {
+            const int m = nt - jb;
+            KTime* kt = syrk_is_small(m) ? slot(ctx, 6, 0)
+                                         : slot(ctx, 0, syrk_flops(m) * (kd / NB), syrk_bytes(m, kd));
+            launch_syrk(sm, ctx->A, lda, nt, c0, jb, kd, ctx->tiles + ctx->tile_off[(size_t)m], ctx->bulk_valu, kt);
+        }
         HIPCK(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
     }
     launch_reduce(sm, ctx->A, lda, N, ctx->dres);

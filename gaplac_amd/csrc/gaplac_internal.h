@@ -58,6 +58,8 @@ void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const dou
 // valu: 1 = v_fma_f64 register-tile kernel, 0 = fp64 MFMA kernel.
 void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int kdepth,
                  const uint32_t* tiles, int valu, KTime* kt);
+// True when launch_syrk over an m x m tile triangle runs the small (quadrant) kernel.
+bool syrk_is_small(int m);
 // Lookahead update of tile columns jb (and jb+1 if ncols == 2) with the kdepth columns
 // starting at tile column k.
 void launch_col_update(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int ncols,

@@ -951,6 +951,8 @@ void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const dou
     trsm_subst_kernel<<<dim3(2 * n), dim3(256), 0, s>>>(A, lda, k, Dinv, kt);
 }
 
+bool syrk_is_small(int m) { return m * (m + 1) / 2 <= QUAD_BULK_MAX_TILES; }
+
 void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int kdepth,
                  const uint32_t* tiles, int valu, KTime* kt) {
     const int m = nt - jb;

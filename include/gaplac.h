@@ -127,8 +127,9 @@ int gaplac_factor(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_
                   int32_t T, const gaplac_term* terms, double noise, const double* v,
                   double* out_L, int64_t ldl, double* out_z);
 
-/* Per-kernel timing of the last evaluation(s), recorded with hipEvents on the stream
- * each kernel is launched on, when profiling is on (off by default). */
+/* Per-kernel timing of the evaluations run while profiling is on (off by default):
+ * per-launch device timestamps (first workgroup start, last wave end; 100 MHz
+ * s_memrealtime), accumulated until gaplac_reset_stats. */
 typedef struct gaplac_stats {
     int64_t evals;
     int64_t syrk_launches;      /* bulk trailing-update launches (tile_gemm_kernel<0>) */
@@ -141,6 +142,10 @@ typedef struct gaplac_stats {
     double  trsm_ms;            /* panel TRSM launches, summed */
     double  colupd_ms;          /* lookahead column-update launches, summed */
     double  total_ms;           /* whole evaluation, first kernel to result */
+    double  syrk_bytes;         /* algorithmic HBM bytes of the bulk launches: C tiles read +
+                                   written once, panel rows read once */
+    int64_t small_launches;     /* small trailing updates (quad_bulk_kernel), not in syrk_* */
+    double  small_ms;
 } gaplac_stats;
 int gaplac_set_profiling(gaplac_ctx* ctx, int on);
 int gaplac_get_stats(gaplac_ctx* ctx, gaplac_stats* out);
