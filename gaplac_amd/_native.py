@@ -32,6 +32,19 @@ EXPORTED = (
     "gaplac_set_profiling",
     "gaplac_get_stats",
     "gaplac_reset_stats",
+    "gaplac_dist_create",
+    "gaplac_dist_destroy",
+    "gaplac_dist_last_error",
+    "gaplac_dist_geometry",
+    "gaplac_dist_set_panel_buffers",
+    "gaplac_dist_begin",
+    "gaplac_dist_factor",
+    "gaplac_dist_panel",
+    "gaplac_dist_comm_begin",
+    "gaplac_dist_comm_end",
+    "gaplac_dist_update",
+    "gaplac_dist_finish",
+    "gaplac_dist_local",
 )
 
 
@@ -99,9 +112,24 @@ def load() -> ctypes.CDLL:
     lib.gaplac_set_profiling.argtypes = [c_void_p, c_int]
     lib.gaplac_get_stats.argtypes = [c_void_p, POINTER(Stats)]
     lib.gaplac_reset_stats.argtypes = [c_void_p]
+    _I32P, _I64P, _VPP = POINTER(c_int32), POINTER(c_int64), POINTER(c_void_p)
+    lib.gaplac_dist_create.argtypes = [c_int, c_int, c_int, c_int, _VPP]
+    lib.gaplac_dist_destroy.argtypes = [c_void_p]
+    lib.gaplac_dist_last_error.argtypes = [c_void_p]
+    lib.gaplac_dist_geometry.argtypes = [c_void_p, c_int64, _I64P, _I32P, _I32P, _I32P, _I64P]
+    lib.gaplac_dist_set_panel_buffers.argtypes = [c_void_p, c_void_p, c_void_p, c_int64]
+    lib.gaplac_dist_begin.argtypes = common + [c_int, _I32P]
+    lib.gaplac_dist_factor.argtypes = [c_void_p, c_int32]
+    lib.gaplac_dist_panel.argtypes = [c_void_p, c_int32, _VPP, _I64P, _I32P]
+    lib.gaplac_dist_comm_begin.argtypes = [c_void_p, c_int32, _VPP]
+    lib.gaplac_dist_comm_end.argtypes = [c_void_p, c_int32]
+    lib.gaplac_dist_update.argtypes = [c_void_p, c_int32]
+    lib.gaplac_dist_finish.argtypes = [c_void_p, _DP, _DP, _I64P]
+    lib.gaplac_dist_local.argtypes = [c_void_p, c_void_p, c_int64]
     for name in EXPORTED:
         getattr(lib, name).restype = getattr(lib, name).restype or c_int
     lib.gaplac_last_error.restype = c_char_p
+    lib.gaplac_dist_last_error.restype = c_char_p
     _lib = lib
     return lib
 

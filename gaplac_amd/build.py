@@ -15,7 +15,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["gaplac_kernels.hip", "gaplac_api.hip"]
+SOURCES = ["gaplac_kernels.hip", "gaplac_api.hip", "gaplac_dist.hip"]
 HEADERS = ["gaplac_internal.h", os.path.join("..", "..", "include", "gaplac.h")]
 OUT = os.path.join(HERE, "_lib", "libgaplac_hip.so")
 ARCH = os.environ.get("GAPLAC_OFFLOAD_ARCH", "gfx950")

@@ -47,7 +47,6 @@ struct gaplac_ctx {
     // profiling: per-launch device timestamps (KTime slots), see kt_begin/kt_end
     bool profiling = false;
     bool serial = false;  // GAPLAC_SERIAL=1: one stream, no overlap (per-kernel timing)
-    int bulk_valu = 0;    // GAPLAC_BULK=valu: v_fma_f64 bulk-update kernel instead of MFMA
     int spw = 4;          // GAPLAC_SPW: super-panel width in 128-column tiles (bulk K = 128 spw)
     gaplac_stats stats{};
     struct Slot {
@@ -98,38 +97,50 @@ int set_err(gaplac_ctx* ctx, int code, const char* fmt, ...) {
 
 int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
+}  // namespace
+
 // Validate terms and build the kernel-argument pack. Mirrors the argument checks of the
 // KernelFunctions constructors GaPLAC calls (src/abstractgp_translations.jl:8-15):
 // LinearKernel requires c >= 0; ScaleTransform(1/l) requires a positive finite scale.
-int pack_terms(gaplac_ctx* ctx, int32_t D, int32_t T, const gaplac_term* terms, TermPack* tp) {
-    if (T < 0 || T > GAPLAC_MAX_TERMS)
-        return set_err(ctx, GAPLAC_E_KIND, "term count %d outside [0, %d]", T, GAPLAC_MAX_TERMS);
-    if (T > 0 && !terms) return set_err(ctx, GAPLAC_E_ARG, "terms is NULL");
+static int pfail(std::string* err, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+static int pfail(std::string* err, int code, const char* fmt, ...) {
+    if (err) {
+        char buf[256];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        *err = buf;
+    }
+    return code;
+}
+
+int gaplac::pack_terms(int32_t D, int32_t T, const gaplac_term* terms, TermPack* tp, std::string* err) {
+#define fail(...) pfail(err, __VA_ARGS__)
+    if (T < 0 || T > GAPLAC_MAX_TERMS) return fail(GAPLAC_E_KIND, "term count %d outside [0, %d]", T, GAPLAC_MAX_TERMS);
+    if (T > 0 && !terms) return fail(GAPLAC_E_ARG, "terms is NULL");
     std::memset(tp, 0, sizeof *tp);
     tp->T = T;
     for (int t = 0; t < T; ++t) {
         const gaplac_term& x = terms[t];
-        if (x.reserved != 0) return set_err(ctx, GAPLAC_E_ARG, "term %d: reserved field not 0", t);
+        if (x.reserved != 0) return fail(GAPLAC_E_ARG, "term %d: reserved field not 0", t);
         // groups must be contiguous: a group id seen before must be the previous term's
         for (int u = 0; u + 1 < t; ++u)
             if (terms[u].group == x.group && terms[t - 1].group != x.group)
-                return set_err(ctx, GAPLAC_E_KIND, "term %d: product group %d not contiguous", t,
-                               x.group);
+                return fail(GAPLAC_E_KIND, "term %d: product group %d not contiguous", t, x.group);
         tp->kind[t] = x.kind;
         tp->col[t] = x.col;
         switch (x.kind) {
             case GAPLAC_SQEXP:
             case GAPLAC_OU:
                 if (!(x.param > 0.0) || !std::isfinite(x.param))
-                    return set_err(ctx, GAPLAC_E_PARAM, "term %d: lengthscale %g must be > 0", t,
-                                   x.param);
+                    return fail(GAPLAC_E_PARAM, "term %d: lengthscale %g must be > 0", t, x.param);
                 tp->p[t] = 1.0 / x.param;  // ScaleTransform(inv(l))
-                if (!(tp->p[t] > 0.0))
-                    return set_err(ctx, GAPLAC_E_PARAM, "term %d: scale 1/l underflows", t);
+                if (!(tp->p[t] > 0.0)) return fail(GAPLAC_E_PARAM, "term %d: scale 1/l underflows", t);
                 break;
             case GAPLAC_LINEAR:
                 if (!(x.param >= 0.0) || !std::isfinite(x.param))
-                    return set_err(ctx, GAPLAC_E_PARAM, "term %d: c = %g must be >= 0", t, x.param);
+                    return fail(GAPLAC_E_PARAM, "term %d: c = %g must be >= 0", t, x.param);
                 tp->p[t] = x.param;
                 break;
             case GAPLAC_CAT:
@@ -137,19 +148,25 @@ int pack_terms(gaplac_ctx* ctx, int32_t D, int32_t T, const gaplac_term* terms, 
                 break;
             case GAPLAC_NOISE:
                 if (!(x.param >= 0.0) || !std::isfinite(x.param))
-                    return set_err(ctx, GAPLAC_E_PARAM, "term %d: noise variance %g must be >= 0",
-                                   t, x.param);
+                    return fail(GAPLAC_E_PARAM, "term %d: noise variance %g must be >= 0", t, x.param);
                 tp->p[t] = x.param;
                 tp->col[t] = 0;
                 break;
             default:
-                return set_err(ctx, GAPLAC_E_KIND, "term %d: unknown kind %d", t, x.kind);
+                return fail(GAPLAC_E_KIND, "term %d: unknown kind %d", t, x.kind);
         }
         if (x.kind != GAPLAC_NOISE && (x.col < 0 || x.col >= D))
-            return set_err(ctx, GAPLAC_E_COL, "term %d: column %d outside [0, %d)", t, x.col, D);
+            return fail(GAPLAC_E_COL, "term %d: column %d outside [0, %d)", t, x.col, D);
         tp->last_in_group[t] = (t == T - 1 || terms[t + 1].group != x.group) ? 1 : 0;
     }
+#undef fail
     return 0;
+}
+
+namespace {
+
+int pack_terms(gaplac_ctx* ctx, int32_t D, int32_t T, const gaplac_term* terms, TermPack* tp) {
+    return gaplac::pack_terms(D, T, terms, tp, ctx ? &ctx->err : nullptr);
 }
 
 int check_common(gaplac_ctx* ctx, int64_t N, int32_t D, const void* X, int64_t ldx, double noise,
@@ -269,10 +286,14 @@ void factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, 
     const int W = ctx->spw;
     const int c0 = W * p, c1 = std::min(W * p + W, nt);
     for (int c = c0; c < c1; ++c) {
-        if (c > c0) launch_col_update(sp, ctx->A, lda, nt, c - 1, c, c1 - c, NB, slot(ctx, 5, 0));
+        double* Acol = ctx->A + (int64_t)c * NB * lda;
+        if (c > c0)
+            launch_col_update(sp, ctx->A, lda, Panel{Acol - NB * lda, lda, 0}, nt, c, c, c1 - c, NB,
+                              slot(ctx, 5, 0));
         double* Dk = ctx->Dinv + (size_t)c * DINV_PER_BLOCK;
-        if ((int64_t)c * NB < N) launch_potrf_diag(sp, ctx->A, lda, N, c, Dk, ctx->dres, slot(ctx, 2, 0));
-        launch_trsm(sp, ctx->A, lda, nt, c, Dk, slot(ctx, 4, 0));
+        if ((int64_t)c * NB < N)
+            launch_potrf_diag(sp, Acol + (int64_t)c * NB, lda, N, (int64_t)c * NB, Dk, ctx->dres, slot(ctx, 2, 0));
+        launch_trsm(sp, Acol, lda, nt, c, Dk, slot(ctx, 4, 0));
     }
 }
 
@@ -293,7 +314,8 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             else
                 HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_gram2, 0));  // rest of the Gram built
             const int ncols = std::min(c0 + 2 * W, nt) - (c0 + W);
-            launch_col_update(sp, ctx->A, lda, nt, c0, c0 + W, ncols, kd, slot(ctx, 5, 0));
+            launch_col_update(sp, ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nt, c0 + W,
+                              c0 + W, ncols, kd, slot(ctx, 5, 0));
             factor_superpanel(ctx, sp, N, lda, nt, p + 1);
             HIPCK(ctx, hipEventRecord(ctx->ev_P[(p + 1) & 1], sp));
         }
@@ -301,13 +323,16 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         const int jb = c0 + 2 * W;
         if (jb < nt) {
             const int m = nt - jb;
-            KTime* kt = syrk_is_small(m) ? slot(ctx, 6, 0)
-                                         : slot(ctx, 0, syrk_flops(m) * (kd / NB), syrk_bytes(m, kd));
-            launch_syrk(sm, ctx->A, lda, nt, c0, jb, kd, ctx->tiles + ctx->tile_off[(size_t)m], ctx->bulk_valu, kt);
+            const BulkArgs ba{ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0},
+                              ctx->tiles + ctx->tile_off[(size_t)m], m * (m + 1) / 2, kd, jb, jb,
+                              ColMap{1, 0, W}};
+            KTime* kt = syrk_is_small(ba.ntiles) ? slot(ctx, 6, 0)
+                                                 : slot(ctx, 0, syrk_flops(m) * (kd / NB), syrk_bytes(m, kd));
+            launch_bulk(sm, ba, kt);
         }
         HIPCK(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
     }
-    launch_reduce(sm, ctx->A, lda, N, ctx->dres);
+    launch_reduce(sm, ctx->A, lda, N, (int64_t)nt * NB, ColMap{1, 0, 1}, ctx->dres);
     HIPCK(ctx, hipGetLastError());
     return 0;
 }
@@ -496,7 +521,6 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     gaplac_ctx* ctx = new gaplac_ctx();
     ctx->device = device;
     if (const char* s = std::getenv("GAPLAC_SERIAL")) ctx->serial = s[0] == '1';
-    if (const char* s = std::getenv("GAPLAC_BULK")) ctx->bulk_valu = std::strcmp(s, "valu") == 0;
     if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
     auto fail = [&](const char* what, hipError_t e) {
         std::fprintf(stderr, "gaplac_ctx_create: %s: %s\n", what, hipGetErrorString(e));

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string>
 #include "../../include/gaplac.h"
 
 namespace gaplac {
@@ -38,34 +39,74 @@ struct KTime {
     unsigned long long end;    // max over waves (init 0)
 };
 
+// Where global tile column bj of the lower triangle is stored. Single-GPU layout: the
+// identity (nranks = 1). 1-D block-column cyclic distribution over nranks: super-panels of
+// W tile columns are dealt round-robin, super-panel s to rank s % nranks, and a rank keeps
+// its super-panels contiguously in order, so local tile column lj holds global column
+//   bj = ((lj / W) * nranks + rank) * W + lj % W.
+// Rows are never redistributed: every storage column keeps global row indices.
+struct ColMap {
+    int nranks, rank, W;
+    __host__ __device__ __forceinline__ int global(int lj) const {
+        return nranks == 1 ? lj : ((lj / W) * nranks + rank) * W + lj % W;
+    }
+};
+
+// The kdepth panel columns a trailing update subtracts: global row r of panel column c is
+// P[c * ld + (r - row0)]. Single-GPU: the factored columns inside A (row0 = 0, ld = lda);
+// distributed: the broadcast panel buffer (row0 = first row of the super-panel).
+struct Panel {
+    const double* P;
+    int64_t ld;
+    int64_t row0;
+};
+
+// One bulk trailing update: tiles (bi, lj) = (bi0 + lo16, lj0 + hi16) of the list,
+// C(bi, bj = cm.global(lj)) -= P_bi P_bj^T with K = kdepth.
+struct BulkArgs {
+    double* C;
+    int64_t ldc;
+    Panel pn;
+    const uint32_t* tiles;
+    int ntiles, kdepth, bi0, lj0;
+    ColMap cm;
+};
+
+// Term validation + kernel-argument pack (gaplac_api.hip); on error returns GAPLAC_E_*
+// and sets *err.
+int pack_terms(int32_t D, int32_t T, const gaplac_term* terms, TermPack* tp, std::string* err);
+
 // Launchers (gaplac_kernels.hip). Every launcher takes a KTime slot (nullptr = off).
-// A is the Np x Np column-major augmented matrix
-// (lda = Np, Np = roundup(N+1, NB)): rows/cols 0..N-1 hold C, row N holds v^T.
+// Single-GPU layout: A is the Np x Np column-major augmented matrix (lda = Np, Np =
+// roundup(N+1, NB)): rows/cols 0..N-1 hold C, row N holds v^T.
 // part 0: all lower tiles; part 1: the first w tile columns; part 2: tiles with both
 // block indices >= w (parts 1 + 2 = part 0).
 void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt,
                  const double* X, int64_t ldx, const double* v, const TermPack* dtp, int part, int w,
                  KTime* kt);
-// Diagonal block k: L_kk in place + Dinv (DINV_ELEMS doubles: 8 column-major 16x16
-// inverses of L_kk's diagonal sub-blocks).
-void launch_potrf_diag(hipStream_t s, double* A, int64_t lda, int64_t N, int k,
+// Gram tiles of a list (entry bi | lj << 16, absolute) into column storage C.
+void launch_gram_list(hipStream_t s, double* C, int64_t ldc, int64_t N, const double* X, int64_t ldx,
+                      const double* v, const TermPack* dtp, const uint32_t* tiles, int ntiles, ColMap cm,
+                      KTime* kt);
+// Diagonal block at Ablk (global rows/cols g0..g0+127): L in place + Dinv (DINV_PER_BLOCK
+// doubles: 8 column-major 16x16 inverses of its diagonal sub-blocks).
+void launch_potrf_diag(hipStream_t s, double* Ablk, int64_t lda, int64_t N, int64_t g0,
                        double* Dinv, EvalResult* res, KTime* kt);
-// TRSM of the panel rows below diagonal block k: A[i,k] <- A[i,k] * L_kk^{-T}, i>k.
-void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Dinv, KTime* kt);
-// Bulk trailing update: lower triangle of tile blocks jb..nt-1 minus the kdepth columns
-// starting at tile column k (kdepth 128 or 256). tiles: super-tile ordered list for the
-// m x m triangle, m = nt - jb (build_tile_list).
-// valu: 1 = v_fma_f64 register-tile kernel, 0 = fp64 MFMA kernel.
-void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int kdepth,
-                 const uint32_t* tiles, int valu, KTime* kt);
-// True when launch_syrk over an m x m tile triangle runs the small (quadrant) kernel.
-bool syrk_is_small(int m);
-// Lookahead update of tile columns jb (and jb+1 if ncols == 2) with the kdepth columns
-// starting at tile column k.
-void launch_col_update(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int ncols,
-                       int kdepth, KTime* kt);
+// TRSM of the panel rows below diagonal block k: Acol is the storage of global column
+// k*NB; rows bi*NB.. for bi = k+1..nt-1 become A[bi,k] L_kk^{-T}.
+void launch_trsm(hipStream_t s, double* Acol, int64_t lda, int nt, int k, const double* Dinv, KTime* kt);
+// Bulk trailing update (tile kernel, or quadrant kernel for small tile counts).
+void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt);
+// True when launch_bulk over ntiles tiles runs the small (quadrant) kernel.
+bool syrk_is_small(int ntiles);
+// Update of global tile columns jb .. jb+ncols-1 (rows >= their diagonal), stored in local
+// tile columns lj0.., with the kdepth panel columns of pn.
+void launch_col_update(hipStream_t s, double* C, int64_t ldc, const Panel& pn, int nt, int jb, int lj0,
+                       int ncols, int kdepth, KTime* kt);
 void build_tile_list(int m, uint32_t* out);
-void launch_reduce(hipStream_t s, const double* A, int64_t lda, int64_t N, EvalResult* res);
+// logdet / quad over storage columns 0..ncols-1 (global columns via cm, those < N).
+void launch_reduce(hipStream_t s, const double* C, int64_t ldc, int64_t N, int64_t ncols, ColMap cm,
+                   EvalResult* res);
 void launch_kt_reset(hipStream_t s, KTime* kt, int n);
 void launch_init_result(hipStream_t s, EvalResult* res);
 

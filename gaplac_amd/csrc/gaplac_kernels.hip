@@ -10,8 +10,10 @@
 // Kernels:
 //   gram_kernel        Gram build, one 128x128 lower tile per workgroup (HBM-write bound)
 //   potrf_diag_kernel  128x128 diagonal block Cholesky + its triangular inverse (registers)
-//   tile_gemm_kernel   fp64 MFMA (v_mfma_f64_16x16x4f64) 128x128 tiles: trailing SYRK
-//                      update (C -= P Q^T) and panel TRSM (P <- P Linv^T)
+//   trsm_subst_kernel  panel TRSM by blocked substitution on fp64 MFMA
+//   tile_syrk_kernel   bulk trailing update C -= P Q^T, fp64 MFMA (v_mfma_f64_16x16x4f64)
+//                      on 128x128 tiles; quad_bulk_kernel / col_update_kernel: the same
+//                      on 64x64 quadrants (small updates, critical-path column updates)
 //   reduce_kernel      logdet = 2 sum log L_jj, quad = ||z||^2, logpdf
 #include "gaplac_internal.h"
 #include <math.h>
@@ -68,27 +70,13 @@ __device__ __forceinline__ void tri_index(int64_t t, int& bi, int& bj) {
 // (16-byte stores, a wave writes one 1 KiB column segment per instruction); the tile's
 // column coordinates are staged once in LDS and read as wave-wide broadcasts.
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ void gram_kernel_body(double* __restrict__ A, int64_t lda,
-                                                   int64_t N, const double* __restrict__ X,
-                                                   int64_t ldx, const double* __restrict__ v,
-                                                   const TermPack* __restrict__ tpp, int nt,
-                                                   int part, int w0) {
+__device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda, int64_t N,
+                                          const double* __restrict__ X, int64_t ldx,
+                                          const double* __restrict__ v,
+                                          const TermPack* __restrict__ tpp, int bi, int bj) {
+    // Ccol: storage of global column bj*NB (row 0); rows are global
     const TermPack& tp = *tpp;  // uniform: scalar loads (device copy refreshed per eval)
     const double noise = tp.noise;
-    int bi, bj;
-    if (part == 1) {  // strip of the first w0 tile columns (the first super-panel)
-        int t = (int)blockIdx.x;
-        bj = 0;
-        while (t >= nt - bj) {
-            t -= nt - bj;
-            ++bj;
-        }
-        bi = bj + t;
-    } else {  // lower triangle of tile blocks w0..nt-1 (part 2), or everything (w0 = 0)
-        tri_index(blockIdx.x, bi, bj);
-        bi += w0;
-        bj += w0;
-    }
     const int64_t r0 = (int64_t)bi * NB, c0 = (int64_t)bj * NB;
     __shared__ double xcol[GAPLAC_MAX_TERMS][NB];
     __shared__ double vcol[NB];
@@ -174,17 +162,47 @@ __device__ __forceinline__ void gram_kernel_body(double* __restrict__ A, int64_t
             o0 = 0.0;
             o1 = 0.0;
         }
-        *reinterpret_cast<double2*>(A + j * lda + i0) = make_double2(o0, o1);
+        *reinterpret_cast<double2*>(Ccol + (int64_t)cc * lda + i0) = make_double2(o0, o1);
     }
 }
 
+// Single-GPU layout. part 1: the first w tile columns; part 2: the lower triangle of tile
+// blocks w..nt-1; part 0: everything.
 __global__ __launch_bounds__(256) void gram_kernel(double* __restrict__ A, int64_t lda,
                                                    int64_t N, const double* __restrict__ X,
                                                    int64_t ldx, const double* __restrict__ v,
-                                                   const TermPack* __restrict__ tpp, int nt, int part, int w,
-        KTime* __restrict__ kt) {
+                                                   const TermPack* __restrict__ tpp, int nt, int part, int w0,
+                                                   KTime* __restrict__ kt) {
     kt_begin(kt);
-    gram_kernel_body(A, lda, N, X, ldx, v, tpp, nt, part, w);
+    int bi, bj;
+    if (part == 1) {
+        int t = (int)blockIdx.x;
+        bj = 0;
+        while (t >= nt - bj) {
+            t -= nt - bj;
+            ++bj;
+        }
+        bi = bj + t;
+    } else {
+        tri_index(blockIdx.x, bi, bj);
+        bi += w0;
+        bj += w0;
+    }
+    gram_tile(A + (int64_t)bj * NB * lda, lda, N, X, ldx, v, tpp, bi, bj);
+    kt_end(kt);
+}
+
+// Distributed layout: tiles[b] = bi | lj << 16 (global row block, local tile column).
+__global__ __launch_bounds__(256) void gram_list_kernel(double* __restrict__ C, int64_t ldc, int64_t N,
+                                                        const double* __restrict__ X, int64_t ldx,
+                                                        const double* __restrict__ v,
+                                                        const TermPack* __restrict__ tpp,
+                                                        const uint32_t* __restrict__ tiles, ColMap cm,
+                                                        KTime* __restrict__ kt) {
+    kt_begin(kt);
+    const uint32_t tv = tiles[blockIdx.x];
+    const int bi = (int)(tv & 0xffffu), lj = (int)(tv >> 16);
+    gram_tile(C + (int64_t)lj * NB * ldc, ldc, N, X, ldx, v, tpp, bi, cm.global(lj));
     kt_end(kt);
 }
 
@@ -210,7 +228,7 @@ __global__ __launch_bounds__(256) void gram_kernel(double* __restrict__ A, int64
 constexpr int DB = 16;                    // sub-block edge
 constexpr int NDB = NB / DB;              // 8
 constexpr int NPK = NDB * (NDB + 1) / 2;  // 36 packed blocks
-constexpr int DINV_ELEMS = NDB * DB * DB; // per diagonal block: 8 column-major 16x16 inverses
+static_assert(NDB * DB * DB == DINV_PER_BLOCK, "Dinv: 8 column-major 16x16 inverses per diagonal block");
 
 __device__ __forceinline__ int bidx(int I, int J) { return I * (I + 1) / 2 + J; }
 
@@ -348,8 +366,8 @@ __device__ __forceinline__ void dpanel(double* Ab, double* rdiag, double* colbuf
     }
 }
 
-__device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ A, int64_t lda,
-                                                         int64_t N, int k,
+__device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ Ag, int64_t lda,
+                                                         int64_t N, int64_t g0,
                                                          double* __restrict__ Dinv,
                                                          EvalResult* __restrict__ res) {
     // one LDS array, small buffers first: their addresses fit ds_read's 16-bit offset
@@ -360,8 +378,6 @@ __device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ A, i
     __builtin_amdgcn_s_setprio(3);  // critical path: win issue arbitration on shared SIMDs
     STAMP(20);
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-    const int64_t g0 = (int64_t)k * NB;
-    double* Ag = A + g0 * lda + g0;
     // load the lower block triangle: element (r, c) of block (I, J) <- A(16I+r, 16J+c)
     {
         const double* colp = Ag + (int64_t)(t >> 4) * lda + (t & 15);
@@ -413,13 +429,14 @@ __device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ A, i
     STAMP(19);
 }
 
-__global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
-                                                         int64_t N, int k,
+// Ag: the diagonal block (global rows/cols g0 .. g0+127) in its storage, leading dim lda.
+__global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ Ag, int64_t lda,
+                                                         int64_t N, int64_t g0,
                                                          double* __restrict__ Dinv,
                                                          EvalResult* __restrict__ res,
-        KTime* __restrict__ kt) {
+                                                         KTime* __restrict__ kt) {
     kt_begin(kt);
-    potrf_diag_kernel_body(A, lda, N, k, Dinv, res);
+    potrf_diag_kernel_body(Ag, lda, N, g0, Dinv, res);
     kt_end(kt);
 }
 
@@ -437,7 +454,8 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
 // ---------------------------------------------------------------------------------
 constexpr int TRSM_LBLK = NDB * (NDB - 1) / 2;  // 28
 
-__device__ __forceinline__ void trsm_subst_kernel_body(double* __restrict__ A, int64_t lda, int k,
+// Acol: storage of the panel's first column (global column k*NB), rows global.
+__device__ __forceinline__ void trsm_subst_kernel_body(double* __restrict__ Acol, int64_t lda, int k,
                                                          const double* __restrict__ Dinv) {
     __shared__ double Ls[(TRSM_LBLK + NDB) * 256];
     __builtin_amdgcn_s_setprio(2);  // critical path
@@ -446,10 +464,10 @@ __device__ __forceinline__ void trsm_subst_kernel_body(double* __restrict__ A, i
     const int wave = tid >> 6, lane = tid & 63;
     const int fr = lane >> 4, fc = lane & 15;
     const int64_t k0 = (int64_t)k * NB;
-    const double* L = A + k0 * lda + k0;  // L_kk, column-major, lda
+    const double* L = Acol + k0;  // L_kk, column-major, lda
     // this wave's 16 rows of tile (bi, k); all of them are loaded up front (the stores of
     // block b would otherwise order the loads of block b+1 behind them)
-    double* B = A + k0 * lda + (int64_t)bi * NB + 64 * (blockIdx.x & 1) + 16 * wave;
+    double* B = Acol + (int64_t)bi * NB + 64 * (blockIdx.x & 1) + 16 * wave;
     d4 Bt[NDB];
 #pragma unroll
     for (int b = 0; b < NDB; ++b)
@@ -501,89 +519,70 @@ __device__ __forceinline__ void trsm_subst_kernel_body(double* __restrict__ A, i
     }
 }
 
-__global__ __launch_bounds__(256) void trsm_subst_kernel(double* __restrict__ A, int64_t lda, int k,
+__global__ __launch_bounds__(256) void trsm_subst_kernel(double* __restrict__ Acol, int64_t lda, int k,
                                                          const double* __restrict__ Dinv,
-        KTime* __restrict__ kt) {
+                                                         KTime* __restrict__ kt) {
     kt_begin(kt);
-    trsm_subst_kernel_body(A, lda, k, Dinv);
+    trsm_subst_kernel_body(Acol, lda, k, Dinv);
     kt_end(kt);
 }
 
 // ---------------------------------------------------------------------------------
-// 128x128 fp64 MFMA tile kernel, K = kdepth (128: one panel; 256: a super-panel of two).
-//   MODE 0 (SYRK): C(bi,bj) -= P_bi * P_bj^T, P = the kdepth columns starting at k*NB.
-//   MODE 1 (TRSM): P_bi <- P_bi * Linv^T (in place), bi > k.
-// 256 threads = 4 waves as 2x2, each wave a 64x64 sub-tile = 4x4 v_mfma_f64_16x16x4f64
-// accumulators. Operands are staged through LDS in 16-deep k-chunks, double-buffered
-// with a register prefetch of the next chunk. The MFMA computes D = Q*P^T (the j-side
-// fragment is the A operand) so that a lane's accumulator column is C's row: stores are
-// 128-byte column segments of the column-major matrix. In SYRK mode the C tile is loaded
-// straight into the accumulators before the k-loop and P is staged negated, so the MFMA
-// chain produces C - P Q^T and the epilogue is stores only.
-// Tile placement: a precomputed list (tiles) maps blockIdx -> (bi, bj). For the bulk
-// trailing update the list is ordered so that the blocks one XCD runs (blockIdx % 8,
-// dealt round-robin by the dispatcher) walk one contiguous run of 8x8 super-tiles: the
-// P/Q row blocks of its ~64 resident tiles (2 MiB) stay in that XCD's 4 MiB L2.
-// Placement only affects speed; any blockIdx -> tile bijection is correct.
+// Bulk trailing update, one 128x128 tile per 256-thread workgroup:
+//   C(bi, bj) -= P_bi P_bj^T,   P = the kdepth panel columns (Panel operand),
+// with C tile (bi, bj) stored in local tile column lj (ColMap: bj = cm.global(lj)).
+// 4 waves as 2x2, each wave a 64x64 sub-tile = 4x4 v_mfma_f64_16x16x4f64 accumulators.
+// Operands are staged through LDS in 16-deep k-chunks, double-buffered with a register
+// prefetch of the next chunk. The MFMA computes D = Q*P^T (the j-side fragment is the A
+// operand) so that a lane's accumulator column is C's row: stores are 128-byte column
+// segments of the column-major matrix. The C tile is loaded straight into the
+// accumulators before the k-loop and P is staged negated, so the MFMA chain produces
+// C - P Q^T and the epilogue is stores only.
+// Tile placement: a precomputed list maps blockIdx -> (bi, lj) = (bi0 + lo16, lj0 + hi16).
+// The list is ordered so that the blocks one XCD runs (blockIdx % 8, dealt round-robin by
+// the dispatcher) walk one contiguous run of 8x8 super-tiles: the panel row blocks of its
+// ~64 resident tiles stay in that XCD's 4 MiB L2. Placement only affects speed; any
+// blockIdx -> tile bijection is correct.
 // ---------------------------------------------------------------------------------
 constexpr int KB = 16;
 constexpr int LR = NB + 16;  // LDS k-row stride: lanes 16..31 land on banks 32..63
 
-template <int MODE>
-__device__ __forceinline__ void tile_gemm_kernel_body(double* __restrict__ A, int64_t lda,
-                                                           int k, int jb, int colmode,
-                                                           const double* __restrict__ Linv,
-                                                           const uint32_t* __restrict__ tiles,
-                                                           int ntiles, int kdepth) {
+__device__ __forceinline__ void tile_decode(const BulkArgs& a, int idx, int& bi, int& bj, int& lj) {
+    const uint32_t tv = a.tiles[idx];
+    bi = a.bi0 + (int)(tv & 0xffffu);
+    lj = a.lj0 + (int)(tv >> 16);
+    bj = a.cm.global(lj);
+}
+
+__device__ __forceinline__ void tile_syrk_body(const BulkArgs& a) {
     __shared__ double sm[2][2][KB][LR];
-    int bi, bj;
-    if (MODE == 1) {
-        bi = k + 1 + (int)blockIdx.x;
-        bj = k;
-    } else if (colmode) {
-        bi = jb + (int)blockIdx.x;
-        bj = jb;
-    } else {
-        const int b = (int)blockIdx.x;
-        const int chunk = (ntiles + 7) >> 3;
-        const int idx = (b & 7) * chunk + (b >> 3);
-        if (idx >= ntiles) return;
-        const uint32_t tv = tiles[idx];
-        bi = jb + (int)(tv & 0xffffu);
-        bj = jb + (int)(tv >> 16);
-    }
-    const int64_t r0 = (int64_t)bi * NB, c0 = (int64_t)bj * NB, k0 = (int64_t)k * NB;
-    const double* P = A + k0 * lda + r0;
-    const double* Q;
-    int64_t ldq;
-    if (MODE == 1) {
-        Q = Linv;
-        ldq = NB;
-    } else {
-        Q = A + k0 * lda + c0;
-        ldq = lda;
-    }
+    const int b = (int)blockIdx.x;
+    const int chunk = (a.ntiles + 7) >> 3;
+    const int idx = (b & 7) * chunk + (b >> 3);
+    if (idx >= a.ntiles) return;
+    int bi, bj, lj;
+    tile_decode(a, idx, bi, bj, lj);
+    const int64_t r0 = (int64_t)bi * NB;
+    const int64_t ldc = a.ldc, ldp = a.pn.ld;
+    double* __restrict__ Ct = a.C + (int64_t)lj * NB * ldc + r0;
+    const double* __restrict__ P = a.pn.P + (r0 - a.pn.row0);
+    const double* __restrict__ Q = a.pn.P + ((int64_t)bj * NB - a.pn.row0);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wi = w & 1, wj = w >> 1;
-    const bool active = !(MODE == 0 && bi == bj && wj > wi);
+    const bool active = !(bi == bj && wj > wi);
     const int fr = lane >> 4, fc = lane & 15;
 
     d4 acc[4][4];
-    if (MODE == 0 && active) {
+    if (active) {
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) {
-            const double* Ci = A + c0 * lda + r0 + 64 * wi + 16 * mi + fc;
+            const double* Ci = Ct + 64 * wi + 16 * mi + fc;
 #pragma unroll
             for (int mj = 0; mj < 4; ++mj)
 #pragma unroll
                 for (int rg = 0; rg < 4; ++rg)
-                    acc[mi][mj][rg] = Ci[(int64_t)(64 * wj + 16 * mj + fr + 4 * rg) * lda];
+                    acc[mi][mj][rg] = Ci[(int64_t)(64 * wj + 16 * mj + fr + 4 * rg) * ldc];
         }
-    } else {
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
     }
 
     double2 pp[4], pq[4];
@@ -592,8 +591,8 @@ __device__ __forceinline__ void tile_gemm_kernel_body(double* __restrict__ A, in
 #pragma unroll
         for (int it = 0; it < 4; ++it) {
             const int64_t col = (int64_t)ch * KB + krow + 4 * it;
-            pp[it] = *reinterpret_cast<const double2*>(P + col * lda + 2 * lane);
-            pq[it] = *reinterpret_cast<const double2*>(Q + col * ldq + 2 * lane);
+            pp[it] = *reinterpret_cast<const double2*>(P + col * ldp + 2 * lane);
+            pq[it] = *reinterpret_cast<const double2*>(Q + col * ldp + 2 * lane);
         }
     };
     auto lstore = [&](int buf) {
@@ -601,10 +600,8 @@ __device__ __forceinline__ void tile_gemm_kernel_body(double* __restrict__ A, in
         for (int it = 0; it < 4; ++it) {
             const int kk = krow + 4 * it;
             double2 v = pp[it];
-            if (MODE == 0) {
-                v.x = -v.x;
-                v.y = -v.y;
-            }
+            v.x = -v.x;
+            v.y = -v.y;
             *reinterpret_cast<double2*>(&sm[buf][0][kk][2 * lane]) = v;
             *reinterpret_cast<double2*>(&sm[buf][1][kk][2 * lane]) = pq[it];
         }
@@ -613,7 +610,7 @@ __device__ __forceinline__ void tile_gemm_kernel_body(double* __restrict__ A, in
     gload(0);
     lstore(0);
     __syncthreads();
-    const int NCH = kdepth / KB;
+    const int NCH = a.kdepth / KB;
     for (int ch = 0; ch < NCH; ++ch) {
         const int buf = ch & 1;
         if (ch + 1 < NCH) gload(ch + 1);
@@ -640,123 +637,27 @@ __device__ __forceinline__ void tile_gemm_kernel_body(double* __restrict__ A, in
     if (!active) return;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
-        double* Ci = A + c0 * lda + r0 + 64 * wi + 16 * mi + fc;
+        double* Ci = Ct + 64 * wi + 16 * mi + fc;
 #pragma unroll
         for (int mj = 0; mj < 4; ++mj)
 #pragma unroll
             for (int rg = 0; rg < 4; ++rg)
-                Ci[(int64_t)(64 * wj + 16 * mj + fr + 4 * rg) * lda] = acc[mi][mj][rg];
+                Ci[(int64_t)(64 * wj + 16 * mj + fr + 4 * rg) * ldc] = acc[mi][mj][rg];
     }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(256, 2) void tile_gemm_kernel(double* __restrict__ A, int64_t lda,
-                                                           int k, int jb, int colmode,
-                                                           const double* __restrict__ Linv,
-                                                           const uint32_t* __restrict__ tiles,
-                                                           int ntiles, int kdepth,
-        KTime* __restrict__ kt) {
+__global__ __launch_bounds__(256, 2) void tile_syrk_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
-    tile_gemm_kernel_body<MODE>(A, lda, k, jb, colmode, Linv, tiles, ntiles, kdepth);
+    tile_syrk_body(a);
     kt_end(kt);
 }
 
 // ---------------------------------------------------------------------------------
-// VALU variant of the bulk trailing update (same tiles, same list, same K): each thread
-// owns an 8x8 register tile (rows tx+16i, columns ty+16j of the 128x128 tile), operands
-// broadcast from LDS (8 + 8 ds_read_b64 per k, conflict-free: 16 consecutive doubles per
-// read), 64 v_fma_f64 per k. Measured fp64 ceilings on MI355X (tools/mfma_f64_rate.hip):
-// v_fma_f64 61.5 TFLOP/s vs v_mfma_f64_16x16x4f64 47.5 TFLOP/s, so the vector pipe is the
-// faster fp64 engine on this part; GAPLAC_BULK selects the kernel.
-// ---------------------------------------------------------------------------------
-__device__ __forceinline__ void tile_valu_kernel_body(double* __restrict__ A, int64_t lda, int k,
-                                                           int jb, const uint32_t* __restrict__ tiles,
-                                                           int ntiles, int kdepth) {
-    __shared__ double sm[2][2][KB][LR];
-    const int b = (int)blockIdx.x;
-    const int chunk = (ntiles + 7) >> 3;
-    const int idx = (b & 7) * chunk + (b >> 3);
-    if (idx >= ntiles) return;
-    const uint32_t tv = tiles[idx];
-    const int bi = jb + (int)(tv & 0xffffu), bj = jb + (int)(tv >> 16);
-    const int64_t r0 = (int64_t)bi * NB, c0 = (int64_t)bj * NB, k0 = (int64_t)k * NB;
-    const double* P = A + k0 * lda + r0;
-    const double* Q = A + k0 * lda + c0;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int tx = tid & 15, ty = tid >> 4;
-    double acc[8][8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const double* Cj = A + (c0 + ty + 16 * j) * lda + r0 + tx;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i][j] = Cj[16 * i];
-    }
-    double2 pp[4], pq[4];
-    const int krow = tid >> 6;
-    auto gload = [&](int ch) {
-#pragma unroll
-        for (int it = 0; it < 4; ++it) {
-            const int64_t col = (int64_t)ch * KB + krow + 4 * it;
-            pp[it] = *reinterpret_cast<const double2*>(P + col * lda + 2 * lane);
-            pq[it] = *reinterpret_cast<const double2*>(Q + col * lda + 2 * lane);
-        }
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-        for (int it = 0; it < 4; ++it) {
-            const int kk = krow + 4 * it;
-            double2 v = pp[it];
-            v.x = -v.x;
-            v.y = -v.y;
-            *reinterpret_cast<double2*>(&sm[buf][0][kk][2 * lane]) = v;
-            *reinterpret_cast<double2*>(&sm[buf][1][kk][2 * lane]) = pq[it];
-        }
-    };
-    gload(0);
-    lstore(0);
-    __syncthreads();
-    const int NCH = kdepth / KB;
-    for (int ch = 0; ch < NCH; ++ch) {
-        const int buf = ch & 1;
-        if (ch + 1 < NCH) gload(ch + 1);
-#pragma unroll 4
-        for (int kk = 0; kk < KB; ++kk) {
-            double a[8], q[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) a[i] = sm[buf][0][kk][tx + 16 * i];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) q[j] = sm[buf][1][kk][ty + 16 * j];
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) acc[i][j] = fma(a[i], q[j], acc[i][j]);
-        }
-        if (ch + 1 < NCH) lstore(buf ^ 1);
-        __syncthreads();
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        double* Cj = A + (c0 + ty + 16 * j) * lda + r0 + tx;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) Cj[16 * i] = acc[i][j];
-    }
-}
-
-__global__ __launch_bounds__(256, 2) void tile_valu_kernel(double* __restrict__ A, int64_t lda, int k,
-                                                           int jb, const uint32_t* __restrict__ tiles,
-                                                           int ntiles, int kdepth,
-        KTime* __restrict__ kt) {
-    kt_begin(kt);
-    tile_valu_kernel_body(A, lda, k, jb, tiles, ntiles, kdepth);
-    kt_end(kt);
-}
-
-// ---------------------------------------------------------------------------------
-// Quadrant update: C_q -= P_q Q_q^T for one 64x64 quadrant (qi, qj) of tile (bi, bj),
-// K = kdepth columns starting at tile column k. 4 waves as 2x2 of 32x32 (2x2 f64 MFMA
-// accumulators each); fragments come straight from global memory (the panel columns are
-// L2-resident), register double-buffered 8 k-steps (32 columns) ahead, no LDS, no
-// barriers. Used where latency matters more than throughput: the lookahead column
+// Quadrant update: C_q -= P_q Q_q^T for one 64x64 quadrant (qi, qj) of tile (bi, bj)
+// (stored in local tile column lj), K = kdepth panel columns. 4 waves as 2x2 of 32x32
+// (2x2 f64 MFMA accumulators each); fragments come straight from global memory (the panel
+// columns are L2-resident), register double-buffered 8 k-steps (32 columns) ahead, no
+// LDS, no barriers. Used where latency matters more than throughput: the lookahead column
 // update on the critical path and the small trailing updates at the end of the
 // factorisation (a 128x128x256 tile alone on a CU takes ~50 us; a quadrant ~4x less).
 // ---------------------------------------------------------------------------------
@@ -764,16 +665,17 @@ constexpr int QG = 8;  // k-steps per prefetch group
 // Bulk updates with at most this many 128x128 tiles run as quadrants (4 WGs per tile).
 constexpr int QUAD_BULK_MAX_TILES = 512;
 
-__device__ __forceinline__ void quad_update(double* __restrict__ A, int64_t lda, int k, int bi, int bj,
-                                            int qi, int qj, int kdepth) {
+__device__ __forceinline__ void quad_update(double* __restrict__ C, int64_t ldc, const Panel& pn, int bi,
+                                            int bj, int lj, int qi, int qj, int kdepth) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wi = wave & 1, wj = wave >> 1;
     const int fr = lane >> 4, fc = lane & 15;
-    const int64_t k0 = (int64_t)k * NB;
-    const int64_t ri = (int64_t)bi * NB + 64 * qi + 32 * wi;  // this wave's 32 rows
-    const int64_t cj = (int64_t)bj * NB + 64 * qj + 32 * wj;  // this wave's 32 columns
-    const double* P = A + k0 * lda + ri + fc;
-    const double* Q = A + k0 * lda + cj + fc;
+    const int64_t ri = (int64_t)bi * NB + 64 * qi + 32 * wi;   // this wave's 32 rows
+    const int64_t cj = (int64_t)bj * NB + 64 * qj + 32 * wj;   // this wave's 32 columns (global)
+    const int64_t cl = (int64_t)lj * NB + 64 * qj + 32 * wj;   // ... in storage
+    const int64_t ldp = pn.ld;
+    const double* P = pn.P + (ri - pn.row0) + fc;
+    const double* Q = pn.P + (cj - pn.row0) + fc;
     d4 acc[2][2];
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
@@ -781,12 +683,12 @@ __device__ __forceinline__ void quad_update(double* __restrict__ A, int64_t lda,
         for (int mj = 0; mj < 2; ++mj)
 #pragma unroll
             for (int rg = 0; rg < 4; ++rg)
-                acc[mi][mj][rg] = A[(cj + 16 * mj + fr + 4 * rg) * lda + ri + 16 * mi + fc];
+                acc[mi][mj][rg] = C[(cl + 16 * mj + fr + 4 * rg) * ldc + ri + 16 * mi + fc];
     double fa[2][QG][2], fb[2][QG][2];  // [buffer][k-step][16-block]
     auto load = [&](int buf, int g) {
 #pragma unroll
         for (int s = 0; s < QG; ++s) {
-            const int64_t col = (int64_t)(g * 4 * QG + 4 * s + fr) * lda;
+            const int64_t col = (int64_t)(g * 4 * QG + 4 * s + fr) * ldp;
             fb[buf][s][0] = P[col];
             fb[buf][s][1] = P[col + 16];
             fa[buf][s][0] = Q[col];
@@ -803,7 +705,7 @@ __device__ __forceinline__ void quad_update(double* __restrict__ A, int64_t lda,
             acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][s][1], b1, acc[1][1], 0, 0, 0);
         }
     };
-    const int ng = kdepth / (4 * QG);  // 4 (K=128) or 8 (K=256)
+    const int ng = kdepth / (4 * QG);  // 4 per 128 panel columns
     load(0, 0);
     for (int g = 0; g < ng; g += 2) {
         if (g + 1 < ng) load(1, g + 1);
@@ -819,41 +721,40 @@ __device__ __forceinline__ void quad_update(double* __restrict__ A, int64_t lda,
         for (int mj = 0; mj < 2; ++mj)
 #pragma unroll
             for (int rg = 0; rg < 4; ++rg)
-                A[(cj + 16 * mj + fr + 4 * rg) * lda + ri + 16 * mi + fc] = acc[mi][mj][rg];
+                C[(cl + 16 * mj + fr + 4 * rg) * ldc + ri + 16 * mi + fc] = acc[mi][mj][rg];
 }
 
-// Lookahead column update (critical path): tiles i >= jb of tile columns jb0 .. jb0+ncols-1
-// (the next super-panel's columns), K = kdepth.
-__global__ __launch_bounds__(256) void col_update_kernel(double* __restrict__ A, int64_t lda, int k,
-                                                         int jb0, int m0, int kdepth,
+// Column update (critical path): tiles i >= jb of the global tile columns jb0 ..
+// jb0+ncols-1, stored in local tile columns lj0 .. lj0+ncols-1 (one super-panel: its
+// columns are contiguous in storage), K = kdepth panel columns.
+__global__ __launch_bounds__(256) void col_update_kernel(double* __restrict__ C, int64_t ldc, Panel pn,
+                                                         int jb0, int lj0, int m0, int kdepth,
                                                          KTime* __restrict__ kt) {
     kt_begin(kt);
     __builtin_amdgcn_s_setprio(2);
     const int q = (int)blockIdx.x & 3;
-    int t = (int)blockIdx.x >> 2, jb = jb0;
+    int t = (int)blockIdx.x >> 2, c = 0;
     for (int mc = m0; t >= mc && mc > 0; --mc) {  // tile column jb0 + c holds m0 - c tiles
         t -= mc;
-        ++jb;
+        ++c;
     }
-    const int bi = jb + t, qi = q >> 1, qj = q & 1;
-    if (!(bi == jb && qj > qi)) quad_update(A, lda, k, bi, jb, qi, qj, kdepth);
+    const int jb = jb0 + c, bi = jb + t, qi = q >> 1, qj = q & 1;
+    if (!(bi == jb && qj > qi)) quad_update(C, ldc, pn, bi, jb, lj0 + c, qi, qj, kdepth);
     kt_end(kt);
 }
 
-// Small bulk trailing updates: the same tile list as tile_gemm_kernel, four quadrant
+// Small bulk trailing updates: the same tile list as tile_syrk_kernel, four quadrant
 // workgroups per tile (XCD-chunked like the tile kernel).
-__global__ __launch_bounds__(256) void quad_bulk_kernel(double* __restrict__ A, int64_t lda, int k, int jb,
-                                                        const uint32_t* __restrict__ tiles, int ntiles,
-                                                        int kdepth, KTime* __restrict__ kt) {
+__global__ __launch_bounds__(256) void quad_bulk_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
     const int b = (int)blockIdx.x >> 2, q = (int)blockIdx.x & 3;
-    const int chunk = (ntiles + 7) >> 3;
+    const int chunk = (a.ntiles + 7) >> 3;
     const int idx = (b & 7) * chunk + (b >> 3);
-    if (idx < ntiles) {
-        const uint32_t tv = tiles[idx];
-        const int bi = jb + (int)(tv & 0xffffu), bj = jb + (int)(tv >> 16);
+    if (idx < a.ntiles) {
+        int bi, bj, lj;
+        tile_decode(a, idx, bi, bj, lj);
         const int qi = q >> 1, qj = q & 1;
-        if (!(bi == bj && qj > qi)) quad_update(A, lda, k, bi, bj, qi, qj, kdepth);
+        if (!(bi == bj && qj > qi)) quad_update(a.C, a.ldc, a.pn, bi, bj, lj, qi, qj, a.kdepth);
     }
     kt_end(kt);
 }
@@ -862,19 +763,25 @@ __global__ __launch_bounds__(256) void quad_bulk_kernel(double* __restrict__ A, 
 // logdet / quad / logpdf (AbstractGPs.logpdf: -((N*log2pi + logdet) + quad) / 2).
 // Fixed-order tree reduction: deterministic across runs.
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void reduce_kernel(const double* __restrict__ A, int64_t lda,
-                                                      int64_t N, EvalResult* __restrict__ res) {
+// Storage columns e = 0 .. ncols-1 hold global columns cm.global(e / NB) * NB + e % NB;
+// only those < N contribute. With the identity map this is the whole-matrix reduction;
+// on a distributed rank it is that rank's partial logdet / quad (summed across ranks by
+// the host; res->logpdf then only holds this rank's share).
+__global__ __launch_bounds__(1024) void reduce_kernel(const double* __restrict__ C, int64_t ldc,
+                                                      int64_t N, int64_t ncols, ColMap cm,
+                                                      EvalResult* __restrict__ res) {
     __shared__ double s1[1024], s2[1024];
     const int tid = threadIdx.x;
     double ld = 0.0, q = 0.0;
     // 8 strided loads in flight per thread per round (one memory latency per round)
-    for (int64_t j0 = tid; j0 < N; j0 += 8 * 1024) {
+    for (int64_t e0 = tid; e0 < ncols; e0 += 8 * 1024) {
         double dg[8], zz[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int64_t j = j0 + (int64_t)u * 1024;
-            dg[u] = j < N ? A[j * lda + j] : 1.0;
-            zz[u] = j < N ? A[j * lda + N] : 0.0;
+            const int64_t e = e0 + (int64_t)u * 1024;
+            const int64_t j = e < ncols ? (int64_t)cm.global((int)(e / NB)) * NB + e % NB : N;
+            dg[u] = j < N ? C[e * ldc + j] : 1.0;
+            zz[u] = j < N ? C[e * ldc + N] : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -940,41 +847,42 @@ void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const
     gram_kernel<<<dim3((unsigned)ntiles), dim3(256), 0, s>>>(A, lda, N, X, ldx, v, dtp, nt, part, w, kt);
 }
 
-void launch_potrf_diag(hipStream_t s, double* A, int64_t lda, int64_t N, int k, double* Dinv,
-                       EvalResult* res, KTime* kt) {
-    potrf_diag_kernel<<<dim3(1), dim3(256), 0, s>>>(A, lda, N, k, Dinv, res, kt);
+void launch_gram_list(hipStream_t s, double* C, int64_t ldc, int64_t N, const double* X, int64_t ldx,
+                      const double* v, const TermPack* dtp, const uint32_t* tiles, int ntiles, ColMap cm,
+                      KTime* kt) {
+    if (ntiles <= 0) return;
+    gram_list_kernel<<<dim3((unsigned)ntiles), dim3(256), 0, s>>>(C, ldc, N, X, ldx, v, dtp, tiles, cm, kt);
 }
 
-void launch_trsm(hipStream_t s, double* A, int64_t lda, int nt, int k, const double* Dinv, KTime* kt) {
+void launch_potrf_diag(hipStream_t s, double* Ablk, int64_t lda, int64_t N, int64_t g0, double* Dinv,
+                       EvalResult* res, KTime* kt) {
+    potrf_diag_kernel<<<dim3(1), dim3(256), 0, s>>>(Ablk, lda, N, g0, Dinv, res, kt);
+}
+
+void launch_trsm(hipStream_t s, double* Acol, int64_t lda, int nt, int k, const double* Dinv, KTime* kt) {
     const int n = nt - k - 1;
     if (n <= 0) return;
-    trsm_subst_kernel<<<dim3(2 * n), dim3(256), 0, s>>>(A, lda, k, Dinv, kt);
+    trsm_subst_kernel<<<dim3(2 * n), dim3(256), 0, s>>>(Acol, lda, k, Dinv, kt);
 }
 
-bool syrk_is_small(int m) { return m * (m + 1) / 2 <= QUAD_BULK_MAX_TILES; }
+bool syrk_is_small(int ntiles) { return ntiles <= QUAD_BULK_MAX_TILES; }
 
-void launch_syrk(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int kdepth,
-                 const uint32_t* tiles, int valu, KTime* kt) {
-    const int m = nt - jb;
-    if (m <= 0) return;
-    const int ntiles = m * (m + 1) / 2;
-    const int grid = ((ntiles + 7) >> 3) << 3;
-    if (ntiles <= QUAD_BULK_MAX_TILES)
-        quad_bulk_kernel<<<dim3((unsigned)(4 * grid)), dim3(256), 0, s>>>(A, lda, k, jb, tiles, ntiles, kdepth, kt);
-    else if (valu)
-        tile_valu_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(A, lda, k, jb, tiles, ntiles, kdepth, kt);
+void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt) {
+    if (a.ntiles <= 0) return;
+    const int grid = ((a.ntiles + 7) >> 3) << 3;
+    if (syrk_is_small(a.ntiles))
+        quad_bulk_kernel<<<dim3((unsigned)(4 * grid)), dim3(256), 0, s>>>(a, kt);
     else
-        tile_gemm_kernel<0><<<dim3((unsigned)grid), dim3(256), 0, s>>>(A, lda, k, jb, 0, nullptr, tiles,
-                                                                        ntiles, kdepth, kt);
+        tile_syrk_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
 }
 
-void launch_col_update(hipStream_t s, double* A, int64_t lda, int nt, int k, int jb, int ncols,
-                       int kdepth, KTime* kt) {
+void launch_col_update(hipStream_t s, double* C, int64_t ldc, const Panel& pn, int nt, int jb, int lj0,
+                       int ncols, int kdepth, KTime* kt) {
     const int m0 = nt - jb;
-    if (m0 <= 0) return;
+    if (m0 <= 0 || ncols <= 0) return;
     int tiles = 0;
     for (int c = 0; c < ncols && c < m0; ++c) tiles += m0 - c;
-    col_update_kernel<<<dim3((unsigned)(4 * tiles)), dim3(256), 0, s>>>(A, lda, k, jb, m0, kdepth, kt);
+    col_update_kernel<<<dim3((unsigned)(4 * tiles)), dim3(256), 0, s>>>(C, ldc, pn, jb, lj0, m0, kdepth, kt);
 }
 
 // Super-tile ordered list of the lower-triangular m x m tile set (entry = bi | bj << 16,
@@ -988,8 +896,9 @@ void build_tile_list(int m, uint32_t* out) {
                     out[n++] = (uint32_t)i | ((uint32_t)j << 16);
 }
 
-void launch_reduce(hipStream_t s, const double* A, int64_t lda, int64_t N, EvalResult* res) {
-    reduce_kernel<<<dim3(1), dim3(1024), 0, s>>>(A, lda, N, res);
+void launch_reduce(hipStream_t s, const double* C, int64_t ldc, int64_t N, int64_t ncols, ColMap cm,
+                   EvalResult* res) {
+    reduce_kernel<<<dim3(1), dim3(1024), 0, s>>>(C, ldc, N, ncols, cm, res);
 }
 
 void launch_init_result(hipStream_t s, EvalResult* res) {

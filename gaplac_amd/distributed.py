@@ -1,0 +1,281 @@
+"""Distributed log-marginal-likelihood: 1-D block-column cyclic Cholesky over ranks.
+
+BASELINE configs[3] (N = 65536 over the GPUs of one node) / SURVEY.md §8e. One process
+per GPU (torch.distributed: backend "nccl" = RCCL over xGMI). Each rank owns the
+super-panels s with s % world == rank (W = 4 tile columns of 128 each by default), builds
+only its own Gram tiles, and the only data-path exchange is one broadcast of each factored
+super-panel from its owner; the result needs one allreduce of (logdet, quad) and a min of
+the failing-pivot index. The compute lives in libgaplac_hip.so (gaplac_dist_* in
+include/gaplac.h); this module sequences the steps and issues the collectives.
+
+Reference semantics are those of gaplac_logpdf (AbstractGPs.logpdf(FiniteGP, v) at
+CLI/src/mcmc.jl:35 and CLI/src/select.jl:49-50): the same value to <= 1e-9 relative,
+PosDefException(info) on a non-positive pivot.
+
+Transports:
+  TorchTransport(group)  one rank per process; broadcasts with torch.distributed on the
+                         library's comm stream (RCCL on GPUs; gloo in CPU/1-GPU tests)
+  LoopbackTransport()    every rank of the job in this process on one device: the
+                         broadcast is a device-to-device copy (tests of the multi-rank
+                         schedule at any rank count on a single GPU)
+
+Schedule (per rank; every library call only enqueues work except finish):
+    begin; factor(0) [owner]; bcast(0)
+    for s in 0..nsp-1: factor(s+1) [owner of s+1]; update(s); bcast(s+1)
+    finish -> partial (logdet, quad, info); combine across ranks
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from ctypes import byref, c_double, c_int32, c_int64, c_void_p
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _native
+from ._native import term_array
+from .backend import ArgumentError, GaplacError, PosDefException, _colmajor
+
+LOG2PI = 1.8378770664093453  # Julia's log2π (AbstractGPs logpdf)
+DEFAULT_SPW = 4
+
+
+class DistRank:
+    """One rank's state (a gaplac_dist context) on `device`."""
+
+    def __init__(self, device: int, nranks: int, rank: int, spw: int = DEFAULT_SPW):
+        self.lib = _native.load()
+        h = c_void_p()
+        rc = self.lib.gaplac_dist_create(int(device), int(nranks), int(rank), int(spw), byref(h))
+        if rc != 0:
+            raise GaplacError(rc, f"gaplac_dist_create(device={device}, nranks={nranks}, rank={rank}) failed")
+        self.h = h
+        self.device, self.nranks, self.rank, self.spw = device, nranks, rank, spw
+        self._bufs = None  # torch tensors backing the panel buffers (kept alive here)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gaplac_dist_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc == 0:
+            return
+        msg = self.lib.gaplac_dist_last_error(self.h)
+        msg = msg.decode() if msg else ""
+        if rc in (_native.E_PARAM, _native.E_KIND, _native.E_COL, _native.E_ARG):
+            raise ArgumentError(f"gaplac error {rc}: {msg}")
+        raise GaplacError(rc, msg)
+
+    def owns(self, s: int) -> bool:
+        return s % self.nranks == self.rank
+
+    def geometry(self, N: int):
+        Np, pel = c_int64(), c_int64()
+        nt, nsp, nloc = c_int32(), c_int32(), c_int32()
+        self._check(self.lib.gaplac_dist_geometry(self.h, int(N), byref(Np), byref(nt), byref(nsp), byref(nloc),
+                                                  byref(pel)))
+        return dict(Np=Np.value, nt=nt.value, nsp=nsp.value, nloc=nloc.value, panel_elems=pel.value)
+
+    def use_torch_panel_buffers(self, N: int):
+        """Back the two panel buffers with torch tensors on this rank's device (so the
+        collective library broadcasts torch tensors)."""
+        import torch
+        need = self.geometry(N)["panel_elems"]
+        if self._bufs is None or self._bufs[0].numel() < need:
+            dev = torch.device("cuda", self.device)
+            self._bufs = [torch.empty(need, dtype=torch.float64, device=dev) for _ in range(2)]
+            self._check(self.lib.gaplac_dist_set_panel_buffers(
+                self.h, c_void_p(self._bufs[0].data_ptr()), c_void_p(self._bufs[1].data_ptr()), need))
+
+    def panel_tensor(self, s: int, count: int):
+        return self._bufs[s & 1][:count]
+
+    # ---- steps
+    def begin(self, X: np.ndarray, terms, noise: float, v: np.ndarray) -> int:
+        Xc = _colmajor(X)
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        N, D = Xc.shape
+        if v.shape[0] != N:
+            raise ArgumentError(f"length of v ({v.shape[0]}) != N ({N})")
+        terms = list(terms)
+        ta = term_array(terms)
+        nsp = c_int32()
+        self._check(self.lib.gaplac_dist_begin(self.h, N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), len(terms), ta,
+                                               float(noise), v.ctypes.data_as(c_void_p), 0, byref(nsp)))
+        return nsp.value
+
+    def begin_device(self, N: int, D: int, dX_ptr: int, ldx: int, terms, noise: float, dv_ptr: int) -> int:
+        terms = list(terms)
+        nsp = c_int32()
+        self._check(self.lib.gaplac_dist_begin(self.h, N, D, c_void_p(dX_ptr), ldx, len(terms), term_array(terms),
+                                               float(noise), c_void_p(dv_ptr), 1, byref(nsp)))
+        return nsp.value
+
+    def factor(self, s: int):
+        self._check(self.lib.gaplac_dist_factor(self.h, int(s)))
+
+    def panel(self, s: int):
+        ptr, count, root = c_void_p(), c_int64(), c_int32()
+        self._check(self.lib.gaplac_dist_panel(self.h, int(s), byref(ptr), byref(count), byref(root)))
+        return ptr.value, count.value, root.value
+
+    def comm_begin(self, s: int) -> int:
+        st = c_void_p()
+        self._check(self.lib.gaplac_dist_comm_begin(self.h, int(s), byref(st)))
+        return st.value or 0
+
+    def comm_end(self, s: int):
+        self._check(self.lib.gaplac_dist_comm_end(self.h, int(s)))
+
+    def update(self, s: int):
+        self._check(self.lib.gaplac_dist_update(self.h, int(s)))
+
+    def finish(self):
+        ld, q, info = c_double(), c_double(), c_int64()
+        self._check(self.lib.gaplac_dist_finish(self.h, byref(ld), byref(q), byref(info)))
+        return ld.value, q.value, info.value
+
+    def local(self, N: int) -> np.ndarray:
+        g = self.geometry(N)
+        out = np.zeros((g["Np"], g["nloc"] * 128), dtype=np.float64, order="F")
+        if g["nloc"]:
+            self._check(self.lib.gaplac_dist_local(self.h, out.ctypes.data_as(c_void_p), g["Np"]))
+        return out
+
+
+class TorchTransport:
+    """One rank per process; torch.distributed collectives on the rank's comm stream.
+
+    device: where the 3-number allreduce runs (default: the current CUDA device for the
+    nccl backend, the CPU otherwise)."""
+
+    def __init__(self, group=None, device=None):
+        self.group = group
+        self.device = device
+
+    def prepare(self, ranks: Sequence, N: int):
+        (r,) = ranks
+        r.use_torch_panel_buffers(N)
+
+    def bcast(self, ranks: Sequence, s: int):
+        import torch
+        import torch.distributed as dist
+        (r,) = ranks
+        _ptr, count, root = r.panel(s)
+        stream = r.comm_begin(s)
+        buf = r.panel_tensor(s, count)
+        src = dist.get_global_rank(self.group, root) if self.group is not None else root
+        if stream and buf.is_cuda:
+            with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=buf.device)):
+                dist.broadcast(buf, src=src, group=self.group, async_op=True).wait()
+        else:
+            dist.broadcast(buf, src=src, group=self.group)
+        r.comm_end(s)
+
+    def combine(self, parts: Sequence, device=None):
+        import torch
+        import torch.distributed as dist
+        (ld, q, info), = parts
+        dev = device if device is not None else self.device
+        if dev is None:
+            dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(self.group) == "nccl" else "cpu"
+        sums = torch.tensor([ld, q], dtype=torch.float64, device=dev)
+        imin = torch.tensor([info if info > 0 else np.iinfo(np.int64).max], dtype=torch.int64, device=dev)
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=self.group)
+        dist.all_reduce(imin, op=dist.ReduceOp.MIN, group=self.group)
+        info = int(imin.item())
+        return float(sums[0].item()), float(sums[1].item()), 0 if info == np.iinfo(np.int64).max else info
+
+
+class LoopbackTransport:
+    """All ranks of the job in this process, on one device: broadcast = D2D copies on the
+    receivers' comm streams, ordered after the root's pack; the root's comm stream then
+    waits for every copy, so its buffer is not re-packed before the copies have read it."""
+
+    def prepare(self, ranks: Sequence, N: int):
+        for r in ranks:
+            r.use_torch_panel_buffers(N)
+
+    def bcast(self, ranks: Sequence, s: int):
+        import torch
+        _p, count, root = ranks[0].panel(s)
+        rootr = next(r for r in ranks if r.rank == root)
+        streams = {r.rank: torch.cuda.ExternalStream(r.comm_begin(s), device=torch.device("cuda", r.device))
+                   for r in ranks}
+        src = rootr.panel_tensor(s, count)
+        for r in ranks:
+            if r.rank == root:
+                continue
+            st = streams[r.rank]
+            st.wait_stream(streams[root])
+            with torch.cuda.stream(st):
+                r.panel_tensor(s, count).copy_(src, non_blocking=True)
+            streams[root].wait_stream(st)
+        for r in ranks:
+            r.comm_end(s)
+
+    def combine(self, parts: Sequence, device=None):
+        ld = sum(p[0] for p in parts)
+        q = sum(p[1] for p in parts)
+        infos = [p[2] for p in parts if p[2] > 0]
+        return ld, q, (min(infos) if infos else 0)
+
+
+def run_schedule(ranks: Sequence, transport, nsp: int):
+    """Enqueue one evaluation's factorisation on the local ranks (begin already called)."""
+    for r in ranks:
+        if r.owns(0):
+            r.factor(0)
+    transport.bcast(ranks, 0)
+    for s in range(nsp):
+        if s + 1 < nsp:
+            for r in ranks:
+                if r.owns(s + 1):
+                    r.factor(s + 1)
+        for r in ranks:
+            r.update(s)
+        if s + 1 < nsp:
+            transport.bcast(ranks, s + 1)
+
+
+def finish(ranks: Sequence, transport, N: int, device=None, full: bool = False):
+    parts = [r.finish() for r in ranks]
+    ld, q, info = transport.combine(parts, device=device)
+    if info > 0:
+        raise PosDefException(info)
+    lp = -((N * LOG2PI + ld) + q) / 2.0
+    return (lp, ld, q) if full else lp
+
+
+def logpdf_dist(ranks: Sequence[DistRank], transport, X, terms, noise: float, v, full: bool = False,
+                device=None):
+    """logpdf of the zero-mean FiniteGP with the factorisation spread over the job's ranks.
+
+    ranks: the DistRank(s) this process drives ([one] with TorchTransport, all of them
+    with LoopbackTransport). Returns the same value on every rank."""
+    X = _colmajor(X)
+    N = X.shape[0]
+    if N == 0:
+        return (-0.0, 0.0, 0.0) if full else -0.0
+    transport.prepare(ranks, N)
+    nsps = [r.begin(X, terms, noise, v) for r in ranks]
+    run_schedule(ranks, transport, nsps[0])
+    return finish(ranks, transport, N, device=device, full=full)
+
+
+def logpdf_dist_device(ranks: Sequence[DistRank], transport, N: int, D: int, dX_ptr: int, ldx: int, terms,
+                       noise: float, dv_ptr: int, full: bool = False, device=None):
+    """As logpdf_dist with X (N x D column-major, leading dim ldx) and v already on the
+    device (the benchmark's entry)."""
+    transport.prepare(ranks, N)
+    nsps = [r.begin_device(N, D, dX_ptr, ldx, terms, noise, dv_ptr) for r in ranks]
+    run_schedule(ranks, transport, nsps[0])
+    return finish(ranks, transport, N, device=device, full=full)

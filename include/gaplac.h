@@ -151,6 +151,59 @@ int gaplac_set_profiling(gaplac_ctx* ctx, int on);
 int gaplac_get_stats(gaplac_ctx* ctx, gaplac_stats* out);
 int gaplac_reset_stats(gaplac_ctx* ctx);
 
+/* ------------------------------------------------------------------------------------
+ * Distributed evaluation (BASELINE configs[3]: N = 65536 over the GPUs of one node; one
+ * process per GPU). 1-D block-column cyclic Cholesky: super-panels of spw 128-wide
+ * tile columns are dealt round-robin over the ranks; each rank builds and stores only its
+ * own columns of the lower triangle (the Gram shards with no redistribution) and the only
+ * data-path exchange is one broadcast per super-panel of the factored panel, which the
+ * HOST enqueues with its collective library (ncclBroadcast = RCCL over xGMI) on the
+ * stream gaplac_dist_comm_begin returns. Same result as gaplac_logpdf (<= 1e-9 rel).
+ * Replaces, like gaplac_logpdf: AbstractGPs.logpdf(FiniteGP, v) — the GaPLAC-owned method
+ * would dispatch here when the job runs on several GPUs.
+ *
+ * Per rank, per evaluation (every call only enqueues, except finish):
+ *   gaplac_dist_begin(...)                         -> nsp
+ *   if (0 % nranks == rank) gaplac_dist_factor(d, 0)
+ *   bcast(0)
+ *   for s in 0..nsp-1:
+ *       if (s+1 < nsp && (s+1) % nranks == rank) gaplac_dist_factor(d, s+1)
+ *       gaplac_dist_update(d, s)
+ *       if (s+1 < nsp) bcast(s+1)
+ *   gaplac_dist_finish(d, &logdet_part, &quad_part, &info_part)
+ *   allreduce: logdet = sum, quad = sum, info = min over nonzero; then
+ *   logpdf = -(N*log(2*pi) + logdet + quad) / 2   (NaN / PosDefException if info > 0)
+ * where bcast(s) = gaplac_dist_panel(d, s, &buf, &count, &root);
+ *                  gaplac_dist_comm_begin(d, s, &stream);
+ *                  ncclBroadcast(buf, buf, count, ncclDouble, root, comm, stream);
+ *                  gaplac_dist_comm_end(d, s);
+ * ---------------------------------------------------------------------------------- */
+typedef struct gaplac_dist gaplac_dist;
+int gaplac_dist_create(int device, int nranks, int rank, int spw, gaplac_dist** out);
+int gaplac_dist_destroy(gaplac_dist* d);
+const char* gaplac_dist_last_error(const gaplac_dist* d);
+/* Padded order Np = roundup(N+1, 128), tile columns nt, super-panels nsp, this rank's
+ * local tile columns nloc, and the doubles one panel buffer must hold. */
+int gaplac_dist_geometry(gaplac_dist* d, int64_t N, int64_t* Np, int32_t* nt, int32_t* nsp,
+                         int32_t* nloc, int64_t* panel_elems);
+/* Optional: two caller-owned device panel buffers (e.g. allocated by the collective
+ * library's host binding), each of >= panel_elems doubles; NULLs = library-owned. */
+int gaplac_dist_set_panel_buffers(gaplac_dist* d, void* buf0, void* buf1, int64_t capacity);
+/* Inputs as for gaplac_logpdf (inputs_on_device: X and v are device pointers). Builds
+ * this rank's Gram tiles; returns the number of super-panels in *out_nsp. */
+int gaplac_dist_begin(gaplac_dist* d, int64_t N, int32_t D, const double* X, int64_t ldx,
+                      int32_t T, const gaplac_term* terms, double noise, const double* v,
+                      int inputs_on_device, int32_t* out_nsp);
+int gaplac_dist_factor(gaplac_dist* d, int32_t s);   /* owner of super-panel s only */
+int gaplac_dist_panel(gaplac_dist* d, int32_t s, void** buf, int64_t* count, int32_t* root);
+int gaplac_dist_comm_begin(gaplac_dist* d, int32_t s, void** hip_stream);
+int gaplac_dist_comm_end(gaplac_dist* d, int32_t s);
+int gaplac_dist_update(gaplac_dist* d, int32_t s);
+/* This rank's partial logdet / quad and first failing pivot (0 = none); synchronises. */
+int gaplac_dist_finish(gaplac_dist* d, double* logdet_part, double* quad_part, int64_t* info_part);
+/* Debug / parity: this rank's column storage (Np x nloc*128, column-major) to host. */
+int gaplac_dist_local(gaplac_dist* d, double* out, int64_t ld);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,113 @@
+"""Distributed (1-D block-column cyclic) schedule on CPU: gaplac_amd/distributed.py driving
+numpy test-double ranks (tests/dist_sim.py) — in one process over an in-process broadcast,
+and as a world_size-2 gloo process group through TorchTransport (the same code path the
+GPUs run over RCCL). Checked against the oracle (<= 1e-9 relative, the north_star bar;
+observed ~1e-15)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from gaplac_amd import distributed as DI
+from gaplac_amd.backend import PosDefException
+from oracle import restatement as R
+from tests.dist_sim import SimRank
+
+RTOL = 1e-9
+
+
+class CpuLoopback(DI.LoopbackTransport):
+    def prepare(self, ranks, N):
+        for r in ranks:
+            r.use_torch_panel_buffers(N)
+
+    def bcast(self, ranks, s):
+        _p, count, root = ranks[0].panel(s)
+        src = next(r for r in ranks if r.rank == root).panel_tensor(s, count)
+        for r in ranks:
+            if r.rank != root:
+                r.panel_tensor(s, count).copy_(src)
+
+
+def _case(N, seed=0):
+    rng = np.random.default_rng(seed)
+    t = rng.uniform(0, 10, N)
+    g = rng.integers(0, max(1, N // 3), N).astype(float)
+    v = rng.standard_normal(N)
+    X = np.column_stack([t, g])
+    terms = [(1, 0, 1.5, 0), (2, 0, 3.0, 1), (4, 1, 0.0, 2), (5, -1, 1.0, 3)]
+    return X, terms, v
+
+
+@pytest.mark.parametrize("world,spw,N", [(1, 2, 150), (2, 2, 150), (3, 1, 200), (4, 2, 257), (5, 3, 95), (8, 1, 40)])
+def test_loopback_schedule_matches_oracle(world, spw, N):
+    X, terms, v = _case(N, seed=world)
+    ranks = [SimRank(world, r, spw=spw, nb=16) for r in range(world)]
+    lp, ld, q = DI.logpdf_dist(ranks, CpuLoopback(), X, terms, 0.1, v, full=True)
+    rl, rd, rq = R.logpdf(X, terms, 0.1, v)
+    assert abs(lp - rl) <= RTOL * abs(rl)
+    assert abs(ld - rd) <= 1e-9 * max(1.0, abs(rd))
+    assert abs(q - rq) <= 1e-9 * max(1.0, abs(rq))
+
+
+def test_loopback_more_ranks_than_superpanels():
+    X, terms, v = _case(20, seed=3)  # nt = 2 tiles of 16 -> 1 super-panel at spw=2
+    ranks = [SimRank(4, r, spw=2, nb=16) for r in range(4)]
+    lp = DI.logpdf_dist(ranks, CpuLoopback(), X, terms, 0.1, v)
+    assert abs(lp - R.logpdf(X, terms, 0.1, v)[0]) <= RTOL * abs(lp)
+
+
+def test_loopback_non_pd_reports_first_failing_pivot():
+    rng = np.random.default_rng(5)
+    N = 90
+    g = rng.integers(0, 10, N).astype(float)
+    X = g[:, None]
+    v = rng.standard_normal(N)
+    terms = [(4, 0, 0.0, 0)]
+    with pytest.raises(R.PosDefException) as ref:
+        R.logpdf(X, terms, 0.0, v)
+    ranks = [SimRank(3, r, spw=1, nb=16) for r in range(3)]
+    with pytest.raises(PosDefException) as got:
+        DI.logpdf_dist(ranks, CpuLoopback(), X, terms, 0.0, v)
+    assert got.value.info == ref.value.info
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        X, terms, v = _case(230, seed=11)
+        r = SimRank(world, rank, spw=2, nb=16)
+        lp, ld, qd = DI.logpdf_dist([r], DI.TorchTransport(), X, terms, 0.1, v, full=True)
+        q.put((rank, lp, ld, qd))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_torch_transport():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    X, terms, v = _case(230, seed=11)
+    rl = R.logpdf(X, terms, 0.1, v)[0]
+    for rank, lp, ld, qd in got:
+        assert abs(lp - rl) <= RTOL * abs(rl)
+    assert got[0][1] == got[1][1]  # every rank returns the same value

@@ -41,9 +41,9 @@ int main() {
     float ms;
     CK(hipEventRecord(e0)); launch_trsm(0, A, Np, 2, 0, Dinv, nullptr); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(&ms, e0, e1)); printf("trsm 1 tile: %.1f us  ", ms * 1e3);
-    CK(hipEventRecord(e0)); launch_col_update(0, A, Np, nt, 0, 1, 1, NB, nullptr); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    CK(hipEventRecord(e0)); launch_col_update(0, A, Np, Panel{A, Np, 0}, nt, 1, 1, 1, NB, nullptr); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(&ms, e0, e1)); printf("col_update 3 tiles K=128: %.1f us  ", ms * 1e3);
-    CK(hipEventRecord(e0)); launch_col_update(0, A, Np, nt, 0, 2, 2, 256, nullptr); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    CK(hipEventRecord(e0)); launch_col_update(0, A, Np, Panel{A, Np, 0}, nt, 2, 2, 2, 256, nullptr); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(&ms, e0, e1)); printf("col_update 2 cols K=256: %.1f us\n", ms * 1e3);
   }
   return 0;
