@@ -114,7 +114,16 @@ def main():
     ap.add_argument("--skip-cpu", action="store_true", help="skip the CPU baseline leg (profiling runs)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event pass")
     ap.add_argument("--profile-steps", type=int, default=2, help="eager steps timed per kernel after the timed region")
+    ap.add_argument("--mode", choices=("replicas", "dist", "single"), default="replicas",
+                    help="replicas (default, the headline metric): independent evals per GPU; dist: one "
+                         "evaluation spread over all ranks (BASELINE configs[3], N=65536); single: the "
+                         "single-GPU path at --n (comparison line for dist)")
+    ap.add_argument("--loopback", type=int, default=0,
+                    help="dist mode on ONE GPU: emulate this many ranks in-process (schedule timing only)")
+    ap.add_argument("--spw", type=int, default=4, help="dist mode: super-panel width in 128-column tiles")
     args = ap.parse_args()
+    if args.mode in ("dist", "single"):
+        return main_dist(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -144,6 +153,11 @@ def main():
     for i in range(args.warmup):
         step(i)
 
+    # hipEvents on s_main around every bulk trailing-update launch of the timed steps
+    # (the production schedule; gaplac_set_profiling mode 2) give the roofline's
+    # per-launch duration.
+    ctx.reset_stats()
+    ctx.set_profiling(0 if args.no_profile else 2)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -155,12 +169,12 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ctx.set_profiling(0)
+    st_ev = ctx.stats()
 
-    # Per-kernel timing for the roofline: a separate pass right after the timed region,
-    # same inputs, replaying the same captured schedule with per-launch device timestamps
-    # wired in (first workgroup start / last wave end on the 100 MHz s_memrealtime clock;
-    # HIP timing events recorded inside a captured graph report no elapsed time on ROCm
-    # 7.2). Cross-checked against the rocprofv3 kernel-trace summaries in profiles/.
+    # Per-kernel breakdown (extra): a separate pass right after the timed region, same
+    # inputs, with per-launch device timestamps wired into every kernel (first workgroup
+    # start / last wave end on the 100 MHz s_memrealtime clock).
     st = None
     if not args.no_profile and args.profile_steps > 0:
         ctx.reset_stats()
@@ -185,9 +199,9 @@ def main():
         return
 
     roofline = None
-    if st and st["syrk_launches"] > 0 and st["syrk_ms"] > 0:
-        flops_per_launch = st["syrk_flops"] / st["syrk_launches"]
-        avg_s = st["syrk_ms"] / st["syrk_launches"] / 1e3
+    if st_ev["syrk_launches"] > 0 and st_ev["syrk_ms"] > 0:
+        flops_per_launch = st_ev["syrk_flops"] / st_ev["syrk_launches"]
+        avg_s = st_ev["syrk_ms"] / st_ev["syrk_launches"] / 1e3
         achieved = flops_per_launch / avg_s / 1e12
         traffic, traffic_src = load_traffic()
         roofline = {
@@ -199,11 +213,11 @@ def main():
             "frac": round(achieved / PEAK_F64_TFLOPS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "traffic_algorithmic": st["syrk_bytes"] / st["syrk_launches"],
+            "traffic_algorithmic": st_ev["syrk_bytes"] / st_ev["syrk_launches"],
             "flops_per_launch": flops_per_launch,
-            "avg_launch_ms": st["syrk_ms"] / st["syrk_launches"],
-            "launches": st["syrk_launches"],
-            "timing": "per-launch device timestamps (s_memrealtime, first WG start to last wave end) in a profiled replay of the same graph after the timed region; cf. profiles/*kernel_stats.csv",
+            "avg_launch_ms": st_ev["syrk_ms"] / st_ev["syrk_launches"],
+            "launches": st_ev["syrk_launches"],
+            "timing": "hipEvents recorded on the launching stream (s_main) around every tile_syrk_kernel launch inside the timed region; cf. profiles/*kernel_stats.csv (rocprofv3 --kernel-trace --stats of the same command)",
         }
     eval_flops = N ** 3 / 3.0 + N ** 2
     eval_tflops = eval_flops * (value / world) / 1e12
@@ -227,6 +241,8 @@ def main():
         extra["colupd_ms_per_eval"] = st["colupd_ms"] / st["evals"]
         extra["syrk_ms_per_eval"] = st["syrk_ms"] / st["evals"]
         extra["small_update_ms_per_eval"] = st["small_ms"] / st["evals"]
+        if st["syrk_launches"]:
+            extra["syrk_avg_launch_ms_stamps"] = st["syrk_ms"] / st["syrk_launches"]
 
     cpu = None
     if world == 1 and not args.skip_cpu:
@@ -257,6 +273,84 @@ def main():
     }
     print(json.dumps(out), flush=True)
     if world > 1:
+        dist.destroy_process_group()
+
+
+def make_inputs_dist(N: int, seed: int = 3):
+    """BASELINE configs[3]: SqExp(:x) l=1.5, x ~ U(-5, 5), v ~ N(0, 1)."""
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(-5.0, 5.0, N)
+    v = rng.standard_normal(N)
+    return x, v
+
+
+def main_dist(args):
+    """One evaluation spread over the ranks of the job (strong scaling: total work fixed)."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    from gaplac_amd import distributed as DI
+    from gaplac_amd.backend import Context
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    N = args.n if args.n != N_DEFAULT else 65536
+    x, v = make_inputs_dist(N)
+    dX = torch.from_numpy(x).to("cuda")
+    dv = torch.from_numpy(v).to("cuda")
+    terms = [(SQEXP, 0, 1.5, 0)]
+    nranks = args.loopback if args.loopback > 0 else world
+    if args.mode == "single":
+        ctx = Context(local_rank)
+        step = lambda: ctx.logpdf_device(N, 1, dX.data_ptr(), N, terms, 0.1, dv.data_ptr())
+        parallelism = "single"
+    else:
+        if args.loopback > 0 or world == 1:
+            nranks = max(1, args.loopback)
+            ranks = [DI.DistRank(local_rank, nranks, r, spw=args.spw) for r in range(nranks)]
+            tr = DI.LoopbackTransport()
+        else:
+            ranks = [DI.DistRank(local_rank, world, rank, spw=args.spw)]
+            tr = DI.TorchTransport(device=torch.device("cuda", local_rank))
+        step = lambda: DI.logpdf_dist_device(ranks, tr, N, 1, dX.data_ptr(), N, terms, 0.1, dv.data_ptr())
+        parallelism = f"1-D block-column cyclic over {nranks} rank(s)" + (" (in-process loopback)" if args.loopback else "")
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lp = None
+    for _ in range(args.steps):
+        lp = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        value = args.steps / elapsed
+        flops = N ** 3 / 3.0 + N ** 2
+        tf_per_gpu = flops * value / 1e12 / max(1, world)
+        out = {
+            "metric": f"log-marginal-likelihood evals/sec at N={N} fp64 (one evaluation over all GPUs)",
+            "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded x~U(-5,5), v~N(0,1); inputs resident in HBM)",
+            "config": {"workload": f"BASELINE configs[3]: SqExp(:x; l=1.5), N={N}, noise 0.1", "N": N,
+                       "parallelism": parallelism, "spw": args.spw, "mode": args.mode},
+            "extra": {"achieved_tflops_per_gpu": round(tf_per_gpu, 3),
+                      "frac_of_fp64_peak": round(tf_per_gpu / PEAK_F64_TFLOPS, 4), "last_logpdf": lp},
+        }
+        print(json.dumps(out), flush=True)
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -153,8 +153,10 @@ class Context:
         self._check(rc)
         return L, z
 
-    def set_profiling(self, on: bool):
-        self.lib.gaplac_set_profiling(self.h, 1 if on else 0)
+    def set_profiling(self, mode):
+        """0/False off, 1/True per-launch device timestamps, 2 hipEvents around the bulk
+        trailing-update launches (production schedule)."""
+        self.lib.gaplac_set_profiling(self.h, int(mode))
 
     def stats(self) -> dict:
         s = _native.Stats()

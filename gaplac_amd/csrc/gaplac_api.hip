@@ -44,8 +44,17 @@ struct gaplac_ctx {
     TermPack* dtp = nullptr;     // device copy of the term descriptor (read by gram_kernel)
     TermPack* htp = nullptr;     // pinned staging for it
     std::string err;
-    // profiling: per-launch device timestamps (KTime slots), see kt_begin/kt_end
-    bool profiling = false;
+    // profiling: 1 = per-launch device timestamps (KTime slots, see kt_begin/kt_end);
+    // 2 = hipEvents recorded on s_main around every bulk tile_syrk launch (eager launches),
+    //     read back by gaplac_get_stats
+    int prof_mode = 0;
+    bool profiling = false;  // prof_mode == 1
+    std::vector<hipEvent_t> evpool;
+    struct EvPair {
+        size_t i0;
+        double flops, bytes;
+    };
+    std::vector<EvPair> evpairs;
     bool serial = false;  // GAPLAC_SERIAL=1: one stream, no overlap (per-kernel timing)
     int spw = 4;          // GAPLAC_SPW: super-panel width in 128-column tiles (bulk K = 128 spw)
     gaplac_stats stats{};
@@ -326,9 +335,24 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             const BulkArgs ba{ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0},
                               ctx->tiles + ctx->tile_off[(size_t)m], m * (m + 1) / 2, kd, jb, jb,
                               ColMap{1, 0, W}};
-            KTime* kt = syrk_is_small(ba.ntiles) ? slot(ctx, 6, 0)
-                                                 : slot(ctx, 0, syrk_flops(m) * (kd / NB), syrk_bytes(m, kd));
+            const bool small = syrk_is_small(ba.ntiles);
+            KTime* kt = small ? slot(ctx, 6, 0) : slot(ctx, 0, syrk_flops(m) * (kd / NB), syrk_bytes(m, kd));
+            const bool ev = ctx->prof_mode == 2 && !small;
+            size_t e0 = 0;
+            if (ev) {
+                e0 = 2 * ctx->evpairs.size();
+                while (ctx->evpool.size() < e0 + 2) {
+                    hipEvent_t e;
+                    HIPCK(ctx, hipEventCreate(&e));
+                    ctx->evpool.push_back(e);
+                }
+                HIPCK(ctx, hipEventRecord(ctx->evpool[e0], sm));
+            }
             launch_bulk(sm, ba, kt);
+            if (ev) {
+                HIPCK(ctx, hipEventRecord(ctx->evpool[e0 + 1], sm));
+                ctx->evpairs.push_back({e0, syrk_flops(m) * (kd / NB), syrk_bytes(m, kd)});
+            }
         }
         HIPCK(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
     }
@@ -410,7 +434,7 @@ int eval_device(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp, EvalR
     }
     *ctx->htp = tp;
     HIPCK(ctx, hipMemcpyAsync(ctx->dtp, ctx->htp, sizeof(TermPack), hipMemcpyHostToDevice, ctx->s_main));
-    if (ctx->use_graph && !ctx->serial) {
+    if (ctx->use_graph && !ctx->serial && ctx->prof_mode != 2) {
         hipGraph_t& G = prof ? ctx->pgraph : ctx->graph;
         hipGraphExec_t& GX = prof ? ctx->pgexec : ctx->gexec;
         int64_t& GN = prof ? ctx->pgN : ctx->gN;
@@ -604,6 +628,7 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     if (ctx->dv) (void)hipFree(ctx->dv);
     drop_graph(ctx, false);
     drop_graph(ctx, true);
+    for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
     if (ctx->dkt) (void)hipFree(ctx->dkt);
     if (ctx->hkt) (void)hipHostFree(ctx->hkt);
     if (ctx->dres) (void)hipFree(ctx->dres);
@@ -744,14 +769,28 @@ int gaplac_factor(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_
     return finish(r, nullptr, nullptr, nullptr);
 }
 
-int gaplac_set_profiling(gaplac_ctx* ctx, int on) {
-    if (!ctx) return GAPLAC_E_ARG;
-    ctx->profiling = on != 0;
+int gaplac_set_profiling(gaplac_ctx* ctx, int mode) {
+    if (!ctx || mode < 0 || mode > 2) return GAPLAC_E_ARG;
+    ctx->prof_mode = mode;
+    ctx->profiling = mode == 1;
     return 0;
 }
 
 int gaplac_get_stats(gaplac_ctx* ctx, gaplac_stats* out) {
     if (!ctx || !out) return GAPLAC_E_ARG;
+    if (!ctx->evpairs.empty()) {  // fold the event-timed bulk launches in
+        HIPCK(ctx, hipSetDevice(ctx->device));
+        HIPCK(ctx, hipStreamSynchronize(ctx->s_main));
+        for (const auto& p : ctx->evpairs) {
+            float ms = 0.f;
+            HIPCK(ctx, hipEventElapsedTime(&ms, ctx->evpool[p.i0], ctx->evpool[p.i0 + 1]));
+            ctx->stats.syrk_ms += ms;
+            ctx->stats.syrk_flops += p.flops;
+            ctx->stats.syrk_bytes += p.bytes;
+            ctx->stats.syrk_launches += 1;
+        }
+        ctx->evpairs.clear();
+    }
     *out = ctx->stats;
     return 0;
 }
@@ -759,6 +798,7 @@ int gaplac_get_stats(gaplac_ctx* ctx, gaplac_stats* out) {
 int gaplac_reset_stats(gaplac_ctx* ctx) {
     if (!ctx) return GAPLAC_E_ARG;
     ctx->stats = gaplac_stats{};
+    ctx->evpairs.clear();
     return 0;
 }
 

@@ -337,6 +337,9 @@ int gaplac_dist_factor(gaplac_dist* d, int32_t s) {
     hipStream_t sp = d->s_panel;
     const int c0 = sp_first(d, s), w = sp_width(d, s), lc0 = sp_local(d, s);
     const int64_t ldc = d->Np;
+    // update(s-2) (s_main) was the last bulk update of SP s's columns, and it read panel
+    // buffer s&1, which the pack below overwrites
+    DCK(d, hipStreamWaitEvent(sp, d->ev_free_main[s & 1], 0));
     if (s > 0) {
         DCK(d, hipStreamWaitEvent(sp, d->ev_recv[(s - 1) & 1], 0));
         launch_col_update(sp, d->C, ldc, panel_of(d, s - 1), d->nt, c0, lc0, w, sp_width(d, s - 1) * NB, nullptr);
@@ -352,8 +355,6 @@ int gaplac_dist_factor(gaplac_dist* d, int32_t s) {
             launch_potrf_diag(sp, Acol + (int64_t)c * NB, ldc, d->N, (int64_t)c * NB, Dk, d->dres, nullptr);
         launch_trsm(sp, Acol, ldc, d->nt, c, Dk, nullptr);
     }
-    // buffer s&1 held panel s-2: its bulk update must be done before it is overwritten
-    DCK(d, hipStreamWaitEvent(sp, d->ev_free_main[s & 1], 0));
     const int64_t r0 = panel_row0(d, s), ldp = panel_ld(d, s);
     DCK(d, hipMemcpy2DAsync(d->pbuf[s & 1], (size_t)ldp * 8, d->C + (int64_t)lc0 * NB * ldc + r0, (size_t)ldc * 8,
                             (size_t)ldp * 8, (size_t)w * NB, hipMemcpyDeviceToDevice, sp));

@@ -127,9 +127,14 @@ int gaplac_factor(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_
                   int32_t T, const gaplac_term* terms, double noise, const double* v,
                   double* out_L, int64_t ldl, double* out_z);
 
-/* Per-kernel timing of the evaluations run while profiling is on (off by default):
- * per-launch device timestamps (first workgroup start, last wave end; 100 MHz
- * s_memrealtime), accumulated until gaplac_reset_stats. */
+/* Per-kernel timing of the evaluations run while profiling is on (off by default),
+ * accumulated until gaplac_reset_stats. gaplac_set_profiling mode:
+ *   0 off;
+ *   1 per-launch device timestamps of every kernel (first workgroup start, last wave
+ *     end; 100 MHz s_memrealtime);
+ *   2 hipEvents recorded on the launching stream around every bulk trailing-update
+ *     (tile_syrk_kernel) launch, the production schedule otherwise unchanged: fills
+ *     syrk_* only, read back at gaplac_get_stats. */
 typedef struct gaplac_stats {
     int64_t evals;
     int64_t syrk_launches;      /* bulk trailing-update launches (tile_gemm_kernel<0>) */
@@ -147,7 +152,7 @@ typedef struct gaplac_stats {
     int64_t small_launches;     /* small trailing updates (quad_bulk_kernel), not in syrk_* */
     double  small_ms;
 } gaplac_stats;
-int gaplac_set_profiling(gaplac_ctx* ctx, int on);
+int gaplac_set_profiling(gaplac_ctx* ctx, int mode);
 int gaplac_get_stats(gaplac_ctx* ctx, gaplac_stats* out);
 int gaplac_reset_stats(gaplac_ctx* ctx);
 

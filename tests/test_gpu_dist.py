@@ -92,6 +92,20 @@ def test_one_rank_matches_single_gpu_path():
     assert abs(got - ref) <= 1e-12 * abs(ref)
 
 
+@pytest.mark.parametrize("world,spw,N", [(1, 4, 16384), (2, 1, 8192), (4, 2, 12000)])
+def test_loopback_large_matches_single_gpu(world, spw, N):
+    """Sizes whose bulk updates run the 128x128 tile kernel on the distributed layout
+    (> 512 tiles per launch) and long enough to expose stream-ordering races; checked
+    against the single-GPU path (itself parity-tested against the oracle)."""
+    X, terms, v = _case(N, seed=N)
+    with Context(0) as ctx:
+        ref = ctx.logpdf(X, terms, 0.1, v)
+    ranks = _ranks(world, spw)
+    for _ in range(2):
+        got = DI.logpdf_dist(ranks, DI.LoopbackTransport(), X, terms, 0.1, v)
+        assert abs(got - ref) <= 1e-11 * abs(ref)
+
+
 def test_loopback_non_pd_info():
     rng = np.random.default_rng(5)
     N = 700
