@@ -92,7 +92,7 @@ def cpu_baseline(N: int, budget_s: float = 25.0):
 
 # PMC traffic of the dominant kernel (tools/profile_round.sh: FETCH_SIZE / WRITE_SIZE
 # passes over the same command, corrected per MI355X_MICROARCH.md; per launch).
-TRAFFIC_FILE = os.path.join("profiles", "r01b_traffic_syrk.json")
+TRAFFIC_FILE = os.path.join("profiles", "r01d_traffic_syrk.json")
 
 
 def load_traffic():
@@ -206,7 +206,7 @@ def main():
         traffic, traffic_src = load_traffic()
         roofline = {
             "bound": "mfma",
-            "kernel": "tile_gemm_kernel<0> (bulk trailing SYRK, K=512, fp64 MFMA 16x16x4)",
+            "kernel": "tile_syrk_kernel (bulk trailing update, 128x128 tiles, K=512, fp64 MFMA 16x16x4)",
             "achieved": round(achieved, 3),
             "peak": PEAK_F64_TFLOPS,
             "unit": "TFLOP/s",

@@ -26,7 +26,7 @@ def per_dispatch(d, counter, kern):
 
 def main():
     fd, wd, out = sys.argv[1:4]
-    kern = sys.argv[4] if len(sys.argv) > 4 else "tile_gemm_kernel<0>"
+    kern = sys.argv[4] if len(sys.argv) > 4 else "tile_syrk_kernel"
     fetch = per_dispatch(fd, "FETCH_SIZE", kern)
     write = per_dispatch(wd, "WRITE_SIZE", kern)
     if not fetch or not write:
