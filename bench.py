@@ -114,16 +114,19 @@ def main():
     ap.add_argument("--skip-cpu", action="store_true", help="skip the CPU baseline leg (profiling runs)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event pass")
     ap.add_argument("--profile-steps", type=int, default=2, help="eager steps timed per kernel after the timed region")
-    ap.add_argument("--mode", choices=("replicas", "dist", "single"), default="replicas",
+    ap.add_argument("--mode", choices=("replicas", "dist", "single", "select"), default="replicas",
                     help="replicas (default, the headline metric): independent evals per GPU; dist: one "
                          "evaluation spread over all ranks (BASELINE configs[3], N=65536); single: the "
-                         "single-GPU path at --n (comparison line for dist)")
+                         "single-GPU path at --n (comparison line for dist); select: BASELINE configs[4], "
+                         "64 candidate formulas x N=8192 through gaplac_logpdf_batch, sharded over ranks")
     ap.add_argument("--loopback", type=int, default=0,
                     help="dist mode on ONE GPU: emulate this many ranks in-process (schedule timing only)")
     ap.add_argument("--spw", type=int, default=4, help="dist mode: super-panel width in 128-column tiles")
     args = ap.parse_args()
     if args.mode in ("dist", "single"):
         return main_dist(args)
+    if args.mode == "select":
+        return main_select(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -282,6 +285,90 @@ def make_inputs_dist(N: int, seed: int = 3):
     x = rng.uniform(-5.0, 5.0, N)
     v = rng.standard_normal(N)
     return x, v
+
+
+def select_models():
+    """BASELINE configs[4]: 64 candidate formulas = 16 structures over the columns
+    (x, t, subject) x lengthscales {0.5, 1, 2, 4}. Columns: 0 x, 1 t,
+    2 subject; every term is its own group (GaPLAC formulas lower to sums)."""
+    x, t, g = 0, 1, 2
+    structures = [
+        lambda l: [(SQEXP, x, l)], lambda l: [(OU, x, l)], lambda l: [(SQEXP, t, l)], lambda l: [(OU, t, l)],
+        lambda l: [(SQEXP, x, l), (CAT, g, 0.0)], lambda l: [(OU, t, l), (CAT, g, 0.0)],
+        lambda l: [(SQEXP, x, l), (OU, t, 2 * l)], lambda l: [(SQEXP, t, l), (LINEAR, x, 0.5)],
+        lambda l: [(SQEXP, x, l), (SQEXP, t, l)], lambda l: [(OU, x, l), (CAT, g, 0.0)],
+        lambda l: [(SQEXP, t, l), (OU, t, 3.0), (CAT, g, 0.0)], lambda l: [(LINEAR, x, l), (CAT, g, 0.0)],
+        lambda l: [(SQEXP, x, l), (OU, x, l), (CAT, g, 0.0)], lambda l: [(OU, t, l), (LINEAR, t, 1.0)],
+        lambda l: [(SQEXP, x, l), (SQEXP, t, 2 * l), (CAT, g, 0.0)],
+        lambda l: [(SQEXP, t, l), (OU, x, l), (LINEAR, x, 0.0), (CAT, g, 0.0)],
+    ]
+    models = []
+    for mk in structures:
+        for l in (0.5, 1.0, 2.0, 4.0):
+            models.append([(k, c, p, i) for i, (k, c, p) in enumerate(mk(l))])
+    return models
+
+
+def main_select(args):
+    """Batched select over 64 formulas (one gaplac_logpdf_batch call per rank; candidates
+    sharded round-robin over ranks, results all-gathered: gaplac_amd/replicas.py)."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    from gaplac_amd import replicas
+    from gaplac_amd.backend import Context
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    N = args.n if args.n != N_DEFAULT else 8192
+    rng = np.random.default_rng(4)
+    X = np.column_stack([rng.uniform(-5, 5, N), rng.uniform(0, 10, N),
+                         rng.integers(0, max(1, N // 3), N).astype(np.float64)])
+    y = rng.standard_normal(N)
+    models = select_models()
+    ctx = Context(local_rank)
+    mine = replicas.shard(len(models), rank, world)
+
+    def step():
+        out, info = ctx.logpdf_batch(X, [models[u] for u in mine], 0.1, y)
+        if world > 1:
+            return replicas.gather_results(mine, list(out), len(models), device=torch.device("cuda", local_rank))
+        return out
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        value = args.steps * len(models) / elapsed
+        out = {
+            "metric": f"select: log-marginal-likelihood evals/sec, {len(models)} formulas x N={N} fp64",
+            "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded x~U(-5,5), t~U(0,10), subject~randint(0,N/3), y~N(0,1))",
+            "config": {"workload": f"BASELINE configs[4]: {len(models)} candidate formulas, N={N}, noise 0.1", "N": N,
+                       "parallelism": f"candidates round-robin over {world} rank(s)"},
+            "extra": {"n_finite": int(np.isfinite(res).sum())},
+        }
+        print(json.dumps(out), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
 
 
 def main_dist(args):

@@ -80,6 +80,11 @@ struct gaplac_ctx {
     const void* gptrs[6] = {};
     const void* pgptrs[6] = {};
     std::vector<Slot> pslots;
+    // Batched select: models in flight on independent lanes (child contexts with their
+    // own workspace and streams; they read the parent's uploaded X and v).
+    std::vector<gaplac_ctx*> lanes;
+    int batch_lanes = 2;           // GAPLAC_BATCH_LANES (measured at N=8192: 1 lane 138, 2 lanes 191, 3-6 lanes 161-187 evals/s)
+    bool borrowed_inputs = false;  // dX / dv belong to the parent
 };
 
 namespace {
@@ -412,16 +417,42 @@ void drop_graph(gaplac_ctx* ctx, bool prof) {
     if (prof) ctx->pslots.clear();
 }
 
-// Full evaluation; inputs already in ctx->dX (ld N) / ctx->dv, term pack in tp (host).
-// Leaves the factor in ctx->A.
-int eval_device(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp, EvalResult* out) {
+// Workspace for order N (grown on demand).
+int ensure_workspace(gaplac_ctx* ctx, int64_t N) {
     const int64_t Np = round_up(N + 1, NB);
     const int nt = (int)(Np / NB);
     int rc;
     HIPCK(ctx, hipSetDevice(ctx->device));
     if ((rc = ensure(ctx, &ctx->A, &ctx->A_elems, (size_t)Np * Np))) return rc;
     if ((rc = ensure(ctx, &ctx->Dinv, &ctx->Dinv_elems, (size_t)nt * DINV_PER_BLOCK))) return rc;
-    if ((rc = ensure_tile_lists(ctx, nt))) return rc;
+    return ensure_tile_lists(ctx, nt);
+}
+
+// Eager enqueue of one evaluation (no profiling, no wait): the batch lanes.
+int eval_enqueue(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp) {
+    int rc;
+    if ((rc = ensure_workspace(ctx, N))) return rc;
+    const int64_t Np = round_up(N + 1, NB);
+    *ctx->htp = tp;
+    HIPCK(ctx, hipMemcpyAsync(ctx->dtp, ctx->htp, sizeof(TermPack), hipMemcpyHostToDevice, ctx->s_main));
+    ctx->slots.clear();
+    ctx->recording = false;
+    return enqueue_eval(ctx, N, D, Np, (int)(Np / NB));
+}
+
+int eval_wait(gaplac_ctx* ctx, EvalResult* out) {
+    HIPCK(ctx, hipStreamSynchronize(ctx->s_main));
+    *out = *ctx->hres;
+    return 0;
+}
+
+// Full evaluation; inputs already in ctx->dX (ld N) / ctx->dv, term pack in tp (host).
+// Leaves the factor in ctx->A.
+int eval_device(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp, EvalResult* out) {
+    const int64_t Np = round_up(N + 1, NB);
+    const int nt = (int)(Np / NB);
+    int rc;
+    if ((rc = ensure_workspace(ctx, N))) return rc;
     const bool prof = ctx->profiling;
     if (prof) {
         const size_t need = (size_t)nt * 6 + 16;  // launches per evaluation, with margin
@@ -546,6 +577,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     ctx->device = device;
     if (const char* s = std::getenv("GAPLAC_SERIAL")) ctx->serial = s[0] == '1';
     if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
+    if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     auto fail = [&](const char* what, hipError_t e) {
         std::fprintf(stderr, "gaplac_ctx_create: %s: %s\n", what, hipGetErrorString(e));
         gaplac_ctx_destroy(ctx);
@@ -613,6 +645,12 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->s_main) (void)hipStreamSynchronize(ctx->s_main);
     if (ctx->s_panel) (void)hipStreamSynchronize(ctx->s_panel);
+    for (gaplac_ctx* c : ctx->lanes) gaplac_ctx_destroy(c);
+    ctx->lanes.clear();
+    if (ctx->borrowed_inputs) {
+        ctx->dX = nullptr;
+        ctx->dv = nullptr;
+    }
     for (int q = 0; q < 2; ++q) {
         if (ctx->ev_P[q]) (void)hipEventDestroy(ctx->ev_P[q]);
         if (ctx->ev_R[q]) (void)hipEventDestroy(ctx->ev_R[q]);
@@ -709,12 +747,47 @@ int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D, 
     }
     HIPCK(ctx, hipSetDevice(ctx->device));
     if ((rc = upload(ctx, N, D, X, ldx, v))) return rc;
-    for (int m = 0; m < nmodels; ++m) {
-        EvalResult r;
-        packs[(size_t)m].noise = noise;
-        if ((rc = eval_device(ctx, N, D, packs[(size_t)m], &r))) return rc;
-        out_info[m] = finish(r, &out_logpdf[m], nullptr, nullptr);
+    HIPCK(ctx, hipStreamSynchronize(ctx->s_main));  // lanes read X / v on their own streams
+    // Models in flight on up to batch_lanes lanes (lane 0 = this context): an order-8192
+    // evaluation alone fills the chip only ~half the time (its panel chain is a
+    // latency-bound critical path), so concurrent models fill the gaps.
+    const int nl = std::max(1, std::min(ctx->batch_lanes, nmodels));
+    while ((int)ctx->lanes.size() < nl - 1) {
+        gaplac_ctx* c = nullptr;
+        if ((rc = gaplac_ctx_create(ctx->device, &c))) return set_err(ctx, rc, "batch lane creation failed");
+        c->borrowed_inputs = true;
+        ctx->lanes.push_back(c);
     }
+    std::vector<gaplac_ctx*> lane((size_t)nl, ctx);
+    for (int l = 1; l < nl; ++l) {
+        gaplac_ctx* c = ctx->lanes[(size_t)l - 1];
+        c->dX = ctx->dX;
+        c->dX_elems = ctx->dX_elems;
+        c->dv = ctx->dv;
+        c->dv_elems = ctx->dv_elems;
+        lane[(size_t)l] = c;
+    }
+    std::vector<int> pending((size_t)nl, -1);
+    auto drain = [&](int l) -> int {
+        const int m = pending[(size_t)l];
+        if (m < 0) return 0;
+        EvalResult r;
+        int e = eval_wait(lane[(size_t)l], &r);
+        if (e) return set_err(ctx, e, "batch lane %d: %s", l, lane[(size_t)l]->err.c_str());
+        out_info[m] = finish(r, &out_logpdf[m], nullptr, nullptr);
+        pending[(size_t)l] = -1;
+        return 0;
+    };
+    for (int m = 0; m < nmodels; ++m) {
+        const int l = m % nl;
+        if ((rc = drain(l))) return rc;
+        packs[(size_t)m].noise = noise;
+        if ((rc = eval_enqueue(lane[(size_t)l], N, D, packs[(size_t)m])))
+            return set_err(ctx, rc, "batch lane %d: %s", l, lane[(size_t)l]->err.c_str());
+        pending[(size_t)l] = m;
+    }
+    for (int l = 0; l < nl; ++l)
+        if ((rc = drain(l))) return rc;
     return 0;
 }
 

@@ -150,6 +150,32 @@ def test_batch_matches_individual(ctx):
     assert info[0] > 0 and np.isnan(out[0]) and info[1] == 0 and np.isfinite(out[1])
 
 
+def test_batch_lanes_bitwise_equal_to_single_evals(ctx):
+    """Models run concurrently on the batch lanes give exactly the single-eval results
+    (same kernels, same schedule per model), with a non-PD model in the middle."""
+    rng = np.random.default_rng(12)
+    N = 3000
+    X = np.column_stack([rng.uniform(-5, 5, N), rng.uniform(0, 10, N), rng.integers(0, 900, N).astype(float)])
+    v = rng.standard_normal(N)
+    models = [[(SQEXP, 0, l, 0)] for l in (0.5, 1.0, 2.0, 4.0)] + [
+        [(OU, 1, 1.0, 0), (CAT, 2, 0.0, 1)], [(CAT, 2, 0.0, 0)], [(LINEAR, 0, 0.5, 0), (SQEXP, 1, 2.0, 1)],
+        [(SQEXP, 1, 1.0, 0), (OU, 1, 3.0, 1), (CAT, 2, 0.0, 2)]]
+    out, info = ctx.logpdf_batch(X, models, 0.1, v)
+    for m, lp, inf in zip(models, out, info):
+        assert inf == 0
+        assert lp == ctx.logpdf(X, m, 0.1, v)
+    # noise 0 for the batch; every model but one carries its own Noise term
+    models2 = [m + [(NOISE, -1, 0.1, len(m))] for m in models[:6]]
+    models2.insert(3, [(CAT, 2, 0.0, 0)])
+    out, info = ctx.logpdf_batch(X, models2, 0.0, v)
+    with pytest.raises(PosDefException) as e:
+        ctx.logpdf(X, models2[3], 0.0, v)
+    assert info[3] == e.value.info and np.isnan(out[3])
+    for i, m in enumerate(models2):
+        if i != 3:
+            assert info[i] == 0 and out[i] == ctx.logpdf(X, m, 0.0, v)
+
+
 def test_abstractgps_frontend_and_select(ctx):
     import pandas as pd
     from tests.golden_io import GOLDEN
