@@ -27,6 +27,8 @@ EXPORTED = (
     "gaplac_logpdf",
     "gaplac_logpdf_device",
     "gaplac_logpdf_batch",
+    "gaplac_logpdf_grad",
+    "gaplac_logpdf_grad_device",
     "gaplac_gram",
     "gaplac_factor",
     "gaplac_set_profiling",
@@ -74,6 +76,10 @@ class Stats(ctypes.Structure):
         ("syrk_bytes", c_double),
         ("small_launches", c_int64),
         ("small_ms", c_double),
+        ("grad_rows_ms", c_double),
+        ("cinv_launches", c_int64),
+        ("cinv_ms", c_double),
+        ("contract_ms", c_double),
     ]
 
 
@@ -105,6 +111,8 @@ def load() -> ctypes.CDLL:
         c_void_p, c_int32, c_int64, c_int32, c_void_p, c_int64, POINTER(c_int32), POINTER(Term),
         c_double, c_void_p, _DP, POINTER(c_int64),
     ]
+    lib.gaplac_logpdf_grad.argtypes = common + [_DP, c_void_p, c_void_p, _DP]
+    lib.gaplac_logpdf_grad_device.argtypes = common + [_DP, c_void_p, c_void_p, _DP]
     lib.gaplac_gram.argtypes = [
         c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, POINTER(Term), c_double, c_void_p, c_int64,
     ]

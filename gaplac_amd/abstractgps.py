@@ -57,6 +57,17 @@ def logpdf(fx: FiniteGP, y, ctx: backend.Context | None = None, full: bool = Fal
     return ctx.logpdf(fx.x, fx.terms, fx.noise, y, full=full)
 
 
+def logpdf_and_gradient(fx: FiniteGP, y, ctx: backend.Context | None = None):
+    """(logpdf, dlogpdf/dy, dlogpdf/dparam per lowered term, dlogpdf/dnoise) on the GPU:
+    what ForwardDiff computes through AbstractGPs.logpdf in the reference's mcmc
+    (CLI/src/mcmc.jl:31-41), as one analytic evaluation (gaplac_logpdf_grad)."""
+    ctx = ctx or backend.default_context()
+    y = np.asarray(y, dtype=np.float64)
+    if y.shape[0] != len(fx):
+        raise F.ArgumentError("DimensionMismatch: length of y does not match the FiniteGP")
+    return ctx.logpdf_grad(fx.x, fx.terms, fx.noise, y)
+
+
 def make_gp(spec: F.Spec, hyperparams=None):
     """src/interface.jl:36-41 — (GP(kern), vars), checking #vars == #kernels."""
     kern, vars_ = K.kernel(F.formula(spec), hyperparams)

@@ -129,6 +129,43 @@ class Context:
         self._check(rc)
         return out, info
 
+    def logpdf_grad(self, X, terms, noise: float, v):
+        """(logpdf, dv, dparam, dnoise): logpdf and its gradient with respect to v, to each
+        term's parameter (l / c / variance; 0 for Cat) and to the observation variance
+        (gaplac_logpdf_grad)."""
+        Xc = _colmajor(X)
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        N, D = Xc.shape
+        if v.shape[0] != N:
+            raise ArgumentError(f"length of v ({v.shape[0]}) != N ({N})")
+        terms = list(terms)
+        ta = term_array(terms)
+        lp, dn = c_double(), c_double()
+        dv = np.empty(N, dtype=np.float64)
+        dp = np.empty(max(1, len(terms)), dtype=np.float64)
+        rc = self.lib.gaplac_logpdf_grad(
+            self.h, N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), len(terms), ta, float(noise),
+            v.ctypes.data_as(c_void_p), byref(lp), dv.ctypes.data_as(c_void_p), dp.ctypes.data_as(c_void_p),
+            byref(dn),
+        )
+        self._check(rc)
+        return lp.value, dv, dp[: len(terms)].copy(), dn.value
+
+    def logpdf_grad_device(self, N: int, D: int, dX_ptr: int, ldx: int, terms, noise: float, dv_ptr: int,
+                           want_dv: bool = True):
+        """Device-resident inputs; returns (logpdf, dv or None, dparam, dnoise)."""
+        terms = list(terms)
+        ta = term_array(terms)
+        lp, dn = c_double(), c_double()
+        dv = np.empty(N, dtype=np.float64) if want_dv else None
+        dp = np.empty(max(1, len(terms)), dtype=np.float64)
+        rc = self.lib.gaplac_logpdf_grad_device(
+            self.h, N, D, c_void_p(dX_ptr), ldx, len(terms), ta, float(noise), c_void_p(dv_ptr), byref(lp),
+            dv.ctypes.data_as(c_void_p) if want_dv else None, dp.ctypes.data_as(c_void_p), byref(dn),
+        )
+        self._check(rc)
+        return lp.value, dv, dp[: len(terms)].copy(), dn.value
+
     def gram(self, X, terms, noise: float = 0.0) -> np.ndarray:
         Xc = _colmajor(X)
         N, D = Xc.shape

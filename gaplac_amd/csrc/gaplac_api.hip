@@ -85,6 +85,22 @@ struct gaplac_ctx {
     std::vector<gaplac_ctx*> lanes;
     int batch_lanes = 2;           // GAPLAC_BATCH_LANES (measured at N=8192: 1 lane 138, 2 lanes 191, 3-6 lanes 161-187 evals/s)
     bool borrowed_inputs = false;  // dX / dv belong to the parent
+    // Gradient (gaplac_logpdf_grad): identity rows below the matrix (lda =
+    // 2 Np while grad_rows), alpha, partial sums, the XCD-balanced C^{-1} tile list.
+    bool grad_rows = false;
+    double* galpha = nullptr;
+    size_t galpha_elems = 0;
+    double* gdv = nullptr;
+    size_t gdv_elems = 0;
+    double* gpart = nullptr;
+    size_t gpart_elems = 0;
+    double* gout = nullptr;   // device: T+1 results
+    double* hgout = nullptr;  // pinned copy
+    GradTermPack* dgp = nullptr;
+    GradTermPack* hgp = nullptr;  // pinned staging
+    uint32_t* glist = nullptr;
+    size_t glist_elems = 0;
+    int glist_m = -1, glist_blocks = 0;
 };
 
 namespace {
@@ -255,6 +271,16 @@ int accumulate_slots(gaplac_ctx* ctx, const std::vector<gaplac_ctx::Slot>& slots
                 ctx->stats.small_ms += ms;
                 ctx->stats.small_launches += 1;
                 break;
+            case 7:
+                ctx->stats.grad_rows_ms += ms;
+                break;
+            case 8:
+                ctx->stats.cinv_ms += ms;
+                ctx->stats.cinv_launches += 1;
+                break;
+            case 9:
+                ctx->stats.contract_ms += ms;
+                break;
             case 1:
                 ctx->stats.gram_ms += ms;
                 ctx->stats.gram_bytes += slots[i].work;
@@ -311,6 +337,33 @@ void factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, 
     }
 }
 
+// Gradient rows: the identity rows E (tile rows nt .. 2nt-1 of the column
+// storage, lda = 2 Np) are factored along on s_main, off the critical path: once SP p's
+// columns are final (P(p)), its identity-row tiles get the column-by-column substitution
+// (rows E <= c of column c; the earlier columns of the SP are applied first, K = 128),
+// then SP p is applied to every later column (rows E < end of SP p, K = 128 W). Tiles
+// below the identity rows' diagonal (E > J) stay exactly zero and are never touched.
+void identity_rows_step(gaplac_ctx* ctx, hipStream_t sm, int64_t lda, int nt, int p) {
+    const int W = ctx->spw;
+    const int c0 = W * p, c1 = std::min(W * p + W, nt);
+    for (int c = c0; c < c1; ++c) {
+        double* Acol = ctx->A + (int64_t)c * NB * lda;
+        if (c > c0) {
+            BulkArgs ba{ctx->A, lda, Panel{Acol - NB * lda, lda, 0}, nullptr, c * (c1 - c), NB, nt, c,
+                        ColMap{1, 0, W}};
+            ba.rect_rows = c;
+            launch_bulk(sm, ba, slot(ctx, 7, 0));
+        }
+        launch_trsm_rows(sm, Acol, lda, c, nt, c + 1, ctx->Dinv + (size_t)c * DINV_PER_BLOCK, slot(ctx, 7, 0));
+    }
+    if (c1 < nt) {
+        BulkArgs ba{ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nullptr, c1 * (nt - c1),
+                    (c1 - c0) * NB, nt, c1, ColMap{1, 0, W}};
+        ba.rect_rows = c1;
+        launch_bulk(sm, ba, slot(ctx, 7, 0));
+    }
+}
+
 int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     hipStream_t sm = ctx->s_main;
     hipStream_t sp = ctx->serial ? sm : ctx->s_panel;
@@ -360,6 +413,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             }
         }
         HIPCK(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
+        if (ctx->grad_rows) identity_rows_step(ctx, sm, lda, nt, p);
     }
     launch_reduce(sm, ctx->A, lda, N, (int64_t)nt * NB, ColMap{1, 0, 1}, ctx->dres);
     HIPCK(ctx, hipGetLastError());
@@ -387,20 +441,35 @@ int ensure_tile_lists(gaplac_ctx* ctx, int nt) {
 // reduction, result copy to the pinned host record. Inputs: ctx->dX (ld N), ctx->dv,
 // ctx->dtp.
 int enqueue_eval(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt) {
+    const int64_t lda = ctx->grad_rows ? 2 * Np : Np;
     launch_init_result(ctx->s_main, ctx->dres);
     if (ctx->recording) launch_kt_reset(ctx->s_main, ctx->dkt, (int)ctx->kt_cap);
     // Gram in two launches: the first super-panel's tile columns, then the rest (the panel
     // chain starts on the first part while the second is still being written).
     const double bytes = 8.0 * (double)Np * (double)(Np + 1) / 2.0 + 8.0 * (double)N * (D + 1);
     const double frac = nt > 0 ? 1.0 - (double)(nt - ctx->spw) * (nt - ctx->spw + 1) / ((double)nt * (nt + 1)) : 1.0;
-    launch_gram(ctx->s_main, ctx->A, Np, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 1, ctx->spw,
+    launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 1, ctx->spw,
                 slot(ctx, 1, bytes * frac));
     HIPCK(ctx, hipEventRecord(ctx->ev_gram, ctx->s_main));
-    launch_gram(ctx->s_main, ctx->A, Np, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 2, ctx->spw,
+    launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 2, ctx->spw,
                 slot(ctx, 1, bytes * (1.0 - frac)));
     HIPCK(ctx, hipEventRecord(ctx->ev_gram2, ctx->s_main));
+    if (ctx->grad_rows) launch_init_identity_rows(ctx->s_main, ctx->A, lda, Np, nt, ctx->spw);
     int rc;
-    if ((rc = factor_and_reduce(ctx, N, Np, nt))) return rc;
+    if ((rc = factor_and_reduce(ctx, N, lda, nt))) return rc;
+    if (ctx->grad_rows) {
+        // alpha = Y z, then M = -C^{-1} over the factor storage, contraction, reduction
+        hipStream_t sm = ctx->s_main;
+        launch_zero_tail_cols(sm, ctx->A, lda, Np, N);
+        launch_alpha(sm, ctx->A, lda, Np, N, ctx->gpart, ctx->galpha, ctx->gdv);
+        launch_cinv_tiles(sm, ctx->A, lda, Np, ctx->glist, ctx->glist_blocks, slot(ctx, 8, 0));
+        launch_grad_contract(sm, ctx->A, lda, N, ctx->dX, N, ctx->galpha, ctx->dtp, ctx->dgp, ctx->gpart,
+                             slot(ctx, 9, 0));
+        const int m = (int)((N + NB - 1) / NB);
+        launch_grad_reduce(sm, ctx->gpart, m * (m + 1) / 2, ctx->htp->T, ctx->gout);
+        HIPCK(ctx, hipMemcpyAsync(ctx->hgout, ctx->gout, sizeof(double) * (GAPLAC_MAX_TERMS + 1),
+                                  hipMemcpyDeviceToHost, sm));
+    }
     HIPCK(ctx, hipMemcpyAsync(ctx->hres, ctx->dres, sizeof(EvalResult), hipMemcpyDeviceToHost,
                               ctx->s_main));
     return 0;
@@ -423,7 +492,23 @@ int ensure_workspace(gaplac_ctx* ctx, int64_t N) {
     const int nt = (int)(Np / NB);
     int rc;
     HIPCK(ctx, hipSetDevice(ctx->device));
-    if ((rc = ensure(ctx, &ctx->A, &ctx->A_elems, (size_t)Np * Np))) return rc;
+    if ((rc = ensure(ctx, &ctx->A, &ctx->A_elems, (size_t)(ctx->grad_rows ? 2 : 1) * Np * Np))) return rc;
+    if (ctx->grad_rows) {
+        const int m = (int)((N + NB - 1) / NB);
+        const size_t nk = (size_t)((N + 511) / 512);
+        const size_t part = std::max(nk * (size_t)N, (size_t)m * (m + 1) / 2 * (GAPLAC_MAX_TERMS + 1));
+        if ((rc = ensure(ctx, &ctx->galpha, &ctx->galpha_elems, (size_t)N))) return rc;
+        if ((rc = ensure(ctx, &ctx->gdv, &ctx->gdv_elems, (size_t)N))) return rc;
+        if ((rc = ensure(ctx, &ctx->gpart, &ctx->gpart_elems, part))) return rc;
+        if (ctx->glist_m != m) {
+            std::vector<uint32_t> host;
+            build_grad_list(m, host);
+            if ((rc = ensure(ctx, &ctx->glist, &ctx->glist_elems, host.size()))) return rc;
+            HIPCK(ctx, hipMemcpy(ctx->glist, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+            ctx->glist_m = m;
+            ctx->glist_blocks = (int)host.size();
+        }
+    }
     if ((rc = ensure(ctx, &ctx->Dinv, &ctx->Dinv_elems, (size_t)nt * DINV_PER_BLOCK))) return rc;
     return ensure_tile_lists(ctx, nt);
 }
@@ -455,7 +540,7 @@ int eval_device(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp, EvalR
     if ((rc = ensure_workspace(ctx, N))) return rc;
     const bool prof = ctx->profiling;
     if (prof) {
-        const size_t need = (size_t)nt * 6 + 16;  // launches per evaluation, with margin
+        const size_t need = (size_t)nt * 9 + 32;  // launches per evaluation, with margin
         if (ctx->kt_cap < need) {
             if ((rc = ensure(ctx, &ctx->dkt, &ctx->kt_cap, need))) return rc;
             if (ctx->hkt) (void)hipHostFree(ctx->hkt);
@@ -465,7 +550,7 @@ int eval_device(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp, EvalR
     }
     *ctx->htp = tp;
     HIPCK(ctx, hipMemcpyAsync(ctx->dtp, ctx->htp, sizeof(TermPack), hipMemcpyHostToDevice, ctx->s_main));
-    if (ctx->use_graph && !ctx->serial && ctx->prof_mode != 2) {
+    if (ctx->use_graph && !ctx->serial && ctx->prof_mode != 2 && !ctx->grad_rows) {
         hipGraph_t& G = prof ? ctx->pgraph : ctx->graph;
         hipGraphExec_t& GX = prof ? ctx->pgexec : ctx->gexec;
         int64_t& GN = prof ? ctx->pgN : ctx->gN;
@@ -559,6 +644,54 @@ void nan_out(double* a, double* b, double* c) {
     if (c) *c = NAN;
 }
 
+// Shared body of gaplac_logpdf_grad / _device.
+int logpdf_grad_impl(gaplac_ctx* ctx, bool on_device, int64_t N, int32_t D, const double* X, int64_t ldx,
+                     int32_t T, const gaplac_term* terms, double noise, const double* v, double* out_logpdf,
+                     double* out_dv, double* out_dparam, double* out_dnoise) {
+    if (out_logpdf) *out_logpdf = NAN;
+    if (out_dnoise) *out_dnoise = NAN;
+    if (out_dparam && T > 0)
+        for (int t = 0; t < T && t < GAPLAC_MAX_TERMS; ++t) out_dparam[t] = NAN;
+    if (out_dv)
+        for (int64_t i = 0; i < N; ++i) out_dv[i] = NAN;
+    int rc = check_common(ctx, N, D, X, ldx, noise, v);
+    if (rc) return rc;
+    TermPack tp;
+    if ((rc = pack_terms(ctx, D, T, terms, &tp))) return rc;
+    if (N == 0) {
+        if (out_logpdf) *out_logpdf = -0.0;
+        if (out_dnoise) *out_dnoise = 0.0;
+        if (out_dparam)
+            for (int t = 0; t < T; ++t) out_dparam[t] = 0.0;
+        return 0;
+    }
+    GradTermPack gp{};
+    for (int t = 0; t < T; ++t) {
+        int a = t, b = t + 1;
+        while (a > 0 && terms[a - 1].group == terms[t].group) --a;
+        while (b < T && terms[b].group == terms[t].group) ++b;
+        gp.gstart[t] = a;
+        gp.gend[t] = b;
+    }
+    HIPCK(ctx, hipSetDevice(ctx->device));
+    if ((rc = on_device ? upload_device(ctx, N, D, X, ldx, v) : upload(ctx, N, D, X, ldx, v))) return rc;
+    tp.noise = noise;
+    *ctx->hgp = gp;
+    HIPCK(ctx, hipMemcpyAsync(ctx->dgp, ctx->hgp, sizeof(GradTermPack), hipMemcpyHostToDevice, ctx->s_main));
+    ctx->grad_rows = true;
+    EvalResult r;
+    rc = eval_device(ctx, N, D, tp, &r);
+    ctx->grad_rows = false;
+    if (rc) return rc;
+    rc = finish(r, out_logpdf, nullptr, nullptr);
+    if (rc) return rc;  // PosDefException: gradients stay NaN
+    if (out_dv) HIPCK(ctx, hipMemcpy(out_dv, ctx->gdv, (size_t)N * sizeof(double), hipMemcpyDeviceToHost));
+    if (out_dparam)
+        for (int t = 0; t < T; ++t) out_dparam[t] = ctx->hgout[t];
+    if (out_dnoise) *out_dnoise = ctx->hgout[T];
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -634,6 +767,15 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
         return fail("hipMalloc", e);
     if ((e = hipHostMalloc(reinterpret_cast<void**>(&ctx->htp), sizeof(TermPack), 0)) != hipSuccess)
         return fail("hipHostMalloc", e);
+    if ((e = hipMalloc(reinterpret_cast<void**>(&ctx->gout), sizeof(double) * (GAPLAC_MAX_TERMS + 1))) != hipSuccess)
+        return fail("hipMalloc", e);
+    if ((e = hipHostMalloc(reinterpret_cast<void**>(&ctx->hgout), sizeof(double) * (GAPLAC_MAX_TERMS + 1), 0)) !=
+        hipSuccess)
+        return fail("hipHostMalloc", e);
+    if ((e = hipMalloc(reinterpret_cast<void**>(&ctx->dgp), sizeof(GradTermPack))) != hipSuccess)
+        return fail("hipMalloc", e);
+    if ((e = hipHostMalloc(reinterpret_cast<void**>(&ctx->hgp), sizeof(GradTermPack), 0)) != hipSuccess)
+        return fail("hipHostMalloc", e);
     if (const char* s = std::getenv("GAPLAC_GRAPH")) ctx->use_graph = s[0] == '1';
     if (const char* s = std::getenv("GAPLAC_GRAPH_PRIO")) ctx->graph_prio = s[0] != '0';
     *out = ctx;
@@ -669,6 +811,14 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
     if (ctx->dkt) (void)hipFree(ctx->dkt);
     if (ctx->hkt) (void)hipHostFree(ctx->hkt);
+    if (ctx->galpha) (void)hipFree(ctx->galpha);
+    if (ctx->gdv) (void)hipFree(ctx->gdv);
+    if (ctx->gpart) (void)hipFree(ctx->gpart);
+    if (ctx->gout) (void)hipFree(ctx->gout);
+    if (ctx->hgout) (void)hipHostFree(ctx->hgout);
+    if (ctx->dgp) (void)hipFree(ctx->dgp);
+    if (ctx->hgp) (void)hipHostFree(ctx->hgp);
+    if (ctx->glist) (void)hipFree(ctx->glist);
     if (ctx->dres) (void)hipFree(ctx->dres);
     if (ctx->dtp) (void)hipFree(ctx->dtp);
     if (ctx->htp) (void)hipHostFree(ctx->htp);
@@ -840,6 +990,20 @@ int gaplac_factor(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_
     for (int64_t j = 0; j < N; ++j)
         for (int64_t i = 0; i < j; ++i) out_L[j * ldl + i] = 0.0;
     return finish(r, nullptr, nullptr, nullptr);
+}
+
+int gaplac_logpdf_grad(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx, int32_t T,
+                       const gaplac_term* terms, double noise, const double* v, double* out_logpdf,
+                       double* out_dv, double* out_dparam, double* out_dnoise) {
+    return logpdf_grad_impl(ctx, false, N, D, X, ldx, T, terms, noise, v, out_logpdf, out_dv, out_dparam,
+                            out_dnoise);
+}
+
+int gaplac_logpdf_grad_device(gaplac_ctx* ctx, int64_t N, int32_t D, const double* dX, int64_t ldx, int32_t T,
+                              const gaplac_term* terms, double noise, const double* dv, double* out_logpdf,
+                              double* out_dv, double* out_dparam, double* out_dnoise) {
+    return logpdf_grad_impl(ctx, true, N, D, dX, ldx, T, terms, noise, dv, out_logpdf, out_dv, out_dparam,
+                            out_dnoise);
 }
 
 int gaplac_set_profiling(gaplac_ctx* ctx, int mode) {

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
+#include <vector>
 #include "../../include/gaplac.h"
 
 namespace gaplac {
@@ -67,9 +68,10 @@ struct BulkArgs {
     double* C;
     int64_t ldc;
     Panel pn;
-    const uint32_t* tiles;
+    const uint32_t* tiles;  // nullptr: rectangular block of rect_rows tile rows (tile_decode)
     int ntiles, kdepth, bi0, lj0;
     ColMap cm;
+    int rect_rows = 0;
 };
 
 // Term validation + kernel-argument pack (gaplac_api.hip); on error returns GAPLAC_E_*
@@ -95,6 +97,10 @@ void launch_potrf_diag(hipStream_t s, double* Ablk, int64_t lda, int64_t N, int6
 // TRSM of the panel rows below diagonal block k: Acol is the storage of global column
 // k*NB; rows bi*NB.. for bi = k+1..nt-1 become A[bi,k] L_kk^{-T}.
 void launch_trsm(hipStream_t s, double* Acol, int64_t lda, int nt, int k, const double* Dinv, KTime* kt);
+// Same substitution for an arbitrary run of row tiles bi0 .. bi0+nrows-1 of column k
+// (the gradient's identity rows below the matrix).
+void launch_trsm_rows(hipStream_t s, double* Acol, int64_t lda, int k, int bi0, int nrows, const double* Dinv,
+                      KTime* kt);
 // Bulk trailing update (tile kernel, or quadrant kernel for small tile counts).
 void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt);
 // True when launch_bulk over ntiles tiles runs the small (quadrant) kernel.
@@ -109,5 +115,39 @@ void launch_reduce(hipStream_t s, const double* C, int64_t ldc, int64_t N, int64
                    EvalResult* res);
 void launch_kt_reset(hipStream_t s, KTime* kt, int n);
 void launch_init_result(hipStream_t s, EvalResult* res);
+
+// ---- gradient of logpdf ----
+// Rows Np .. 2Np-1 of the column storage (lda = 2 Np) hold the identity rows E = [I 0]
+// whose factorisation leaves Y = L^{-T} (upper triangular). Y tile (E, J) is stored at
+// A + J*NB*lda + Np + E*NB.
+// Reset the identity rows: tiles E <= J get identity / zero, tiles below the diagonal
+// within a super-panel of W tile columns get zero (read as panel rows by its update).
+void launch_init_identity_rows(hipStream_t s, double* A, int64_t lda, int64_t Np, int nt, int W);
+// Zero Y[:, N .. Np) (the columns of the padding / v row).
+void launch_zero_tail_cols(hipStream_t s, double* A, int64_t lda, int64_t Np, int64_t N);
+// alpha = Y z (= C^{-1} v), z = row N of the factor: partial sums per 512-column chunk,
+// then a fixed-order sum; also writes dv = -alpha.
+void launch_alpha(hipStream_t s, const double* A, int64_t lda, int64_t Np, int64_t N, double* partial,
+                  double* alpha, double* dv);
+// Product-group bounds per term (the gradient of a term inside a product group carries
+// the group's other terms).
+struct GradTermPack {
+    int32_t gstart[GAPLAC_MAX_TERMS];  // first term of t's product group
+    int32_t gend[GAPLAC_MAX_TERMS];    // one past its last term
+};
+// M = -C^{-1} = -Y Y^T over the lower tiles I >= J (I, J < m) into the factor storage
+// (rows / columns < Np of A): tile (I, J) = -sum_{k >= I NB} Y_Ik Y_Jk^T. list[b] = I | J << 16
+// for workgroup b, 0xffffffff = idle (build_grad_list).
+void launch_cinv_tiles(hipStream_t s, double* A, int64_t lda, int64_t Np, const uint32_t* list, int nblocks,
+                       KTime* kt);
+// Per lower tile of M: its share of sum_ij (alpha_i alpha_j - Cinv_ij) dC_ij/dtheta for every
+// term parameter (t < T) and the observation variance (t = T): partial[tile * (T+1) + t].
+void launch_grad_contract(hipStream_t s, const double* A, int64_t lda, int64_t N, const double* X, int64_t ldx,
+                          const double* alpha, const TermPack* dtp, const GradTermPack* dgp, double* partial,
+                          KTime* kt);
+// dparam[t] = 0.5 * sum over tiles (fixed order), t = 0..T (T = observation variance).
+void launch_grad_reduce(hipStream_t s, const double* partial, int ntiles, int T, double* out);
+// Workgroup -> tile list for launch_grad_tiles over the m x m triangle (XCD-balanced).
+void build_grad_list(int m, std::vector<uint32_t>& out);
 
 }  // namespace gaplac

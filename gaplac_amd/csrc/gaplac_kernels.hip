@@ -18,6 +18,8 @@
 #include "gaplac_internal.h"
 #include <math.h>
 
+#include <algorithm>
+
 namespace gaplac {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -75,6 +77,9 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
                                           const double* __restrict__ v,
                                           const TermPack* __restrict__ tpp, int bi, int bj) {
     // Ccol: storage of global column bj*NB (row 0); rows are global
+    // No FMA contraction: KernelFunctions scales each coordinate (rounded) and then
+    // differences, so equal coordinates give exactly 0 (p*xa - p*xj fused would not).
+#pragma clang fp contract(off)
     const TermPack& tp = *tpp;  // uniform: scalar loads (device copy refreshed per eval)
     const double noise = tp.noise;
     const int64_t r0 = (int64_t)bi * NB, c0 = (int64_t)bj * NB;
@@ -455,12 +460,12 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ Ag
 constexpr int TRSM_LBLK = NDB * (NDB - 1) / 2;  // 28
 
 // Acol: storage of the panel's first column (global column k*NB), rows global.
-__device__ __forceinline__ void trsm_subst_kernel_body(double* __restrict__ Acol, int64_t lda, int k,
+__device__ __forceinline__ void trsm_subst_kernel_body(double* __restrict__ Acol, int64_t lda, int k, int bi0,
                                                          const double* __restrict__ Dinv) {
     __shared__ double Ls[(TRSM_LBLK + NDB) * 256];
     __builtin_amdgcn_s_setprio(2);  // critical path
     const int tid = threadIdx.x;
-    const int bi = k + 1 + (int)(blockIdx.x >> 1);
+    const int bi = bi0 + (int)(blockIdx.x >> 1);
     const int wave = tid >> 6, lane = tid & 63;
     const int fr = lane >> 4, fc = lane & 15;
     const int64_t k0 = (int64_t)k * NB;
@@ -520,10 +525,10 @@ __device__ __forceinline__ void trsm_subst_kernel_body(double* __restrict__ Acol
 }
 
 __global__ __launch_bounds__(256) void trsm_subst_kernel(double* __restrict__ Acol, int64_t lda, int k,
-                                                         const double* __restrict__ Dinv,
+                                                         int bi0, const double* __restrict__ Dinv,
                                                          KTime* __restrict__ kt) {
     kt_begin(kt);
-    trsm_subst_kernel_body(Acol, lda, k, Dinv);
+    trsm_subst_kernel_body(Acol, lda, k, bi0, Dinv);
     kt_end(kt);
 }
 
@@ -548,14 +553,108 @@ constexpr int KB = 16;
 constexpr int LR = NB + 16;  // LDS k-row stride: lanes 16..31 land on banks 32..63
 
 __device__ __forceinline__ void tile_decode(const BulkArgs& a, int idx, int& bi, int& bj, int& lj) {
-    const uint32_t tv = a.tiles[idx];
-    bi = a.bi0 + (int)(tv & 0xffffu);
-    lj = a.lj0 + (int)(tv >> 16);
+    int r, c;
+    if (a.rect_rows > 0) {
+        // rectangular block (rect_rows x ntiles/rect_rows), generated on the fly: strips of
+        // 8 tile rows, columns outer within a strip (an XCD's contiguous run of the list
+        // shares its 8 panel row blocks and walks the columns)
+        const int mr = a.rect_rows, mc = a.ntiles / mr;
+        const int full = (mr >> 3) * 8 * mc;
+        if (idx < full) {
+            const int strip = idx / (8 * mc), w = idx - strip * 8 * mc;
+            c = w >> 3;
+            r = strip * 8 + (w & 7);
+        } else {
+            const int rem = mr & 7, w = idx - full;
+            c = w / rem;
+            r = (mr & ~7) + (w - c * rem);
+        }
+    } else {
+        const uint32_t tv = a.tiles[idx];
+        r = (int)(tv & 0xffffu);
+        c = (int)(tv >> 16);
+    }
+    bi = a.bi0 + r;
+    lj = a.lj0 + c;
     bj = a.cm.global(lj);
 }
 
-__device__ __forceinline__ void tile_syrk_body(const BulkArgs& a) {
+// Shared k-loop of the 128x128 tile kernels: acc[mi][mj] (wave (wi, wj) of the 2x2 wave
+// grid) += -P_i Q_j^T over kdepth panel columns, where P (rows of tile i) and Q (rows of
+// tile j) are column-major with leading dimension ldp. Lane element (mi, mj, rg) is tile
+// entry (row 64 wi + 16 mi + (lane & 15), column 64 wj + 16 mj + (lane >> 4) + 4 rg).
+// Inactive waves (upper quadrant of a diagonal tile) only help with the staging.
+__device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const double* __restrict__ Q,
+                                             int64_t ldp, int kdepth, bool active, d4 (&acc)[4][4]) {
     __shared__ double sm[2][2][KB][LR];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wi = w & 1, wj = w >> 1;
+    const int fr = lane >> 4, fc = lane & 15;
+    // staging: thread -> (k row krow + 4 it, rows 2 lane, 2 lane + 1) of both operands
+    const int krow = tid >> 6;  // 0..3
+    const double* Pr = P + (int64_t)krow * ldp + 2 * lane;
+    const double* Qr = Q + (int64_t)krow * ldp + 2 * lane;
+    const int64_t s4 = 4 * ldp;
+    double2 p0, p1, p2, p3, q0, q1, q2, q3;
+#define GAPLAC_GLOAD(ch)                                                               \
+    do {                                                                               \
+        const int64_t o_ = (int64_t)(ch) * KB * ldp;                                   \
+        p0 = *reinterpret_cast<const double2*>(Pr + o_);                               \
+        p1 = *reinterpret_cast<const double2*>(Pr + o_ + s4);                          \
+        p2 = *reinterpret_cast<const double2*>(Pr + o_ + 2 * s4);                      \
+        p3 = *reinterpret_cast<const double2*>(Pr + o_ + 3 * s4);                      \
+        q0 = *reinterpret_cast<const double2*>(Qr + o_);                               \
+        q1 = *reinterpret_cast<const double2*>(Qr + o_ + s4);                          \
+        q2 = *reinterpret_cast<const double2*>(Qr + o_ + 2 * s4);                      \
+        q3 = *reinterpret_cast<const double2*>(Qr + o_ + 3 * s4);                      \
+    } while (0)
+#define GAPLAC_LSTORE(buf)                                                             \
+    do {                                                                               \
+        double* sp_ = &sm[buf][0][krow][2 * lane];                                     \
+        double* sq_ = &sm[buf][1][krow][2 * lane];                                     \
+        *reinterpret_cast<double2*>(sp_) = make_double2(-p0.x, -p0.y);                 \
+        *reinterpret_cast<double2*>(sp_ + 4 * LR) = make_double2(-p1.x, -p1.y);        \
+        *reinterpret_cast<double2*>(sp_ + 8 * LR) = make_double2(-p2.x, -p2.y);        \
+        *reinterpret_cast<double2*>(sp_ + 12 * LR) = make_double2(-p3.x, -p3.y);       \
+        *reinterpret_cast<double2*>(sq_) = q0;                                         \
+        *reinterpret_cast<double2*>(sq_ + 4 * LR) = q1;                                \
+        *reinterpret_cast<double2*>(sq_ + 8 * LR) = q2;                                \
+        *reinterpret_cast<double2*>(sq_ + 12 * LR) = q3;                               \
+    } while (0)
+
+    GAPLAC_GLOAD(0);
+    GAPLAC_LSTORE(0);
+    __syncthreads();
+    const int NCH = kdepth / KB;
+    for (int ch = 0; ch < NCH; ++ch) {
+        const int buf = ch & 1;
+        const bool more = ch + 1 < NCH;
+        if (more) GAPLAC_GLOAD(ch + 1);
+        if (active) {
+#pragma unroll
+            for (int ks = 0; ks < KB; ks += 4) {
+                double fa[4], fb[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    fa[m] = sm[buf][1][ks + fr][64 * wj + 16 * m + fc];
+                    fb[m] = sm[buf][0][ks + fr][64 * wi + 16 * m + fc];
+                }
+#pragma unroll
+                for (int mj = 0; mj < 4; ++mj)
+#pragma unroll
+                    for (int mi = 0; mi < 4; ++mi)
+                        acc[mi][mj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mj], fb[mi],
+                                                                            acc[mi][mj], 0, 0, 0);
+            }
+        }
+        if (more) GAPLAC_LSTORE(buf ^ 1);
+        __syncthreads();
+    }
+#undef GAPLAC_GLOAD
+#undef GAPLAC_LSTORE
+}
+
+__device__ __forceinline__ void tile_syrk_body(const BulkArgs& a) {
     const int b = (int)blockIdx.x;
     const int chunk = (a.ntiles + 7) >> 3;
     const int idx = (b & 7) * chunk + (b >> 3);
@@ -563,7 +662,7 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a) {
     int bi, bj, lj;
     tile_decode(a, idx, bi, bj, lj);
     const int64_t r0 = (int64_t)bi * NB;
-    const int64_t ldc = a.ldc, ldp = a.pn.ld;
+    const int64_t ldc = a.ldc;
     double* __restrict__ Ct = a.C + (int64_t)lj * NB * ldc + r0;
     const double* __restrict__ P = a.pn.P + (r0 - a.pn.row0);
     const double* __restrict__ Q = a.pn.P + ((int64_t)bj * NB - a.pn.row0);
@@ -584,56 +683,7 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a) {
                     acc[mi][mj][rg] = Ci[(int64_t)(64 * wj + 16 * mj + fr + 4 * rg) * ldc];
         }
     }
-
-    double2 pp[4], pq[4];
-    const int krow = tid >> 6;  // 0..3
-    auto gload = [&](int ch) {
-#pragma unroll
-        for (int it = 0; it < 4; ++it) {
-            const int64_t col = (int64_t)ch * KB + krow + 4 * it;
-            pp[it] = *reinterpret_cast<const double2*>(P + col * ldp + 2 * lane);
-            pq[it] = *reinterpret_cast<const double2*>(Q + col * ldp + 2 * lane);
-        }
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-        for (int it = 0; it < 4; ++it) {
-            const int kk = krow + 4 * it;
-            double2 v = pp[it];
-            v.x = -v.x;
-            v.y = -v.y;
-            *reinterpret_cast<double2*>(&sm[buf][0][kk][2 * lane]) = v;
-            *reinterpret_cast<double2*>(&sm[buf][1][kk][2 * lane]) = pq[it];
-        }
-    };
-
-    gload(0);
-    lstore(0);
-    __syncthreads();
-    const int NCH = a.kdepth / KB;
-    for (int ch = 0; ch < NCH; ++ch) {
-        const int buf = ch & 1;
-        if (ch + 1 < NCH) gload(ch + 1);
-        if (active) {
-#pragma unroll
-            for (int ks = 0; ks < KB; ks += 4) {
-                double fa[4], fb[4];
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    fa[m] = sm[buf][1][ks + fr][64 * wj + 16 * m + fc];
-                    fb[m] = sm[buf][0][ks + fr][64 * wi + 16 * m + fc];
-                }
-#pragma unroll
-                for (int mj = 0; mj < 4; ++mj)
-#pragma unroll
-                    for (int mi = 0; mi < 4; ++mi)
-                        acc[mi][mj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mj], fb[mi],
-                                                                            acc[mi][mj], 0, 0, 0);
-            }
-        }
-        if (ch + 1 < NCH) lstore(buf ^ 1);
-        __syncthreads();
-    }
+    tile_mma_neg(P, Q, a.pn.ld, a.kdepth, active, acc);
     if (!active) return;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
@@ -830,6 +880,273 @@ __global__ void init_result_kernel(EvalResult* res) {
     res->info = ~0ull;
 }
 
+// ---------------------------------------------------------------------------------
+// Gradient of logpdf: the factorisation also runs
+// over identity rows E = [I 0] stored below the matrix (rows Np .. 2Np-1, lda = 2 Np),
+// which leaves Y = E L^{-T} = L^{-T} there (upper triangular). Then
+//   alpha = C^{-1} v = Y z                                        (alpha_*_kernel)
+//   C^{-1} = Y Y^T,   tile (I, J), I >= J: sum_{k >= I NB} Y_Ik Y_Jk^T  (grad_tile_kernel)
+//   dlogp/dtheta = 1/2 sum_ij (alpha_i alpha_j - Cinv_ij) dC_ij/dtheta
+// with dC/dtheta evaluated on the fly from X (never stored), for every term parameter at
+// once, and tile partial sums reduced in a fixed order (deterministic).
+// ---------------------------------------------------------------------------------
+
+// Identity rows: tiles (E, J) with E <= J get I on E == J and 0 elsewhere; tiles below the
+// diagonal inside a super-panel's columns (J < E, same super-panel of W tile columns) are
+// zeroed too: the super-panel's bulk update reads them as panel rows. The other tiles below
+// the diagonal are never read.
+__global__ __launch_bounds__(256) void init_identity_rows_kernel(double* __restrict__ A, int64_t lda,
+                                                                 int64_t Np, int W) {
+    const int J = (int)blockIdx.x, E = (int)blockIdx.y;
+    if (E > J && E / W != J / W) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    double* base = A + (int64_t)J * NB * lda + Np + (int64_t)E * NB + 2 * lane;
+    for (int c = w; c < NB; c += 4) {
+        double2 o = make_double2(0.0, 0.0);
+        if (E == J) {
+            o.x = (2 * lane == c) ? 1.0 : 0.0;
+            o.y = (2 * lane + 1 == c) ? 1.0 : 0.0;
+        }
+        *reinterpret_cast<double2*>(base + (int64_t)c * lda) = o;
+    }
+}
+
+// Y[:, N .. Np) = 0 (columns of the v row and of the padding).
+__global__ __launch_bounds__(256) void zero_tail_cols_kernel(double* __restrict__ A, int64_t lda, int64_t Np,
+                                                             int64_t N) {
+    const int64_t col = N + blockIdx.y;
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (col < Np && r < Np) A[col * lda + Np + r] = 0.0;
+}
+
+// alpha partial sums: block (x, y) = rows 256x .. 256x+255, columns 512y .. 512y+511.
+__global__ __launch_bounds__(256) void alpha_partial_kernel(const double* __restrict__ A, int64_t lda,
+                                                            int64_t Np, int64_t N, double* __restrict__ partial) {
+    __shared__ double zs[512];
+    const int tid = threadIdx.x;
+    const int64_t k0 = (int64_t)blockIdx.y * 512;
+    const int64_t i = (int64_t)blockIdx.x * 256 + tid;
+    for (int t = tid; t < 512; t += 256) zs[t] = (k0 + t < N) ? A[(k0 + t) * lda + N] : 0.0;
+    __syncthreads();
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    // Y is upper triangular: only columns k >= i are read (the tiles below the identity
+    // rows' diagonal are never written and hold stale data)
+    if (i < N && k0 + 512 > i) {
+        const double* y = A + k0 * lda + Np + i;
+        const int kn = (int)((N - k0) < 512 ? (N - k0) : 512);
+        int kk = i > k0 ? (int)(i - k0) : 0;
+        for (; kk + 4 <= kn; kk += 4) {
+            s0 += y[(int64_t)kk * lda] * zs[kk];
+            s1 += y[(int64_t)(kk + 1) * lda] * zs[kk + 1];
+            s2 += y[(int64_t)(kk + 2) * lda] * zs[kk + 2];
+            s3 += y[(int64_t)(kk + 3) * lda] * zs[kk + 3];
+        }
+        for (; kk < kn; ++kk) s0 += y[(int64_t)kk * lda] * zs[kk];
+    }
+    if (i < N) partial[(int64_t)blockIdx.y * N + i] = (s0 + s1) + (s2 + s3);
+}
+
+__global__ __launch_bounds__(256) void alpha_reduce_kernel(const double* __restrict__ partial, int64_t N, int nk,
+                                                           double* __restrict__ alpha, double* __restrict__ dv) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    double a = 0.0;
+    for (int y = 0; y < nk; ++y) a += partial[(int64_t)y * N + i];
+    alpha[i] = a;
+    dv[i] = -a;
+}
+
+// K_t(i, j) and dK_t/dparam_t(i, j) with the Gram kernel's arithmetic (p = 1/l for
+// SqExp / OU: the coordinate is scaled first, then differenced).
+__device__ __forceinline__ double term_k(int kind, double p, double xi, double xj, bool diag) {
+#pragma clang fp contract(off)
+    switch (kind) {
+        case GAPLAC_SQEXP: {
+            const double u = p * xi - p * xj;
+            return exp(-(u * u) * 0.5);
+        }
+        case GAPLAC_OU:
+            return exp(-fabs(p * xi - p * xj));
+        case GAPLAC_LINEAR:
+            return xi * xj + p;
+        case GAPLAC_CAT:
+            return (xi == xj) ? 1.0 : 0.0;
+        default:
+            return diag ? p : 0.0;
+    }
+}
+__device__ __forceinline__ double term_dk(int kind, double p, double xi, double xj, bool diag) {
+#pragma clang fp contract(off)
+    switch (kind) {
+        case GAPLAC_SQEXP: {  // d/dl exp(-u^2/2), u = (x_i - x_j)/l:  k u^2 / l
+            const double u = p * xi - p * xj;
+            const double u2 = u * u;
+            return exp(-u2 * 0.5) * u2 * p;
+        }
+        case GAPLAC_OU: {  // d/dl exp(-|u|): k |u| / l
+            const double a = fabs(p * xi - p * xj);
+            return exp(-a) * a * p;
+        }
+        case GAPLAC_LINEAR:  // d/dc (x_i x_j + c)
+            return 1.0;
+        case GAPLAC_CAT:
+            return 0.0;
+        default:  // NOISE term: d/dvariance
+            return diag ? 1.0 : 0.0;
+    }
+}
+
+// -C^{-1} tile (I, J), I >= J, into the (no longer needed) factor storage:
+// A[I, J] = -sum_{k >= I NB} Y_Ik Y_Jk^T. list[b] = I | J << 16 (0xffffffff = idle).
+__global__ __launch_bounds__(256, 2) void cinv_tile_kernel(double* __restrict__ A, int64_t lda, int64_t Np,
+                                                           const uint32_t* __restrict__ list,
+                                                           KTime* __restrict__ kt) {
+    kt_begin(kt);
+    const uint32_t e = list[blockIdx.x];
+    if (e != 0xffffffffu) {
+        const int I = (int)(e & 0xffffu), J = (int)(e >> 16);
+        const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+        const int wi = w & 1, wj = w >> 1;
+        const int fr = lane >> 4, fc = lane & 15;
+        const int64_t k0 = (int64_t)I * NB;
+        const double* Y = A + Np;
+        const bool active = !(I == J && wj > wi);
+        d4 acc[4][4];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int mj = 0; mj < 4; ++mj) acc[mi][mj] = d4{0.0, 0.0, 0.0, 0.0};
+        tile_mma_neg(Y + k0 * lda + (int64_t)I * NB, Y + k0 * lda + (int64_t)J * NB, lda, (int)(Np - k0), active,
+                     acc);
+        if (active) {
+            double* Ct = A + (int64_t)J * NB * lda + (int64_t)I * NB;
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                double* Ci = Ct + 64 * wi + 16 * mi + fc;
+#pragma unroll
+                for (int mj = 0; mj < 4; ++mj)
+#pragma unroll
+                    for (int rg = 0; rg < 4; ++rg)
+                        Ci[(int64_t)(64 * wj + 16 * mj + fr + 4 * rg) * lda] = acc[mi][mj][rg];
+            }
+        }
+    }
+    kt_end(kt);
+}
+
+__device__ __forceinline__ double wave_sum(double x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
+// Contraction of one lower tile (I, J) of M = -C^{-1} (in A) with every dC/dtheta:
+//   partial[tile][t] = sum_{(i,j) in tile, i >= j, i,j < N} wt_ij (alpha_i alpha_j + M_ij) dC_ij/dtheta_t
+// (wt = 2 off the diagonal: the symmetric pair), t = T: the observation variance
+// (dC/dnoise = I). Same lane layout as the Gram kernel: two rows per lane, column
+// coordinates staged in LDS.
+__global__ __launch_bounds__(256) void grad_contract_kernel(const double* __restrict__ A, int64_t lda, int64_t N,
+                                                            const double* __restrict__ X, int64_t ldx,
+                                                            const double* __restrict__ alpha,
+                                                            const TermPack* __restrict__ tpp,
+                                                            const GradTermPack* __restrict__ gpp,
+                                                            double* __restrict__ partial, KTime* __restrict__ kt) {
+    kt_begin(kt);
+    __shared__ double xcol[GAPLAC_MAX_TERMS][NB];
+    __shared__ double acol[NB];
+    __shared__ double red[4][GAPLAC_MAX_TERMS + 1];
+    const TermPack& tp = *tpp;
+    const int T = tp.T;
+    int I, J;
+    tri_index(blockIdx.x, I, J);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t c0 = (int64_t)J * NB;
+    for (int idx = tid; idx < T * NB; idx += 256) {
+        const int t = idx / NB, c = idx % NB;
+        const int64_t j = c0 + c;
+        xcol[t][c] = (j < N && tp.kind[t] != GAPLAC_NOISE) ? X[(int64_t)tp.col[t] * ldx + j] : 0.0;
+    }
+    if (tid < NB) acol[tid] = (c0 + tid < N) ? alpha[c0 + tid] : 0.0;
+    const int64_t i0 = (int64_t)I * NB + 2 * lane;
+    double xa[GAPLAC_MAX_TERMS], xb[GAPLAC_MAX_TERMS];
+#pragma unroll
+    for (int t = 0; t < GAPLAC_MAX_TERMS; ++t) {
+        xa[t] = 0.0;
+        xb[t] = 0.0;
+        if (t < T && tp.kind[t] != GAPLAC_NOISE) {
+            const double* xc = X + (int64_t)tp.col[t] * ldx;
+            if (i0 < N) xa[t] = xc[i0];
+            if (i0 + 1 < N) xb[t] = xc[i0 + 1];
+        }
+    }
+    const double ai0 = i0 < N ? alpha[i0] : 0.0, ai1 = i0 + 1 < N ? alpha[i0 + 1] : 0.0;
+    double g[GAPLAC_MAX_TERMS + 1];
+#pragma unroll
+    for (int t = 0; t <= GAPLAC_MAX_TERMS; ++t) g[t] = 0.0;
+    __syncthreads();
+    const double* Mt = A + c0 * lda + i0;
+    for (int cc = w; cc < NB; cc += 4) {
+        const int64_t j = c0 + cc;
+        if (j >= N) break;
+        const double2 m = *reinterpret_cast<const double2*>(Mt + (int64_t)cc * lda);
+        const double aj = acol[cc];
+        const double wt0 = (i0 < N && i0 >= j) ? (i0 == j ? 1.0 : 2.0) : 0.0;
+        const double wt1 = (i0 + 1 < N && i0 + 1 >= j) ? (i0 + 1 == j ? 1.0 : 2.0) : 0.0;
+        const double w0 = wt0 * (ai0 * aj + m.x), w1 = wt1 * (ai1 * aj + m.y);
+        if (i0 == j) g[GAPLAC_MAX_TERMS] += w0;
+        if (i0 + 1 == j) g[GAPLAC_MAX_TERMS] += w1;
+#pragma unroll
+        for (int t = 0; t < GAPLAC_MAX_TERMS; ++t) {
+            if (t < T) {
+                const int kind = tp.kind[t];
+                const double p = tp.p[t], xj = xcol[t][cc];
+                double d0 = term_dk(kind, p, xa[t], xj, i0 == j);
+                double d1 = term_dk(kind, p, xb[t], xj, i0 + 1 == j);
+                const int gs = gpp->gstart[t], ge = gpp->gend[t];
+                if (ge - gs > 1) {  // product-group extension: times the group's other terms
+#pragma unroll
+                    for (int s2 = 0; s2 < GAPLAC_MAX_TERMS; ++s2) {
+                        if (s2 >= gs && s2 < ge && s2 != t) {
+                            const double y = xcol[s2][cc];
+                            d0 *= term_k(tp.kind[s2], tp.p[s2], xa[s2], y, i0 == j);
+                            d1 *= term_k(tp.kind[s2], tp.p[s2], xb[s2], y, i0 + 1 == j);
+                        }
+                    }
+                }
+                g[t] += w0 * d0 + w1 * d1;
+            }
+        }
+    }
+    // fixed-order reduction: wave butterflies, then the 4 waves in order
+#pragma unroll
+    for (int t = 0; t <= GAPLAC_MAX_TERMS; ++t) {
+        const double x = wave_sum(g[t]);
+        if (lane == 0) red[w][t] = x;
+    }
+    __syncthreads();
+    if (tid <= T) {
+        const int t = tid == T ? GAPLAC_MAX_TERMS : tid;
+        partial[(int64_t)blockIdx.x * (T + 1) + tid] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    }
+    kt_end(kt);
+}
+
+// out[t] = 1/2 sum_b partial[b][t], t = 0..T, fixed order.
+__global__ __launch_bounds__(256) void grad_reduce_kernel(const double* __restrict__ partial, int nb, int T,
+                                                          double* __restrict__ out) {
+    __shared__ double s[256];
+    const int t = blockIdx.x, tid = threadIdx.x;
+    double x = 0.0;
+    for (int b = tid; b < nb; b += 256) x += partial[(int64_t)b * (T + 1) + t];
+    s[tid] = x;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) s[tid] += s[tid + o];
+        __syncthreads();
+    }
+    if (tid == 0) out[t] = 0.5 * s[0];
+}
+
 // ------------------------------- launchers ---------------------------------------
 void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const double* X,
                  int64_t ldx, const double* v, const TermPack* dtp, int part, int w, KTime* kt) {
@@ -862,7 +1179,13 @@ void launch_potrf_diag(hipStream_t s, double* Ablk, int64_t lda, int64_t N, int6
 void launch_trsm(hipStream_t s, double* Acol, int64_t lda, int nt, int k, const double* Dinv, KTime* kt) {
     const int n = nt - k - 1;
     if (n <= 0) return;
-    trsm_subst_kernel<<<dim3(2 * n), dim3(256), 0, s>>>(Acol, lda, k, Dinv, kt);
+    trsm_subst_kernel<<<dim3(2 * n), dim3(256), 0, s>>>(Acol, lda, k, k + 1, Dinv, kt);
+}
+
+void launch_trsm_rows(hipStream_t s, double* Acol, int64_t lda, int k, int bi0, int nrows, const double* Dinv,
+                      KTime* kt) {
+    if (nrows <= 0) return;
+    trsm_subst_kernel<<<dim3(2 * nrows), dim3(256), 0, s>>>(Acol, lda, k, bi0, Dinv, kt);
 }
 
 bool syrk_is_small(int ntiles) { return ntiles <= QUAD_BULK_MAX_TILES; }
@@ -899,6 +1222,65 @@ void build_tile_list(int m, uint32_t* out) {
 void launch_reduce(hipStream_t s, const double* C, int64_t ldc, int64_t N, int64_t ncols, ColMap cm,
                    EvalResult* res) {
     reduce_kernel<<<dim3(1), dim3(1024), 0, s>>>(C, ldc, N, ncols, cm, res);
+}
+
+void launch_init_identity_rows(hipStream_t s, double* A, int64_t lda, int64_t Np, int nt, int W) {
+    if (nt <= 0) return;
+    init_identity_rows_kernel<<<dim3((unsigned)nt, (unsigned)nt), dim3(256), 0, s>>>(A, lda, Np, W);
+}
+
+void launch_zero_tail_cols(hipStream_t s, double* A, int64_t lda, int64_t Np, int64_t N) {
+    if (Np <= N) return;
+    zero_tail_cols_kernel<<<dim3((unsigned)((Np + 255) / 256), (unsigned)(Np - N)), dim3(256), 0, s>>>(A, lda, Np, N);
+}
+
+void launch_alpha(hipStream_t s, const double* A, int64_t lda, int64_t Np, int64_t N, double* partial,
+                  double* alpha, double* dv) {
+    if (N <= 0) return;
+    const int nk = (int)((N + 511) / 512);
+    alpha_partial_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nk), dim3(256), 0, s>>>(A, lda, Np, N,
+                                                                                             partial);
+    alpha_reduce_kernel<<<dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s>>>(partial, N, nk, alpha, dv);
+}
+
+void launch_cinv_tiles(hipStream_t s, double* A, int64_t lda, int64_t Np, const uint32_t* list, int nblocks,
+                       KTime* kt) {
+    if (nblocks <= 0) return;
+    cinv_tile_kernel<<<dim3((unsigned)nblocks), dim3(256), 0, s>>>(A, lda, Np, list, kt);
+}
+
+void launch_grad_contract(hipStream_t s, const double* A, int64_t lda, int64_t N, const double* X, int64_t ldx,
+                          const double* alpha, const TermPack* dtp, const GradTermPack* dgp, double* partial,
+                          KTime* kt) {
+    const int m = (int)((N + NB - 1) / NB);
+    const int64_t tiles = (int64_t)m * (m + 1) / 2;
+    if (tiles <= 0) return;
+    grad_contract_kernel<<<dim3((unsigned)tiles), dim3(256), 0, s>>>(A, lda, N, X, ldx, alpha, dtp, dgp, partial,
+                                                                     kt);
+}
+
+void launch_grad_reduce(hipStream_t s, const double* partial, int nb, int T, double* out) {
+    grad_reduce_kernel<<<dim3((unsigned)(T + 1)), dim3(256), 0, s>>>(partial, nb, T, out);
+}
+
+// Lower m x m tile triangle in 8x8 super-tiles, super-rows first (deepest Y products
+// first: tile (I, J) contracts over Np - I NB columns); super-tile s goes to XCD s % 8
+// (the dispatcher deals workgroup b to XCD b % 8), so every XCD gets a share of the deep
+// tiles and its resident tiles share 8 + 8 panel row blocks in its L2.
+void build_grad_list(int m, std::vector<uint32_t>& out) {
+    std::vector<std::vector<uint32_t>> seq(8);
+    int st = 0;
+    for (int I = 0; I < (m + 7) / 8; ++I)
+        for (int J = 0; J <= I; ++J, ++st) {
+            std::vector<uint32_t>& q = seq[(size_t)(st & 7)];
+            for (int i = 8 * I; i < 8 * I + 8 && i < m; ++i)
+                for (int j = 8 * J; j < 8 * J + 8 && j <= i; ++j) q.push_back((uint32_t)i | ((uint32_t)j << 16));
+        }
+    size_t len = 0;
+    for (const auto& q : seq) len = std::max(len, q.size());
+    out.assign(8 * len, 0xffffffffu);
+    for (size_t x = 0; x < 8; ++x)
+        for (size_t k = 0; k < seq[x].size(); ++k) out[8 * k + x] = seq[x][k];
 }
 
 void launch_init_result(hipStream_t s, EvalResult* res) {

@@ -116,6 +116,27 @@ int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D,
                         const gaplac_term* terms, double noise, const double* v,
                         double* out_logpdf, int64_t* out_info);
 
+/* Gradient of the same log-marginal-likelihood. NUTS in
+ * CLI/src/mcmc.jl:31-41 differentiates logpdf(FiniteGP(GP(kernel(formula; ℓ)), RowVecs(X),
+ * 0.1), fx) with ForwardDiff Duals, which cannot cross a ccall; the GaPLAC-owned method
+ * returns the analytic gradient instead (a ChainRules rrule / Dual overload):
+ *     out_dv[i]     = d logp / d v_i          = -(C^{-1} v)_i                  (N entries)
+ *     out_dparam[t] = d logp / d param_t      = 1/2 (a' dC a - tr(C^{-1} dC)),  a = C^{-1} v,
+ *                     dC = dK_t/dparam_t (times the other terms of t's product group):
+ *                     l of SQEXP / OU (k u^2/l, k |u|/l with u = x_i/l - x_j/l), c of LINEAR (1),
+ *                     the variance of a NOISE term (delta_ij); 0 for CAT (no parameter)
+ *     out_dnoise    = d logp / d noise        (dC = I)
+ * The mcmc glue sums out_dparam over the terms whose variable is in `--infer` (they share ℓ).
+ * Any output pointer may be NULL. Same return convention as gaplac_logpdf (outputs NaN on
+ * error / PosDefException). Replaces: ForwardDiff.gradient through AbstractGPs.logpdf. */
+int gaplac_logpdf_grad(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx,
+                       int32_t T, const gaplac_term* terms, double noise, const double* v,
+                       double* out_logpdf, double* out_dv, double* out_dparam, double* out_dnoise);
+/* Same with X and v resident on the device (outputs are host pointers). */
+int gaplac_logpdf_grad_device(gaplac_ctx* ctx, int64_t N, int32_t D, const double* dX, int64_t ldx,
+                              int32_t T, const gaplac_term* terms, double noise, const double* dv,
+                              double* out_logpdf, double* out_dv, double* out_dparam, double* out_dnoise);
+
 /* Debug / parity entries (tests only; not on the timed path). */
 /* Gram matrix sum_t K_t(X) + noise*I as a dense N×N column-major host matrix
  * (replaces KernelFunctions.kernelmatrix + Diagonal(Fill(noise, N))). */
@@ -151,6 +172,11 @@ typedef struct gaplac_stats {
                                    written once, panel rows read once */
     int64_t small_launches;     /* small trailing updates (quad_bulk_kernel), not in syrk_* */
     double  small_ms;
+    /* gradient evaluations (gaplac_logpdf_grad), profiling mode 1 */
+    double  grad_rows_ms;       /* identity-row substitution + updates (L^{-T} rows) */
+    int64_t cinv_launches;      /* -C^{-1} = -L^{-T} L^{-1} tile launches (cinv_tile_kernel) */
+    double  cinv_ms;
+    double  contract_ms;        /* dC/dtheta contraction (grad_contract_kernel) */
 } gaplac_stats;
 int gaplac_set_profiling(gaplac_ctx* ctx, int mode);
 int gaplac_get_stats(gaplac_ctx* ctx, gaplac_stats* out);

@@ -154,3 +154,93 @@ def cholesky_lower(X, terms, noise: float):
     if info > 0:
         raise PosDefException(int(info))
     return U.T.copy()
+
+
+# ---------------------------------------------------------------------------------------
+# Gradient of the log-marginal-likelihood (what NUTS in
+# CLI/src/mcmc.jl:31-41 differentiates through logpdf(FiniteGP, fx) with ForwardDiff).
+#   d logp / d v      = -alpha,  alpha = C^-1 v
+#   d logp / d theta  = 1/2 * sum_ij (alpha_i alpha_j - (C^-1)_ij) dC_ij/dtheta
+# per term parameter theta (l of SqExp/OU, c of Linear, variance of a Noise term; Cat
+# has none -> 0) and for the FiniteGP observation variance (dC/dnoise = I).
+# Term derivatives of the KernelFunctions kernels built at
+# src/abstractgp_translations.jl:8-15 (u = x_i/l - x_j/l, the ScaleTransform(1/l) form):
+#   SqExp  k = exp(-u^2/2)  dk/dl = k u^2 / l
+#   OU     k = exp(-|u|)    dk/dl = k |u| / l
+#   Linear k = x_i x_j + c  dk/dc = 1
+# A term inside a product group (extension) is multiplied by the group's other terms.
+# ---------------------------------------------------------------------------------------
+def term_derivative(X: np.ndarray, kind: int, col: int, param: float) -> np.ndarray:
+    """dK_t/dparam_t for one term (zeros for Cat)."""
+    N = X.shape[0]
+    if kind == NOISE:
+        return np.eye(N)
+    if kind == CAT:
+        return np.zeros((N, N))
+    x = np.ascontiguousarray(X[:, col], dtype=np.float64)
+    if kind == LINEAR:
+        return np.ones((N, N))
+    s = 1.0 / param
+    sx = s * x
+    u = sx[:, None] - sx[None, :]
+    if kind == SQEXP:
+        return np.exp(-(u * u) * 0.5) * (u * u) / param
+    if kind == OU:
+        a = np.abs(u)
+        return np.exp(-a) * a / param
+    raise ValueError(f"unknown term kind {kind}")
+
+
+def logpdf_grad(X, terms, noise: float, v):
+    """(logpdf, dv, dparam[T], dnoise) with the definitions above.
+
+    Raises PosDefException(info) like logpdf."""
+    X = np.asarray(X, dtype=np.float64)
+    if X.ndim == 1:
+        X = X[:, None]
+    v = np.asarray(v, dtype=np.float64)
+    terms = list(terms)
+    N = X.shape[0]
+    if N == 0:
+        return -0.0, np.zeros(0), np.zeros(len(terms)), 0.0
+    C = gram(X, terms, noise)
+    lp, _, _ = logpdf_from_cov(C, v)
+    U, info = lapack.dpotrf(C, lower=0, clean=1, overwrite_a=0)
+    alpha = scipy.linalg.cho_solve((U, False), v, check_finite=False)
+    Cinv = scipy.linalg.cho_solve((U, False), np.eye(N), check_finite=False)
+    W = np.outer(alpha, alpha) - Cinv
+    dparam = np.zeros(len(terms))
+    for t, (kind, col, param, group) in enumerate(terms):
+        dK = term_derivative(X, kind, col, param)
+        for s, (k2, c2, p2, g2) in enumerate(terms):
+            if s != t and g2 == group:
+                dK = dK * term_matrix(X, k2, c2, p2)
+        dparam[t] = 0.5 * float(np.sum(W * dK))
+    dnoise = 0.5 * float(np.trace(W))
+    return float(lp), -alpha, dparam, dnoise
+
+
+def logpdf_grad_scale(X, terms, noise: float, v):
+    """Per-parameter magnitude 1/2 sum_ij |alpha_i alpha_j - Cinv_ij| |dC_ij| (and the same
+    for the observation variance): the size of the terms the gradient sums, used to state
+    the parity tolerance of a gradient entry that cancels to near zero."""
+    X = np.asarray(X, dtype=np.float64)
+    if X.ndim == 1:
+        X = X[:, None]
+    terms = list(terms)
+    N = X.shape[0]
+    C = gram(X, terms, noise)
+    U, info = lapack.dpotrf(C, lower=0, clean=1, overwrite_a=0)
+    if info:
+        raise PosDefException(int(info))
+    alpha = scipy.linalg.cho_solve((U, False), np.asarray(v, dtype=np.float64), check_finite=False)
+    Cinv = scipy.linalg.cho_solve((U, False), np.eye(N), check_finite=False)
+    A = np.abs(np.outer(alpha, alpha)) + np.abs(Cinv)
+    out = np.zeros(len(terms))
+    for t, (kind, col, param, group) in enumerate(terms):
+        dK = term_derivative(X, kind, col, param)
+        for s2, (k2, c2, p2, g2) in enumerate(terms):
+            if s2 != t and g2 == group:
+                dK = dK * term_matrix(X, k2, c2, p2)
+        out[t] = 0.5 * float(np.sum(A * np.abs(dK)))
+    return out, 0.5 * float(np.trace(A))

@@ -52,6 +52,12 @@ def case(name, X, terms, noise, v, formula=None, vars_=None, note=""):
     try:
         lp, ld, q = R.logpdf(X, terms, noise, v)
         rec.update(info=0, logpdf=lp.hex(), logdet=ld.hex(), quad=q.hex())
+        # gradient (gaplac_logpdf_grad): d/dv, d/dparam per term, d/dnoise, and the
+        # per-entry magnitude scale the parity tolerance is stated against
+        _, dv, dparam, dnoise = R.logpdf_grad(X, terms, noise, v)
+        sc, scn = R.logpdf_grad_scale(X, terms, noise, v)
+        rec.update(dv=hexs(dv), dparam=hexs(dparam), dnoise=float(dnoise).hex(),
+                   dparam_scale=hexs(sc), dnoise_scale=float(scn).hex())
         try:
             lpg, _, _ = R.logpdf(X, terms, noise, v, distances="gemm")
             rec["logpdf_gemm_distances"] = lpg.hex()

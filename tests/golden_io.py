@@ -23,7 +23,11 @@ def load_cases():
         c["v"] = np.array([float.fromhex(h) for h in c["v"]])
         c["terms"] = [(k, col, float.fromhex(p), g) for (k, col, p, g) in c["terms"]]
         c["noise"] = float.fromhex(c["noise"])
-        for key in ("logpdf", "logdet", "quad", "gram_sum", "gram_diag_sum", "logpdf_gemm_distances"):
+        for key in ("logpdf", "logdet", "quad", "gram_sum", "gram_diag_sum", "logpdf_gemm_distances", "dnoise",
+                    "dnoise_scale"):
             c[key] = _f(c.get(key))
+        for key in ("dv", "dparam", "dparam_scale"):
+            if c.get(key) is not None:
+                c[key] = np.array([float.fromhex(h) for h in c[key]])
         out.append(c)
     return out
