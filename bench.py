@@ -114,11 +114,12 @@ def main():
     ap.add_argument("--skip-cpu", action="store_true", help="skip the CPU baseline leg (profiling runs)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event pass")
     ap.add_argument("--profile-steps", type=int, default=2, help="eager steps timed per kernel after the timed region")
-    ap.add_argument("--mode", choices=("replicas", "dist", "single", "select"), default="replicas",
+    ap.add_argument("--mode", choices=("replicas", "dist", "single", "select", "grad"), default="replicas",
                     help="replicas (default, the headline metric): independent evals per GPU; dist: one "
                          "evaluation spread over all ranks (BASELINE configs[3], N=65536); single: the "
                          "single-GPU path at --n (comparison line for dist); select: BASELINE configs[4], "
-                         "64 candidate formulas x N=8192 through gaplac_logpdf_batch, sharded over ranks")
+                         "64 candidate formulas x N=8192 through gaplac_logpdf_batch, sharded over ranks; "
+                         "grad: logpdf + gradient (gaplac_logpdf_grad, the mcmc/NUTS step) on the configs[2] workload")
     ap.add_argument("--loopback", type=int, default=0,
                     help="dist mode on ONE GPU: emulate this many ranks in-process (schedule timing only)")
     ap.add_argument("--spw", type=int, default=4, help="dist mode: super-panel width in 128-column tiles")
@@ -127,6 +128,8 @@ def main():
         return main_dist(args)
     if args.mode == "select":
         return main_select(args)
+    if args.mode == "grad":
+        return main_grad(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -273,6 +276,129 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "extra": extra,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_grad_baseline(N: int):
+    """One oracle gradient evaluation (numpy Gram, scipy-openblas dpotrf + dpotri, numpy
+    dK/dtheta contractions) at N on the host cores."""
+    from oracle import restatement as R
+    X, v = make_inputs(N)
+    Xs, vs = make_inputs(1024)
+    R.logpdf_grad_potri(Xs, terms_for(1.5), 0.1, vs)
+    t0 = time.perf_counter()
+    R.logpdf_grad_potri(X, terms_for(1.5), 0.1, v)
+    dt = time.perf_counter() - t0
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max((d.get("num_threads", 1) for d in threadpool_info() if d.get("user_api") == "blas"), default=1)
+    except Exception:
+        threads = os.cpu_count() or 1
+    return {"value": 1.0 / dt, "unit": "grad evals/s", "cores": int(threads), "kind": "port",
+            "sample": f"1 full logpdf+gradient eval at N={N} (same workload), {dt:.1f} s: numpy Gram, scipy-openblas "
+                      f"dpotrf + dpotri ({threads} BLAS threads), numpy dK/dtheta contractions (1 thread)"}
+
+
+def main_grad(args):
+    """logpdf + gradient evals/s (the mcmc NUTS step: gaplac_logpdf_grad_device), replicas."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    from gaplac_amd.backend import Context
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    N = args.n
+    X, v = make_inputs(N)
+    dX = torch.from_numpy(np.ascontiguousarray(X.T)).to("cuda")
+    dv = torch.from_numpy(v).to("cuda")
+    torch.cuda.synchronize()
+    ctx = Context(local_rank)
+
+    def step(i):
+        lval = LENGTHSCALES[(i + rank) % len(LENGTHSCALES)]
+        return ctx.logpdf_grad_device(N, 2, dX.data_ptr(), N, terms_for(lval), 0.1, dv.data_ptr())
+
+    for i in range(args.warmup):
+        step(i)
+    ctx.reset_stats()
+    ctx.set_profiling(0 if args.no_profile else 2)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = None
+    for i in range(args.steps):
+        res = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_profiling(0)
+    st_ev = ctx.stats()
+    st = None
+    if not args.no_profile and args.profile_steps > 0:
+        ctx.reset_stats()
+        ctx.set_profiling(True)
+        for i in range(args.profile_steps):
+            step(i)
+        ctx.set_profiling(False)
+        st = ctx.stats()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    value = args.steps * world / elapsed
+    Np = (N + 1 + 127) // 128 * 128
+    m = (N + 127) // 128
+    # -C^{-1} tiles: algorithmic flops of the lower triangle of Y Y^T (Y = L^{-T} upper
+    # triangular): sum_{i >= j} 2 (N - i) = N^3/3 + O(N^2)
+    cinv_flops = N ** 3 / 3.0
+    roofline = None
+    if st_ev["cinv_launches"] > 0 and st_ev["cinv_ms"] > 0:
+        avg_s = st_ev["cinv_ms"] / st_ev["cinv_launches"] / 1e3
+        ach = cinv_flops / avg_s / 1e12
+        roofline = {"bound": "mfma", "kernel": "cinv_tile_kernel (-C^{-1} = -L^{-T} L^{-1} lower tiles, fp64 MFMA 16x16x4)",
+                    "achieved": round(ach, 3), "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(ach / PEAK_F64_TFLOPS, 4), "traffic": None,
+                    "flops_per_launch": cinv_flops, "avg_launch_ms": avg_s * 1e3,
+                    "launches": st_ev["cinv_launches"],
+                    "timing": "hipEvents on s_main around every cinv_tile_kernel launch inside the timed region"}
+    grad_flops = N ** 3  # potrf N^3/3 + identity rows (L^{-T}) N^3/3 + C^{-1} N^3/3
+    tf = grad_flops * (value / world) / 1e12
+    extra = {"whole_eval": {"flops_per_eval": grad_flops, "achieved_tflops_per_gpu": round(tf, 3),
+                            "frac_of_fp64_peak": round(tf / PEAK_F64_TFLOPS, 4)},
+             "last_logpdf": res[0], "last_dparam": [float(x) for x in res[2]], "last_dnoise": res[3]}
+    if st_ev["syrk_launches"] > 0 and st_ev["syrk_ms"] > 0:
+        extra["tile_syrk_tflops"] = round(st_ev["syrk_flops"] / (st_ev["syrk_ms"] / 1e3) / 1e12, 3)
+    if st and st["evals"] > 0:
+        e = st["evals"]
+        extra.update(profiled_span_ms_per_eval=st["total_ms"] / e, syrk_ms_per_eval=st["syrk_ms"] / e,
+                     identity_rows_ms_per_eval=st["grad_rows_ms"] / e, cinv_ms_per_eval=st["cinv_ms"] / e,
+                     contract_ms_per_eval=st["contract_ms"] / e, diag_ms_per_eval=st["panel_ms"] / e,
+                     trsm_ms_per_eval=st["trsm_ms"] / e, colupd_ms_per_eval=st["colupd_ms"] / e)
+    cpu = None
+    if world == 1 and not args.skip_cpu:
+        cpu = cpu_grad_baseline(N)
+    out = {
+        "metric": f"log-marginal-likelihood + gradient evals/sec at N={N} fp64 (mcmc NUTS step)",
+        "value": value, "unit": "grad evals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded t~U(0,10), subject~randint(0,N/3), v~N(0,1); inputs resident in HBM)",
+        "config": {"workload": f"BASELINE configs[2] terms, gradient w.r.t. v, every term parameter and the noise, N={N}",
+                   "N": N, "terms": 4, "parallelism": "replicas" if world > 1 else "single"},
+        "roofline": roofline, "cpu_baseline": cpu, "extra": extra,
     }
     print(json.dumps(out), flush=True)
     if world > 1:

@@ -53,6 +53,7 @@ struct gaplac_ctx {
     struct EvPair {
         size_t i0;
         double flops, bytes;
+        int kind;  // 0 bulk tile_syrk launch, 8 cinv_tile launch
     };
     std::vector<EvPair> evpairs;
     bool serial = false;  // GAPLAC_SERIAL=1: one stream, no overlap (per-kernel timing)
@@ -409,7 +410,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             launch_bulk(sm, ba, kt);
             if (ev) {
                 HIPCK(ctx, hipEventRecord(ctx->evpool[e0 + 1], sm));
-                ctx->evpairs.push_back({e0, syrk_flops(m) * (kd / NB), syrk_bytes(m, kd)});
+                ctx->evpairs.push_back({e0, syrk_flops(m) * (kd / NB), syrk_bytes(m, kd), 0});
             }
         }
         HIPCK(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
@@ -462,7 +463,22 @@ int enqueue_eval(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt) {
         hipStream_t sm = ctx->s_main;
         launch_zero_tail_cols(sm, ctx->A, lda, Np, N);
         launch_alpha(sm, ctx->A, lda, Np, N, ctx->gpart, ctx->galpha, ctx->gdv);
+        size_t e0 = 0;
+        const bool ev = ctx->prof_mode == 2;
+        if (ev) {
+            e0 = 2 * ctx->evpairs.size();
+            while (ctx->evpool.size() < e0 + 2) {
+                hipEvent_t e;
+                HIPCK(ctx, hipEventCreate(&e));
+                ctx->evpool.push_back(e);
+            }
+            HIPCK(ctx, hipEventRecord(ctx->evpool[e0], sm));
+        }
         launch_cinv_tiles(sm, ctx->A, lda, Np, ctx->glist, ctx->glist_blocks, slot(ctx, 8, 0));
+        if (ev) {
+            HIPCK(ctx, hipEventRecord(ctx->evpool[e0 + 1], sm));
+            ctx->evpairs.push_back({e0, 0.0, 0.0, 8});
+        }
         launch_grad_contract(sm, ctx->A, lda, N, ctx->dX, N, ctx->galpha, ctx->dtp, ctx->dgp, ctx->gpart,
                              slot(ctx, 9, 0));
         const int m = (int)((N + NB - 1) / NB);
@@ -1021,6 +1037,11 @@ int gaplac_get_stats(gaplac_ctx* ctx, gaplac_stats* out) {
         for (const auto& p : ctx->evpairs) {
             float ms = 0.f;
             HIPCK(ctx, hipEventElapsedTime(&ms, ctx->evpool[p.i0], ctx->evpool[p.i0 + 1]));
+            if (p.kind == 8) {
+                ctx->stats.cinv_ms += ms;
+                ctx->stats.cinv_launches += 1;
+                continue;
+            }
             ctx->stats.syrk_ms += ms;
             ctx->stats.syrk_flops += p.flops;
             ctx->stats.syrk_bytes += p.bytes;

@@ -154,8 +154,9 @@ int gaplac_factor(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_
  *   1 per-launch device timestamps of every kernel (first workgroup start, last wave
  *     end; 100 MHz s_memrealtime);
  *   2 hipEvents recorded on the launching stream around every bulk trailing-update
- *     (tile_syrk_kernel) launch, the production schedule otherwise unchanged: fills
- *     syrk_* only, read back at gaplac_get_stats. */
+ *     (tile_syrk_kernel) launch and every -C^{-1} tile launch of a gradient evaluation,
+ *     the production schedule otherwise unchanged: fills syrk_* and cinv_* only, read
+ *     back at gaplac_get_stats. */
 typedef struct gaplac_stats {
     int64_t evals;
     int64_t syrk_launches;      /* bulk trailing-update launches (tile_gemm_kernel<0>) */

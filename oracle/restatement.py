@@ -244,3 +244,34 @@ def logpdf_grad_scale(X, terms, noise: float, v):
                 dK = dK * term_matrix(X, k2, c2, p2)
         out[t] = 0.5 * float(np.sum(A * np.abs(dK)))
     return out, 0.5 * float(np.trace(A))
+
+
+def logpdf_grad_potri(X, terms, noise: float, v):
+    """Same result as logpdf_grad with C^{-1} from LAPACK dpotri on the dpotrf factor (what a
+    CPU port of the gradient would call; used as bench.py's timed CPU baseline for the
+    gradient). Returns (logpdf, dv, dparam, dnoise)."""
+    X = np.asarray(X, dtype=np.float64)
+    if X.ndim == 1:
+        X = X[:, None]
+    v = np.asarray(v, dtype=np.float64)
+    terms = list(terms)
+    C = gram(X, terms, noise)
+    lp, _, _ = logpdf_from_cov(C, v)
+    U, info = lapack.dpotrf(C, lower=0, clean=1, overwrite_a=1)
+    del C
+    alpha = scipy.linalg.cho_solve((U, False), v, check_finite=False)
+    Cinv, info = lapack.dpotri(U, lower=0, overwrite_c=1)
+    del U
+    Cinv = np.triu(Cinv) + np.triu(Cinv, 1).T
+    W = np.outer(alpha, alpha)
+    W -= Cinv
+    del Cinv
+    dparam = np.zeros(len(terms))
+    for t, (kind, col, param, group) in enumerate(terms):
+        dK = term_derivative(X, kind, col, param)
+        for s2, (k2, c2, p2, g2) in enumerate(terms):
+            if s2 != t and g2 == group:
+                dK *= term_matrix(X, k2, c2, p2)
+        dparam[t] = 0.5 * float(np.vdot(W, dK))
+        del dK
+    return float(lp), -alpha, dparam, 0.5 * float(np.trace(W))
