@@ -92,11 +92,12 @@ def cpu_baseline(N: int, budget_s: float = 25.0):
 
 # PMC traffic of the dominant kernel (tools/profile_round.sh: FETCH_SIZE / WRITE_SIZE
 # passes over the same command, corrected per MI355X_MICROARCH.md; per launch).
-TRAFFIC_FILE = os.path.join("profiles", "r01d_traffic_syrk.json")
+TRAFFIC_FILE = os.path.join("profiles", "r01e_traffic_syrk.json")
+TRAFFIC_FILE_CINV = os.path.join("profiles", "r01e_traffic_cinv.json")
 
 
-def load_traffic():
-    path = os.path.join(HERE, TRAFFIC_FILE)
+def load_traffic(name=TRAFFIC_FILE):
+    path = os.path.join(HERE, name)
     try:
         with open(path) as f:
             d = json.load(f)
@@ -370,7 +371,10 @@ def main_grad(args):
         ach = cinv_flops / avg_s / 1e12
         roofline = {"bound": "mfma", "kernel": "cinv_tile_kernel (-C^{-1} = -L^{-T} L^{-1} lower tiles, fp64 MFMA 16x16x4)",
                     "achieved": round(ach, 3), "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(ach / PEAK_F64_TFLOPS, 4), "traffic": None,
+                    "frac": round(ach / PEAK_F64_TFLOPS, 4), "traffic": load_traffic(TRAFFIC_FILE_CINV)[0],
+                    "traffic_source": load_traffic(TRAFFIC_FILE_CINV)[1],
+                    # Y's upper triangle read once + M's lower triangle written once
+                    "traffic_algorithmic": 2 * 8.0 * Np * (Np + 1) / 2,
                     "flops_per_launch": cinv_flops, "avg_launch_ms": avg_s * 1e3,
                     "launches": st_ev["cinv_launches"],
                     "timing": "hipEvents on s_main around every cinv_tile_kernel launch inside the timed region"}
