@@ -29,6 +29,8 @@ EXPORTED = (
     "gaplac_logpdf_batch",
     "gaplac_logpdf_grad",
     "gaplac_logpdf_grad_device",
+    "gaplac_posterior_mean_var",
+    "gaplac_rand",
     "gaplac_gram",
     "gaplac_factor",
     "gaplac_set_profiling",
@@ -113,6 +115,8 @@ def load() -> ctypes.CDLL:
     ]
     lib.gaplac_logpdf_grad.argtypes = common + [_DP, c_void_p, c_void_p, _DP]
     lib.gaplac_logpdf_grad_device.argtypes = common + [_DP, c_void_p, c_void_p, _DP]
+    lib.gaplac_posterior_mean_var.argtypes = common + [c_int64, c_void_p, c_int64, c_void_p, c_void_p]
+    lib.gaplac_rand.argtypes = common + [c_void_p]
     lib.gaplac_gram.argtypes = [
         c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, POINTER(Term), c_double, c_void_p, c_int64,
     ]

@@ -68,6 +68,59 @@ def logpdf_and_gradient(fx: FiniteGP, y, ctx: backend.Context | None = None):
     return ctx.logpdf_grad(fx.x, fx.terms, fx.noise, y)
 
 
+class PosteriorGP:
+    """AbstractGPs.posterior(fx, y): the GP conditioned on observations y at fx's inputs.
+    Evaluation happens per query (mean_and_var at test inputs), one gaplac_posterior_mean_var
+    call each."""
+
+    def __init__(self, fx: FiniteGP, y, ctx: backend.Context | None = None):
+        y = np.asarray(y, dtype=np.float64)
+        if y.shape[0] != len(fx):
+            raise F.ArgumentError("DimensionMismatch: length of y does not match the FiniteGP")
+        self.prior = fx
+        self.y = y
+        self.ctx = ctx
+
+    def _xs(self, x):
+        X = np.asarray(x, dtype=np.float64)
+        if X.ndim == 1:
+            X = X[:, None]
+        return X
+
+    def mean_and_var(self, x):
+        """AbstractGPs.mean_and_var(f::PosteriorGP, x): posterior mean and marginal variance
+        (latent: no observation noise) at the rows of x."""
+        ctx = self.ctx or backend.default_context()
+        return ctx.posterior_mean_var(self.prior.x, self.prior.terms, self.prior.noise, self.y, self._xs(x))
+
+    def mean(self, x):
+        return self.mean_and_var(x)[0]
+
+    def var(self, x):
+        return self.mean_and_var(x)[1]
+
+
+def posterior(fx: FiniteGP, y, ctx: backend.Context | None = None) -> PosteriorGP:
+    """AbstractGPs.posterior(fx, y) (CLI/src/select.jl:51-52, src/plotting.jl:8)."""
+    return PosteriorGP(fx, y, ctx)
+
+
+def mean_and_var(f: PosteriorGP, x):
+    """AbstractGPs.mean_and_var(pgp, xtest) (src/plotting.jl:12)."""
+    return f.mean_and_var(x)
+
+
+def rand(fx: FiniteGP, z=None, rng=None, ctx: backend.Context | None = None):
+    """rand(rng, fx) = cholesky(C).U' * randn(rng, N) for the zero-mean FiniteGP
+    (CLI/src/sample.jl:25). The standard-normal draws stay on the host: pass z, or an rng
+    (numpy Generator) to draw it."""
+    ctx = ctx or backend.default_context()
+    if z is None:
+        rng = rng if rng is not None else np.random.default_rng()
+        z = rng.standard_normal(len(fx))
+    return ctx.rand(fx.x, fx.terms, fx.noise, z)
+
+
 def make_gp(spec: F.Spec, hyperparams=None):
     """src/interface.jl:36-41 — (GP(kern), vars), checking #vars == #kernels."""
     kern, vars_ = K.kernel(F.formula(spec), hyperparams)

@@ -166,6 +166,46 @@ class Context:
         self._check(rc)
         return lp.value, dv, dp[: len(terms)].copy(), dn.value
 
+    def posterior_mean_var(self, X, terms, noise: float, y, Xs):
+        """(mean, var) of the posterior of the zero-mean FiniteGP given y, at the rows of Xs
+        (gaplac_posterior_mean_var)."""
+        Xc = _colmajor(X)
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        N, D = Xc.shape
+        if y.shape[0] != N:
+            raise ArgumentError(f"length of y ({y.shape[0]}) != N ({N})")
+        Xsc = _colmajor(Xs)
+        M = Xsc.shape[0]
+        if Xsc.shape[1] != D:
+            raise ArgumentError(f"test inputs have {Xsc.shape[1]} columns, training inputs {D}")
+        terms = list(terms)
+        ta = term_array(terms)
+        mean = np.empty(M, dtype=np.float64)
+        var = np.empty(M, dtype=np.float64)
+        rc = self.lib.gaplac_posterior_mean_var(
+            self.h, N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), len(terms), ta, float(noise),
+            y.ctypes.data_as(c_void_p), M, Xsc.ctypes.data_as(c_void_p), max(M, 1),
+            mean.ctypes.data_as(c_void_p), var.ctypes.data_as(c_void_p),
+        )
+        self._check(rc)
+        return mean, var
+
+    def rand(self, X, terms, noise: float, z):
+        """L z with C = K(X) + noise I = L L^T (gaplac_rand): one draw of the FiniteGP for the
+        standard-normal vector z."""
+        Xc = _colmajor(X)
+        z = np.ascontiguousarray(z, dtype=np.float64)
+        N, D = Xc.shape
+        if z.shape[0] != N:
+            raise ArgumentError(f"length of z ({z.shape[0]}) != N ({N})")
+        terms = list(terms)
+        ta = term_array(terms)
+        out = np.empty(N, dtype=np.float64)
+        rc = self.lib.gaplac_rand(self.h, N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), len(terms), ta,
+                                  float(noise), z.ctypes.data_as(c_void_p), out.ctypes.data_as(c_void_p))
+        self._check(rc)
+        return out
+
     def gram(self, X, terms, noise: float = 0.0) -> np.ndarray:
         Xc = _colmajor(X)
         N, D = Xc.shape

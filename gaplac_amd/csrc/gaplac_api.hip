@@ -86,9 +86,18 @@ struct gaplac_ctx {
     std::vector<gaplac_ctx*> lanes;
     int batch_lanes = 2;           // GAPLAC_BATCH_LANES (measured at N=8192: 1 lane 138, 2 lanes 191, 3-6 lanes 161-187 evals/s)
     bool borrowed_inputs = false;  // dX / dv belong to the parent
-    // Gradient (gaplac_logpdf_grad): identity rows below the matrix (lda =
-    // 2 Np while grad_rows), alpha, partial sums, the XCD-balanced C^{-1} tile list.
-    bool grad_rows = false;
+    // Extra rows below the matrix, factored along (lda = Np + 128 xr_tiles):
+    //   1 = identity rows E = [I 0] -> L^{-T} (gradient, gaplac_logpdf_grad)
+    //   2 = K(xs, X) -> (L^{-1} K(X, xs))^T (posterior, gaplac_posterior_mean_var, §10)
+    int xr_mode = 0;
+    int xr_tiles = 0;
+    int64_t xr_M = 0;       // mode 2: test points
+    double* dXs = nullptr;  // mode 2: test inputs (ld M)
+    size_t dXs_elems = 0;
+    double* pmean = nullptr;
+    double* pvar = nullptr;
+    size_t pmv_elems = 0;
+    // gradient: alpha, partial sums, the XCD-balanced C^{-1} tile list
     double* galpha = nullptr;
     size_t galpha_elems = 0;
     double* gdv = nullptr;
@@ -338,29 +347,35 @@ void factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, 
     }
 }
 
-// Gradient rows: the identity rows E (tile rows nt .. 2nt-1 of the column
-// storage, lda = 2 Np) are factored along on s_main, off the critical path: once SP p's
-// columns are final (P(p)), its identity-row tiles get the column-by-column substitution
-// (rows E <= c of column c; the earlier columns of the SP are applied first, K = 128),
-// then SP p is applied to every later column (rows E < end of SP p, K = 128 W). Tiles
-// below the identity rows' diagonal (E > J) stay exactly zero and are never touched.
-void identity_rows_step(gaplac_ctx* ctx, hipStream_t sm, int64_t lda, int nt, int p) {
+// Extra rows, tile rows nt .. nt + xr_tiles - 1 of the column storage,
+// factored along on s_main, off the critical path: once SP p's columns are final (P(p)),
+// its extra-row tiles get the column-by-column substitution (the earlier columns of the SP
+// applied first, K = 128), then SP p is applied to every later column (K = 128 W).
+// Identity rows (gradient): only rows E <= c of column c are nonzero (Y = L^{-T} is upper
+// triangular), so each step touches rows [0, c] / [0, end of SP); tiles below Y's diagonal
+// stay exactly zero and are never written. Cross-covariance rows (posterior): all rows.
+void extra_rows_step(gaplac_ctx* ctx, hipStream_t sm, int64_t lda, int nt, int p) {
     const int W = ctx->spw;
+    const bool tri = ctx->xr_mode == 1;
+    const int mt = ctx->xr_tiles;
     const int c0 = W * p, c1 = std::min(W * p + W, nt);
     for (int c = c0; c < c1; ++c) {
         double* Acol = ctx->A + (int64_t)c * NB * lda;
         if (c > c0) {
-            BulkArgs ba{ctx->A, lda, Panel{Acol - NB * lda, lda, 0}, nullptr, c * (c1 - c), NB, nt, c,
+            const int rows = tri ? c : mt;
+            BulkArgs ba{ctx->A, lda, Panel{Acol - NB * lda, lda, 0}, nullptr, rows * (c1 - c), NB, nt, c,
                         ColMap{1, 0, W}};
-            ba.rect_rows = c;
+            ba.rect_rows = rows;
             launch_bulk(sm, ba, slot(ctx, 7, 0));
         }
-        launch_trsm_rows(sm, Acol, lda, c, nt, c + 1, ctx->Dinv + (size_t)c * DINV_PER_BLOCK, slot(ctx, 7, 0));
+        launch_trsm_rows(sm, Acol, lda, c, nt, tri ? c + 1 : mt, ctx->Dinv + (size_t)c * DINV_PER_BLOCK,
+                         slot(ctx, 7, 0));
     }
     if (c1 < nt) {
-        BulkArgs ba{ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nullptr, c1 * (nt - c1),
+        const int rows = tri ? c1 : mt;
+        BulkArgs ba{ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nullptr, rows * (nt - c1),
                     (c1 - c0) * NB, nt, c1, ColMap{1, 0, W}};
-        ba.rect_rows = c1;
+        ba.rect_rows = rows;
         launch_bulk(sm, ba, slot(ctx, 7, 0));
     }
 }
@@ -414,7 +429,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             }
         }
         HIPCK(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
-        if (ctx->grad_rows) identity_rows_step(ctx, sm, lda, nt, p);
+        if (ctx->xr_mode) extra_rows_step(ctx, sm, lda, nt, p);
     }
     launch_reduce(sm, ctx->A, lda, N, (int64_t)nt * NB, ColMap{1, 0, 1}, ctx->dres);
     HIPCK(ctx, hipGetLastError());
@@ -442,23 +457,30 @@ int ensure_tile_lists(gaplac_ctx* ctx, int nt) {
 // reduction, result copy to the pinned host record. Inputs: ctx->dX (ld N), ctx->dv,
 // ctx->dtp.
 int enqueue_eval(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt) {
-    const int64_t lda = ctx->grad_rows ? 2 * Np : Np;
+    const int64_t lda = Np + (int64_t)NB * ctx->xr_tiles;
     launch_init_result(ctx->s_main, ctx->dres);
     if (ctx->recording) launch_kt_reset(ctx->s_main, ctx->dkt, (int)ctx->kt_cap);
     // Gram in two launches: the first super-panel's tile columns, then the rest (the panel
     // chain starts on the first part while the second is still being written).
     const double bytes = 8.0 * (double)Np * (double)(Np + 1) / 2.0 + 8.0 * (double)N * (D + 1);
-    const double frac = nt > 0 ? 1.0 - (double)(nt - ctx->spw) * (nt - ctx->spw + 1) / ((double)nt * (nt + 1)) : 1.0;
+    const int rest = std::max(0, nt - ctx->spw);  // tile columns of the second Gram launch
+    const double frac = nt > 0 ? 1.0 - (double)rest * (rest + 1) / ((double)nt * (nt + 1)) : 1.0;
     launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 1, ctx->spw,
                 slot(ctx, 1, bytes * frac));
     HIPCK(ctx, hipEventRecord(ctx->ev_gram, ctx->s_main));
     launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 2, ctx->spw,
                 slot(ctx, 1, bytes * (1.0 - frac)));
     HIPCK(ctx, hipEventRecord(ctx->ev_gram2, ctx->s_main));
-    if (ctx->grad_rows) launch_init_identity_rows(ctx->s_main, ctx->A, lda, Np, nt, ctx->spw);
+    if (ctx->xr_mode == 1) launch_init_identity_rows(ctx->s_main, ctx->A, lda, Np, nt, ctx->spw);
+    if (ctx->xr_mode == 2)
+        launch_cross_gram(ctx->s_main, ctx->A, lda, Np, nt, N, ctx->xr_M, ctx->xr_tiles, ctx->dX, N, ctx->dXs,
+                          ctx->xr_M, ctx->dtp);
     int rc;
     if ((rc = factor_and_reduce(ctx, N, lda, nt))) return rc;
-    if (ctx->grad_rows) {
+    if (ctx->xr_mode == 2)
+        launch_posterior(ctx->s_main, ctx->A, lda, Np, N, ctx->xr_M, ctx->dXs, ctx->xr_M, ctx->dtp, ctx->gpart,
+                         ctx->pmean, ctx->pvar);
+    if (ctx->xr_mode == 1) {
         // alpha = Y z, then M = -C^{-1} over the factor storage, contraction, reduction
         hipStream_t sm = ctx->s_main;
         launch_zero_tail_cols(sm, ctx->A, lda, Np, N);
@@ -508,8 +530,22 @@ int ensure_workspace(gaplac_ctx* ctx, int64_t N) {
     const int nt = (int)(Np / NB);
     int rc;
     HIPCK(ctx, hipSetDevice(ctx->device));
-    if ((rc = ensure(ctx, &ctx->A, &ctx->A_elems, (size_t)(ctx->grad_rows ? 2 : 1) * Np * Np))) return rc;
-    if (ctx->grad_rows) {
+    if ((rc = ensure(ctx, &ctx->A, &ctx->A_elems, (size_t)(Np + (int64_t)NB * ctx->xr_tiles) * Np))) return rc;
+    if (ctx->xr_mode == 2) {
+        const size_t M = (size_t)ctx->xr_M;
+        if ((rc = ensure(ctx, &ctx->gpart, &ctx->gpart_elems, 2 * M * (size_t)((N + 511) / 512)))) return rc;
+        if (ctx->pmv_elems < M) {
+            if (ctx->pmean) (void)hipFree(ctx->pmean);
+            if (ctx->pvar) (void)hipFree(ctx->pvar);
+            ctx->pmean = ctx->pvar = nullptr;
+            ctx->pmv_elems = 0;
+            if (hipMalloc(reinterpret_cast<void**>(&ctx->pmean), M * 8) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void**>(&ctx->pvar), M * 8) != hipSuccess)
+                return set_err(ctx, GAPLAC_E_OOM, "hipMalloc of posterior outputs failed");
+            ctx->pmv_elems = M;
+        }
+    }
+    if (ctx->xr_mode == 1) {
         const int m = (int)((N + NB - 1) / NB);
         const size_t nk = (size_t)((N + 511) / 512);
         const size_t part = std::max(nk * (size_t)N, (size_t)m * (m + 1) / 2 * (GAPLAC_MAX_TERMS + 1));
@@ -566,7 +602,7 @@ int eval_device(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp, EvalR
     }
     *ctx->htp = tp;
     HIPCK(ctx, hipMemcpyAsync(ctx->dtp, ctx->htp, sizeof(TermPack), hipMemcpyHostToDevice, ctx->s_main));
-    if (ctx->use_graph && !ctx->serial && ctx->prof_mode != 2 && !ctx->grad_rows) {
+    if (ctx->use_graph && !ctx->serial && ctx->prof_mode != 2 && !ctx->xr_mode) {
         hipGraph_t& G = prof ? ctx->pgraph : ctx->graph;
         hipGraphExec_t& GX = prof ? ctx->pgexec : ctx->gexec;
         int64_t& GN = prof ? ctx->pgN : ctx->gN;
@@ -694,10 +730,12 @@ int logpdf_grad_impl(gaplac_ctx* ctx, bool on_device, int64_t N, int32_t D, cons
     tp.noise = noise;
     *ctx->hgp = gp;
     HIPCK(ctx, hipMemcpyAsync(ctx->dgp, ctx->hgp, sizeof(GradTermPack), hipMemcpyHostToDevice, ctx->s_main));
-    ctx->grad_rows = true;
+    ctx->xr_mode = 1;
+    ctx->xr_tiles = (int)(round_up(N + 1, NB) / NB);
     EvalResult r;
     rc = eval_device(ctx, N, D, tp, &r);
-    ctx->grad_rows = false;
+    ctx->xr_mode = 0;
+    ctx->xr_tiles = 0;
     if (rc) return rc;
     rc = finish(r, out_logpdf, nullptr, nullptr);
     if (rc) return rc;  // PosDefException: gradients stay NaN
@@ -705,6 +743,63 @@ int logpdf_grad_impl(gaplac_ctx* ctx, bool on_device, int64_t N, int32_t D, cons
     if (out_dparam)
         for (int t = 0; t < T; ++t) out_dparam[t] = ctx->hgout[t];
     if (out_dnoise) *out_dnoise = ctx->hgout[T];
+    return 0;
+}
+
+// Shared body of gaplac_posterior_mean_var.
+int posterior_impl(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx, int32_t T,
+                   const gaplac_term* terms, double noise, const double* y, int64_t M, const double* Xs,
+                   int64_t ldxs, double* out_mean, double* out_var) {
+    for (int64_t j = 0; j < M; ++j) {
+        if (out_mean) out_mean[j] = NAN;
+        if (out_var) out_var[j] = NAN;
+    }
+    int rc = check_common(ctx, N, D, X, ldx, noise, y);
+    if (rc) return rc;
+    if (M < 0 || (M > 0 && D > 0 && (!Xs || ldxs < M)))
+        return set_err(ctx, GAPLAC_E_ARG, "M < 0, or Xs NULL / ldxs < M");
+    TermPack tp;
+    if ((rc = pack_terms(ctx, D, T, terms, &tp))) return rc;
+    if (M == 0) return 0;
+    HIPCK(ctx, hipSetDevice(ctx->device));
+    if (N == 0) {  // posterior of an empty FiniteGP = the prior: mean 0, var kdiag
+        for (int64_t j = 0; j < M; ++j) {
+            double kd = 0.0, pr = 1.0;
+            for (int t = 0; t < T; ++t) {
+                const double x = tp.kind[t] == GAPLAC_NOISE ? 0.0 : Xs[(int64_t)tp.col[t] * ldxs + j];
+                double k = 1.0;
+                if (tp.kind[t] == GAPLAC_LINEAR) k = x * x + tp.p[t];
+                if (tp.kind[t] == GAPLAC_NOISE) k = tp.p[t];
+                pr *= k;
+                if (tp.last_in_group[t]) {
+                    kd += pr;
+                    pr = 1.0;
+                }
+            }
+            if (out_mean) out_mean[j] = 0.0;
+            if (out_var) out_var[j] = kd;
+        }
+        return 0;
+    }
+    if ((rc = upload(ctx, N, D, X, ldx, y))) return rc;
+    const size_t nxs = (size_t)M * (size_t)(D > 0 ? D : 1);
+    if ((rc = ensure(ctx, &ctx->dXs, &ctx->dXs_elems, nxs))) return rc;
+    if (D > 0)
+        HIPCK(ctx, hipMemcpy2DAsync(ctx->dXs, (size_t)M * 8, Xs, (size_t)ldxs * 8, (size_t)M * 8, (size_t)D,
+                                    hipMemcpyHostToDevice, ctx->s_main));
+    tp.noise = noise;
+    ctx->xr_mode = 2;
+    ctx->xr_tiles = (int)((M + NB - 1) / NB);
+    ctx->xr_M = M;
+    EvalResult r;
+    rc = eval_device(ctx, N, D, tp, &r);
+    ctx->xr_mode = 0;
+    ctx->xr_tiles = 0;
+    if (rc) return rc;
+    rc = finish(r, nullptr, nullptr, nullptr);
+    if (rc) return rc;
+    if (out_mean) HIPCK(ctx, hipMemcpy(out_mean, ctx->pmean, (size_t)M * 8, hipMemcpyDeviceToHost));
+    if (out_var) HIPCK(ctx, hipMemcpy(out_var, ctx->pvar, (size_t)M * 8, hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -828,6 +923,9 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     if (ctx->dkt) (void)hipFree(ctx->dkt);
     if (ctx->hkt) (void)hipHostFree(ctx->hkt);
     if (ctx->galpha) (void)hipFree(ctx->galpha);
+    if (ctx->dXs) (void)hipFree(ctx->dXs);
+    if (ctx->pmean) (void)hipFree(ctx->pmean);
+    if (ctx->pvar) (void)hipFree(ctx->pvar);
     if (ctx->gdv) (void)hipFree(ctx->gdv);
     if (ctx->gpart) (void)hipFree(ctx->gpart);
     if (ctx->gout) (void)hipFree(ctx->gout);
@@ -1020,6 +1118,39 @@ int gaplac_logpdf_grad_device(gaplac_ctx* ctx, int64_t N, int32_t D, const doubl
                               double* out_dv, double* out_dparam, double* out_dnoise) {
     return logpdf_grad_impl(ctx, true, N, D, dX, ldx, T, terms, noise, dv, out_logpdf, out_dv, out_dparam,
                             out_dnoise);
+}
+
+int gaplac_posterior_mean_var(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx, int32_t T,
+                              const gaplac_term* terms, double noise, const double* y, int64_t M,
+                              const double* Xs, int64_t ldxs, double* out_mean, double* out_var) {
+    return posterior_impl(ctx, N, D, X, ldx, T, terms, noise, y, M, Xs, ldxs, out_mean, out_var);
+}
+
+int gaplac_rand(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx, int32_t T,
+                const gaplac_term* terms, double noise, const double* z, double* out) {
+    if (out)
+        for (int64_t i = 0; i < N; ++i) out[i] = NAN;
+    int rc = check_common(ctx, N, D, X, ldx, noise, z);
+    if (rc) return rc;
+    if (N > 0 && !out) return set_err(ctx, GAPLAC_E_ARG, "out is NULL");
+    TermPack tp;
+    if ((rc = pack_terms(ctx, D, T, terms, &tp))) return rc;
+    if (N == 0) return 0;
+    HIPCK(ctx, hipSetDevice(ctx->device));
+    if ((rc = upload(ctx, N, D, X, ldx, z))) return rc;  // z also rides in the v row (unused)
+    tp.noise = noise;
+    EvalResult r;
+    if ((rc = eval_device(ctx, N, D, tp, &r))) return rc;
+    if ((rc = finish(r, nullptr, nullptr, nullptr))) return rc;
+    const size_t nk = (size_t)((N + 511) / 512);
+    if ((rc = ensure(ctx, &ctx->gpart, &ctx->gpart_elems, nk * (size_t)N))) return rc;
+    if ((rc = ensure(ctx, &ctx->gdv, &ctx->gdv_elems, (size_t)N))) return rc;
+    const int64_t Np = round_up(N + 1, NB);
+    launch_lower_mv(ctx->s_main, ctx->A, Np, N, ctx->dv, ctx->gpart, ctx->gdv);
+    HIPCK(ctx, hipGetLastError());
+    HIPCK(ctx, hipMemcpyAsync(out, ctx->gdv, (size_t)N * 8, hipMemcpyDeviceToHost, ctx->s_main));
+    HIPCK(ctx, hipStreamSynchronize(ctx->s_main));
+    return 0;
 }
 
 int gaplac_set_profiling(gaplac_ctx* ctx, int mode) {

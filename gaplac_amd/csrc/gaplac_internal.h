@@ -145,6 +145,19 @@ void launch_cinv_tiles(hipStream_t s, double* A, int64_t lda, int64_t Np, const 
 void launch_grad_contract(hipStream_t s, const double* A, int64_t lda, int64_t N, const double* X, int64_t ldx,
                           const double* alpha, const TermPack* dtp, const GradTermPack* dgp, double* partial,
                           KTime* kt);
+// ---- posterior mean / variance ----
+// Extra rows Np .. Np + 128 mt - 1 (lda = Np + 128 mt) = K(xs, X): mt x nt tiles, zero
+// outside test point j < M and training point i < N.
+void launch_cross_gram(hipStream_t s, double* A, int64_t lda, int64_t Np, int nt, int64_t N, int64_t M, int mt,
+                       const double* X, int64_t ldx, const double* Xs, int64_t ldxs, const TermPack* dtp);
+// After the factorisation: mean_j = sum_k V^T[j,k] z_k, var_j = kdiag(xs_j) - sum_k V^T[j,k]^2
+// (partial: 2 * ceil(N/512) * M doubles).
+void launch_posterior(hipStream_t s, const double* A, int64_t lda, int64_t Np, int64_t N, int64_t M,
+                      const double* Xs, int64_t ldxs, const TermPack* dtp, double* partial, double* mean,
+                      double* var);
+// ---- rand(FiniteGP): out = L z over the factor's lower triangle (partial: ceil(N/512) * N) ----
+void launch_lower_mv(hipStream_t s, const double* A, int64_t lda, int64_t N, const double* z, double* partial,
+                     double* out);
 // dparam[t] = 0.5 * sum over tiles (fixed order), t = 0..T (T = observation variance).
 void launch_grad_reduce(hipStream_t s, const double* partial, int ntiles, int T, double* out);
 // Workgroup -> tile list for launch_grad_tiles over the m x m triangle (XCD-balanced).

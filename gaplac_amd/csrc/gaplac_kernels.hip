@@ -1147,6 +1147,166 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(const double* __restri
     if (tid == 0) out[t] = 0.5 * s[0];
 }
 
+// ---------------------------------------------------------------------------------
+// Posterior mean / variance at test points (AbstractGPs
+// mean_and_var(posterior(fx, y), xs)): the rows below the matrix hold K(xs, X) (one row per
+// test point); factoring them along leaves V^T = K(xs, X) L^{-T} there, so
+//   mean_j = sum_k V^T[j,k] z_k          (= K(xs, X) C^{-1} y, z = L^{-1} y in row N)
+//   var_j  = k(xs_j, xs_j) - sum_k V^T[j,k]^2
+// ---------------------------------------------------------------------------------
+
+// Cross-covariance rows: tile (E, J) of the extra rows = K(xs rows E NB.., X columns J NB..),
+// no noise (the posterior's cross-covariance is the latent kernel); 0 outside j < M, i < N.
+__global__ __launch_bounds__(256) void cross_gram_kernel(double* __restrict__ A, int64_t lda, int64_t Np,
+                                                         int64_t N, int64_t M, const double* __restrict__ X,
+                                                         int64_t ldx, const double* __restrict__ Xs,
+                                                         int64_t ldxs, const TermPack* __restrict__ tpp) {
+    __shared__ double xcol[GAPLAC_MAX_TERMS][NB];
+    const TermPack& tp = *tpp;
+    const int T = tp.T;
+    const int J = (int)blockIdx.x, E = (int)blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t c0 = (int64_t)J * NB;
+    for (int idx = tid; idx < T * NB; idx += 256) {
+        const int t = idx / NB, c = idx % NB;
+        xcol[t][c] = (c0 + c < N && tp.kind[t] != GAPLAC_NOISE) ? X[(int64_t)tp.col[t] * ldx + c0 + c] : 0.0;
+    }
+    const int64_t j0 = (int64_t)E * NB + 2 * lane;  // test points j0, j0 + 1
+    double xa[GAPLAC_MAX_TERMS], xb[GAPLAC_MAX_TERMS];
+#pragma unroll
+    for (int t = 0; t < GAPLAC_MAX_TERMS; ++t) {
+        xa[t] = 0.0;
+        xb[t] = 0.0;
+        if (t < T && tp.kind[t] != GAPLAC_NOISE) {
+            const double* xc = Xs + (int64_t)tp.col[t] * ldxs;
+            if (j0 < M) xa[t] = xc[j0];
+            if (j0 + 1 < M) xb[t] = xc[j0 + 1];
+        }
+    }
+    __syncthreads();
+    double* base = A + c0 * lda + Np + j0;
+    for (int cc = w; cc < NB; cc += 4) {
+        double tot0 = 0.0, tot1 = 0.0, pr0 = 1.0, pr1 = 1.0;
+#pragma unroll
+        for (int t = 0; t < GAPLAC_MAX_TERMS; ++t) {
+            if (t < T) {
+                const int kind = tp.kind[t];
+                const double p = tp.p[t], xj = xcol[t][cc];
+                // an index-noise term couples a point only with itself: 0 across point sets
+                pr0 *= kind == GAPLAC_NOISE ? 0.0 : term_k(kind, p, xa[t], xj, false);
+                pr1 *= kind == GAPLAC_NOISE ? 0.0 : term_k(kind, p, xb[t], xj, false);
+                if (tp.last_in_group[t]) {
+                    tot0 += pr0;
+                    tot1 += pr1;
+                    pr0 = 1.0;
+                    pr1 = 1.0;
+                }
+            }
+        }
+        const bool colok = c0 + cc < N;
+        const double o0 = (colok && j0 < M) ? tot0 : 0.0, o1 = (colok && j0 + 1 < M) ? tot1 : 0.0;
+        *reinterpret_cast<double2*>(base + (int64_t)cc * lda) = make_double2(o0, o1);
+    }
+}
+
+// Partial sums over 512-column chunks of the extra rows: pm = V^T z, pv = |V^T|^2.
+__global__ __launch_bounds__(256) void post_partial_kernel(const double* __restrict__ A, int64_t lda, int64_t Np,
+                                                           int64_t N, int64_t M, double* __restrict__ pm,
+                                                           double* __restrict__ pv) {
+    __shared__ double zs[512];
+    const int tid = threadIdx.x;
+    const int64_t k0 = (int64_t)blockIdx.y * 512;
+    const int64_t j = (int64_t)blockIdx.x * 256 + tid;
+    for (int t = tid; t < 512; t += 256) zs[t] = (k0 + t < N) ? A[(k0 + t) * lda + N] : 0.0;
+    __syncthreads();
+    double m0 = 0.0, m1 = 0.0, v0 = 0.0, v1 = 0.0;
+    if (j < M) {
+        const double* y = A + k0 * lda + Np + j;
+        const int kn = (int)((N - k0) < 512 ? (N - k0) : 512);
+        int kk = 0;
+        for (; kk + 2 <= kn; kk += 2) {
+            const double a = y[(int64_t)kk * lda], b = y[(int64_t)(kk + 1) * lda];
+            m0 += a * zs[kk];
+            m1 += b * zs[kk + 1];
+            v0 += a * a;
+            v1 += b * b;
+        }
+        for (; kk < kn; ++kk) {
+            const double a = y[(int64_t)kk * lda];
+            m0 += a * zs[kk];
+            v0 += a * a;
+        }
+        pm[(int64_t)blockIdx.y * M + j] = m0 + m1;
+        pv[(int64_t)blockIdx.y * M + j] = v0 + v1;
+    }
+}
+
+// mean_j, var_j = kdiag(xs_j) - sum of the partials (fixed order).
+__global__ __launch_bounds__(256) void post_finish_kernel(const double* __restrict__ pm,
+                                                          const double* __restrict__ pv, int64_t M, int nk,
+                                                          const double* __restrict__ Xs, int64_t ldxs,
+                                                          const TermPack* __restrict__ tpp,
+                                                          double* __restrict__ mean, double* __restrict__ var) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= M) return;
+    const TermPack& tp = *tpp;
+    double kd = 0.0, pr = 1.0;
+    for (int t = 0; t < tp.T; ++t) {
+        const int kind = tp.kind[t];
+        const double x = kind == GAPLAC_NOISE ? 0.0 : Xs[(int64_t)tp.col[t] * ldxs + j];
+        pr *= term_k(kind, tp.p[t], x, x, true);
+        if (tp.last_in_group[t]) {
+            kd += pr;
+            pr = 1.0;
+        }
+    }
+    double m = 0.0, v = 0.0;
+    for (int y = 0; y < nk; ++y) {
+        m += pm[(int64_t)y * M + j];
+        v += pv[(int64_t)y * M + j];
+    }
+    mean[j] = m;
+    var[j] = kd - v;
+}
+
+// ---------------------------------------------------------------------------------
+// rand(FiniteGP) (AbstractGPs: m + cholesky(C).U' * randn): out = L z
+// over the factor's lower triangle (k <= i: the diagonal tiles' upper parts hold junk).
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void lower_mv_partial_kernel(const double* __restrict__ A, int64_t lda,
+                                                               int64_t N, const double* __restrict__ z,
+                                                               double* __restrict__ partial) {
+    __shared__ double zs[512];
+    const int tid = threadIdx.x;
+    const int64_t k0 = (int64_t)blockIdx.y * 512;
+    const int64_t i = (int64_t)blockIdx.x * 256 + tid;
+    for (int t = tid; t < 512; t += 256) zs[t] = (k0 + t < N) ? z[k0 + t] : 0.0;
+    __syncthreads();
+    if (i >= N) return;
+    double s0 = 0.0, s1 = 0.0;
+    if (k0 <= i) {
+        const double* l = A + k0 * lda + i;
+        const int64_t kmax = i + 1 - k0;  // k <= i
+        const int kn = (int)(kmax < 512 ? kmax : 512);
+        int kk = 0;
+        for (; kk + 2 <= kn; kk += 2) {
+            s0 += l[(int64_t)kk * lda] * zs[kk];
+            s1 += l[(int64_t)(kk + 1) * lda] * zs[kk + 1];
+        }
+        for (; kk < kn; ++kk) s0 += l[(int64_t)kk * lda] * zs[kk];
+    }
+    partial[(int64_t)blockIdx.y * N + i] = s0 + s1;
+}
+
+__global__ __launch_bounds__(256) void lower_mv_reduce_kernel(const double* __restrict__ partial, int64_t N, int nk,
+                                                              double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    double a = 0.0;
+    for (int y = 0; y < nk; ++y) a += partial[(int64_t)y * N + i];
+    out[i] = a;
+}
+
 // ------------------------------- launchers ---------------------------------------
 void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const double* X,
                  int64_t ldx, const double* v, const TermPack* dtp, int part, int w, KTime* kt) {
@@ -1157,8 +1317,8 @@ void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const
         for (int c = 0; c < w; ++c) ntiles += nt - c;
     } else {
         if (part == 0) w = 0;
-        const int64_t m = nt - w;
-        ntiles = m * (m + 1) / 2;
+        const int64_t m = nt - w;  // part 2 with nt <= w: nothing left (m <= 0)
+        ntiles = m > 0 ? m * (m + 1) / 2 : 0;
     }
     if (ntiles <= 0) return;
     gram_kernel<<<dim3((unsigned)ntiles), dim3(256), 0, s>>>(A, lda, N, X, ldx, v, dtp, nt, part, w, kt);
@@ -1281,6 +1441,34 @@ void build_grad_list(int m, std::vector<uint32_t>& out) {
     out.assign(8 * len, 0xffffffffu);
     for (size_t x = 0; x < 8; ++x)
         for (size_t k = 0; k < seq[x].size(); ++k) out[8 * k + x] = seq[x][k];
+}
+
+void launch_cross_gram(hipStream_t s, double* A, int64_t lda, int64_t Np, int nt, int64_t N, int64_t M, int mt,
+                       const double* X, int64_t ldx, const double* Xs, int64_t ldxs, const TermPack* dtp) {
+    if (nt <= 0 || mt <= 0) return;
+    cross_gram_kernel<<<dim3((unsigned)nt, (unsigned)mt), dim3(256), 0, s>>>(A, lda, Np, N, M, X, ldx, Xs, ldxs, dtp);
+}
+
+void launch_posterior(hipStream_t s, const double* A, int64_t lda, int64_t Np, int64_t N, int64_t M,
+                      const double* Xs, int64_t ldxs, const TermPack* dtp, double* partial, double* mean,
+                      double* var) {
+    if (M <= 0) return;
+    const int nk = (int)((N + 511) / 512);
+    double* pm = partial;
+    double* pv = partial + (size_t)nk * M;
+    post_partial_kernel<<<dim3((unsigned)((M + 255) / 256), (unsigned)nk), dim3(256), 0, s>>>(A, lda, Np, N, M, pm,
+                                                                                            pv);
+    post_finish_kernel<<<dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s>>>(pm, pv, M, nk, Xs, ldxs, dtp, mean,
+                                                                             var);
+}
+
+void launch_lower_mv(hipStream_t s, const double* A, int64_t lda, int64_t N, const double* z, double* partial,
+                     double* out) {
+    if (N <= 0) return;
+    const int nk = (int)((N + 511) / 512);
+    lower_mv_partial_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nk), dim3(256), 0, s>>>(A, lda, N, z,
+                                                                                                partial);
+    lower_mv_reduce_kernel<<<dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s>>>(partial, N, nk, out);
 }
 
 void launch_init_result(hipStream_t s, EvalResult* res) {

@@ -137,6 +137,26 @@ int gaplac_logpdf_grad_device(gaplac_ctx* ctx, int64_t N, int32_t D, const doubl
                               int32_t T, const gaplac_term* terms, double noise, const double* dv,
                               double* out_logpdf, double* out_dv, double* out_dparam, double* out_dnoise);
 
+/* Posterior mean and variance at M test points:
+ *     mean_j = k(xs_j, X) C^{-1} y,   var_j = k(xs_j, xs_j) - k(xs_j, X) C^{-1} k(X, xs_j)
+ * with C = K(X) + noise I (the FiniteGP's covariance) and the latent kernel k (no noise) for
+ * the test points. Xs is M x D column-major (leading dimension ldxs) with the same columns as
+ * X. Replaces: mean_and_var(posterior(FiniteGP(GP(k), X, noise), y), xs) of AbstractGPs
+ * 0.5.12, reached from src/plotting.jl:8-12 (and posterior(pr, y) in CLI/src/select.jl:51-52).
+ * Same return convention as gaplac_logpdf (PosDefException info > 0; outputs NaN). */
+int gaplac_posterior_mean_var(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx,
+                              int32_t T, const gaplac_term* terms, double noise, const double* y,
+                              int64_t M, const double* Xs, int64_t ldxs,
+                              double* out_mean, double* out_var);
+
+/* One draw of the FiniteGP: out = L z with C = K(X) + noise I = L L^T
+ * and z the N standard-normal values the caller drew (the host keeps the RNG stream, so a
+ * given z gives the same sample as the reference). Replaces: rand(rng, FiniteGP(GP(k), X,
+ * noise)) = mean + cholesky(C).U' * randn(rng, N) (zero mean), reached from
+ * CLI/src/sample.jl:25. */
+int gaplac_rand(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx,
+                int32_t T, const gaplac_term* terms, double noise, const double* z, double* out);
+
 /* Debug / parity entries (tests only; not on the timed path). */
 /* Gram matrix sum_t K_t(X) + noise*I as a dense N×N column-major host matrix
  * (replaces KernelFunctions.kernelmatrix + Diagonal(Fill(noise, N))). */

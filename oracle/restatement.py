@@ -275,3 +275,92 @@ def logpdf_grad_potri(X, terms, noise: float, v):
         dparam[t] = 0.5 * float(np.vdot(W, dK))
         del dK
     return float(lp), -alpha, dparam, 0.5 * float(np.trace(W))
+
+
+# ---------------------------------------------------------------------------------------
+# Posterior mean / variance and rand (rank 3), AbstractGPs 0.5.12:
+#   posterior(fx, y): C = cov(fx) (K + noise I), alpha = C^-1 (y - 0)
+#   mean_and_var(post, xs): m = K(xs, X) alpha,
+#                           v = kernelmatrix_diag(k, xs) - colsum((U' \ K(X, xs)).^2)
+#     (diag_Xt_invA_X(C::Cholesky, X) = sum(abs2, C.U' \ X; dims=1)); reached from
+#     src/plotting.jl:8-12 and CLI/src/select.jl:51-52.
+#   rand(rng, fx) = mean(fx) + cholesky(C).U' * randn(rng, N), CLI/src/sample.jl:25.
+# The index-noise extension couples a point with itself only: 0 across point sets, its
+# variance on kernelmatrix_diag.
+# ---------------------------------------------------------------------------------------
+def cross_term_matrix(Xa: np.ndarray, Xb: np.ndarray, kind: int, col: int, param: float) -> np.ndarray:
+    """K_t(Xa rows, Xb rows) for one term (len(Xa) x len(Xb))."""
+    if kind == NOISE:
+        return np.zeros((Xa.shape[0], Xb.shape[0]))
+    a = np.ascontiguousarray(Xa[:, col], dtype=np.float64)
+    b = np.ascontiguousarray(Xb[:, col], dtype=np.float64)
+    if kind in (SQEXP, OU):
+        s = 1.0 / param
+        d = (s * a)[:, None] - (s * b)[None, :]
+        return np.exp(-(d * d) * 0.5) if kind == SQEXP else np.exp(-np.abs(d))
+    if kind == LINEAR:
+        return np.outer(a, b) + param
+    if kind == CAT:
+        return (a[:, None] == b[None, :]).astype(np.float64)
+    raise ValueError(f"unknown term kind {kind}")
+
+
+def cross_gram(Xa, Xb, terms) -> np.ndarray:
+    total = np.zeros((Xa.shape[0], Xb.shape[0]))
+    prod = None
+    terms = list(terms)
+    for t, (kind, col, param, group) in enumerate(terms):
+        K = cross_term_matrix(Xa, Xb, kind, col, param)
+        prod = K if prod is None else prod * K
+        if t == len(terms) - 1 or terms[t + 1][3] != group:
+            total = total + prod
+            prod = None
+    return total
+
+
+def kernel_diag(Xs, terms) -> np.ndarray:
+    """kernelmatrix_diag(k, xs) (no observation noise)."""
+    M = Xs.shape[0]
+    total = np.zeros(M)
+    prod = None
+    terms = list(terms)
+    for t, (kind, col, param, group) in enumerate(terms):
+        if kind == NOISE:
+            K = np.full(M, float(param))
+        elif kind == LINEAR:
+            x = Xs[:, col]
+            K = x * x + param
+        else:
+            K = np.ones(M)
+        prod = K if prod is None else prod * K
+        if t == len(terms) - 1 or terms[t + 1][3] != group:
+            total = total + prod
+            prod = None
+    return total
+
+
+def posterior_mean_var(X, terms, noise: float, y, Xs):
+    X = np.asarray(X, dtype=np.float64)
+    X = X[:, None] if X.ndim == 1 else X
+    Xs = np.asarray(Xs, dtype=np.float64)
+    Xs = Xs[:, None] if Xs.ndim == 1 else Xs
+    terms = list(terms)
+    C = gram(X, terms, noise)
+    U, info = lapack.dpotrf(C, lower=0, clean=1, overwrite_a=0)
+    if info > 0:
+        raise PosDefException(int(info))
+    alpha = scipy.linalg.cho_solve((U, False), np.asarray(y, dtype=np.float64), check_finite=False)
+    Kxs = cross_gram(X, Xs, terms)  # N x M
+    mean = Kxs.T @ alpha
+    V = scipy.linalg.solve_triangular(U, Kxs, trans="T", lower=False, check_finite=False)
+    var = kernel_diag(Xs, terms) - np.sum(V * V, axis=0)
+    return mean, var
+
+
+def rand_from(X, terms, noise: float, z):
+    """cholesky(C).U' * z for a given standard-normal vector z (zero mean)."""
+    C = gram(X, terms, noise)
+    U, info = lapack.dpotrf(C, lower=0, clean=1, overwrite_a=0)
+    if info > 0:
+        raise PosDefException(int(info))
+    return U.T @ np.asarray(z, dtype=np.float64)

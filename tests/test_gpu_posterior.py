@@ -1,0 +1,132 @@
+"""Parity of gaplac_posterior_mean_var and gaplac_rand (HIP, through the C-ABI) against
+the sklearn-pinned restatements (tests/test_posterior_oracle.py).
+
+Tolerance (north_star: <= 1e-9 relative fp64): mean within 1e-9 of max |mean| (>= 1),
+variance within 1e-9 of the prior variance it is reduced from (kernel_diag, >= 1), rand
+within 1e-12 of max |sample|. At N = 16384 size-independent properties: the posterior mean
+at the training inputs equals y - noise * alpha (alpha from gaplac_logpdf_grad), and a
+sample s = L z has logpdf quad term ||L^{-1} s||^2 = ||z||^2.
+"""
+import numpy as np
+import pytest
+
+from gaplac_amd import abstractgps as AG
+from gaplac_amd import formula as F
+from gaplac_amd._native import CAT, LINEAR, NOISE, OU, SQEXP
+from gaplac_amd.backend import ArgumentError, Context, PosDefException
+from oracle import restatement as R
+from tests.conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not gpu_available():
+        pytest.skip("no GPU")
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def check(ctx, X, terms, noise, y, Xs):
+    m, v = ctx.posterior_mean_var(X, terms, noise, y, Xs)
+    rm, rv = R.posterior_mean_var(X, terms, noise, y, Xs)
+    kd = R.kernel_diag(np.asarray(Xs).reshape(len(Xs), -1), terms)
+    assert np.max(np.abs(m - rm)) <= TOL * max(1.0, np.max(np.abs(rm)))
+    assert np.all(np.abs(v - rv) <= TOL * np.maximum(1.0, np.abs(kd)))
+
+
+@pytest.mark.parametrize("N,M", [(1, 1), (5, 3), (127, 129), (128, 128), (129, 1), (300, 1000), (700, 257),
+                                 (1000, 64), (513, 513)])
+def test_sizes_composite(ctx, N, M):
+    rng = np.random.default_rng(N * 7 + M)
+    def cols(n):
+        return np.column_stack([rng.uniform(0, 10, n), rng.integers(0, 40, n).astype(float), rng.normal(size=n)])
+    X, Xs = cols(N), cols(M)
+    y = rng.normal(size=N)
+    terms = [(SQEXP, 0, 1.5, 0), (OU, 0, 3.0, 1), (CAT, 1, 0.0, 2), (LINEAR, 2, 0.5, 3)]
+    check(ctx, X, terms, 0.1, y, Xs)
+
+
+def test_product_groups_and_noise_term(ctx):
+    rng = np.random.default_rng(12)
+    N, M = 260, 190
+    X = np.column_stack([rng.uniform(0, 5, N), rng.normal(size=N)])
+    Xs = np.column_stack([rng.uniform(0, 5, M), rng.normal(size=M)])
+    terms = [(SQEXP, 0, 1.3, 0), (LINEAR, 1, 0.4, 0), (OU, 0, 2.5, 1), (NOISE, -1, 0.2, 2)]
+    check(ctx, X, terms, 0.1, rng.normal(size=N), Xs)
+
+
+def test_abstractgps_surface(ctx):
+    # src/plotting.jl:1-12: posterior(fx, y) then mean_and_var over a 100-point range
+    rng = np.random.default_rng(13)
+    N = 400
+    x = rng.uniform(-5, 5, N)
+    y = np.sin(x) + 0.3 * rng.normal(size=N)
+    spec = F.gp_spec("y ~| SqExp(:x; l=1.5)")
+    gp, vars_ = AG.make_gp(spec)
+    fx = AG.FiniteGP(gp, x, 0.1)
+    xt = np.linspace(x.min() - 1, x.max() + 1, 100)
+    m, v = AG.mean_and_var(AG.posterior(fx, y, ctx=ctx), xt)
+    rm, rv = R.posterior_mean_var(x[:, None], fx.terms, 0.1, y, xt[:, None])
+    assert np.max(np.abs(m - rm)) <= TOL * max(1.0, np.max(np.abs(rm)))
+    assert np.max(np.abs(v - rv)) <= TOL
+    with pytest.raises(ArgumentError):
+        ctx.posterior_mean_var(x, fx.terms, 0.1, y[:-1], xt)
+
+
+def test_empty_training_set_is_the_prior(ctx):
+    Xs = np.linspace(0, 1, 7)[:, None]
+    terms = [(SQEXP, 0, 1.0, 0), (LINEAR, 0, 0.5, 1)]
+    m, v = ctx.posterior_mean_var(np.zeros((0, 1)), terms, 0.1, np.zeros(0), Xs)
+    assert np.all(m == 0.0) and np.allclose(v, R.kernel_diag(Xs, terms), rtol=0, atol=1e-15)
+
+
+def test_nonpd_raises(ctx):
+    X = np.repeat(np.arange(8.0), 4)[:, None]
+    with pytest.raises(PosDefException):
+        ctx.posterior_mean_var(X, [(CAT, 0, 0.0, 0)], 0.0, np.ones(32), X[:3])
+    with pytest.raises(PosDefException):
+        ctx.rand(X, [(CAT, 0, 0.0, 0)], 0.0, np.ones(32))
+
+
+@pytest.mark.parametrize("N", [1, 2, 127, 128, 129, 511, 513, 1000])
+def test_rand_matches_oracle(ctx, N):
+    rng = np.random.default_rng(N)
+    X = np.column_stack([rng.uniform(-5, 5, N), rng.integers(0, 9, N).astype(float)])
+    terms = [(SQEXP, 0, 1.2, 0), (CAT, 1, 0.0, 1)]
+    z = rng.normal(size=N)
+    s = ctx.rand(X, terms, 0.1, z)
+    r = R.rand_from(X, terms, 0.1, z)
+    assert np.max(np.abs(s - r)) <= 1e-12 * max(1.0, np.max(np.abs(r)))
+
+
+def test_rand_surface_draws_on_host(ctx):
+    spec = F.gp_spec("y :~| SqExp(:x; l=1)")
+    gp, _ = AG.make_gp(spec)
+    x = np.arange(-5, 5.0001, 0.1)
+    fx = AG.FiniteGP(gp, x, 0.1)
+    a = AG.rand(fx, rng=np.random.default_rng(1), ctx=ctx)
+    b = AG.rand(fx, z=np.random.default_rng(1).standard_normal(len(x)), ctx=ctx)
+    assert np.array_equal(a, b) and a.shape == x.shape
+
+
+def test_large_n_properties(ctx):
+    N = 16384
+    rng = np.random.default_rng(2)
+    t = rng.uniform(0, 10, N)
+    g = rng.integers(0, N // 3, N).astype(float)
+    X = np.column_stack([t, g])
+    y = rng.normal(size=N)
+    terms = [(SQEXP, 0, 1.5, 0), (OU, 0, 3.0, 1), (CAT, 1, 0.0, 2)]
+    idx = rng.choice(N, 600, replace=False)
+    m, v = ctx.posterior_mean_var(X, terms, 0.1, y, X[idx])
+    _, dv, _, _ = ctx.logpdf_grad(X, terms, 0.1, y)   # dv = -alpha
+    assert np.max(np.abs(m - (y[idx] + 0.1 * dv[idx]))) <= 1e-8 * max(1.0, np.max(np.abs(y)))
+    assert np.all(v > 0) and np.all(v < 3.0)
+    z = rng.normal(size=N)
+    s = ctx.rand(X, terms, 0.1, z)
+    _, _, q = ctx.logpdf(X, terms, 0.1, s, full=True)
+    assert abs(q - float(z @ z)) <= 1e-9 * float(z @ z)
