@@ -50,6 +50,14 @@ def terms_for(l_sqexp: float):
     return [(SQEXP, 0, l_sqexp, 0), (OU, 0, 3.0, 1), (CAT, 1, 0.0, 2), (NOISE, -1, 1.0, 3)]
 
 
+def _blas_threads() -> int:
+    try:
+        from threadpoolctl import threadpool_info
+        return max((d.get("num_threads", 1) for d in threadpool_info() if d.get("user_api") == "blas"), default=1)
+    except Exception:
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(N: int, budget_s: float = 25.0):
     """Time the oracle (numpy Gram + scipy/OpenBLAS dpotrf + dtrsv) on the host cores."""
     from oracle import restatement as R
@@ -115,12 +123,15 @@ def main():
     ap.add_argument("--skip-cpu", action="store_true", help="skip the CPU baseline leg (profiling runs)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event pass")
     ap.add_argument("--profile-steps", type=int, default=2, help="eager steps timed per kernel after the timed region")
-    ap.add_argument("--mode", choices=("replicas", "dist", "single", "select", "grad"), default="replicas",
+    ap.add_argument("--mode", choices=("replicas", "dist", "single", "select", "grad", "posterior", "rand"),
+                    default="replicas",
                     help="replicas (default, the headline metric): independent evals per GPU; dist: one "
                          "evaluation spread over all ranks (BASELINE configs[3], N=65536); single: the "
                          "single-GPU path at --n (comparison line for dist); select: BASELINE configs[4], "
                          "64 candidate formulas x N=8192 through gaplac_logpdf_batch, sharded over ranks; "
-                         "grad: logpdf + gradient (gaplac_logpdf_grad, the mcmc/NUTS step) on the configs[2] workload")
+                         "grad: logpdf + gradient (gaplac_logpdf_grad, the mcmc/NUTS step) on the configs[2] workload; "
+                         "posterior: mean_and_var(posterior(fx, y), xs) at --m test points; rand: one FiniteGP draw")
+    ap.add_argument("--m", type=int, default=1024, help="posterior mode: test points")
     ap.add_argument("--loopback", type=int, default=0,
                     help="dist mode on ONE GPU: emulate this many ranks in-process (schedule timing only)")
     ap.add_argument("--spw", type=int, default=4, help="dist mode: super-panel width in 128-column tiles")
@@ -131,6 +142,8 @@ def main():
         return main_select(args)
     if args.mode == "grad":
         return main_grad(args)
+    if args.mode in ("posterior", "rand"):
+        return main_post(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -403,6 +416,87 @@ def main_grad(args):
         "config": {"workload": f"BASELINE configs[2] terms, gradient w.r.t. v, every term parameter and the noise, N={N}",
                    "N": N, "terms": 4, "parallelism": "replicas" if world > 1 else "single"},
         "roofline": roofline, "cpu_baseline": cpu, "extra": extra,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main_post(args):
+    """posterior: mean_and_var(posterior(FiniteGP(X, 0.1), y), xs) over M test points
+    (gaplac_posterior_mean_var; src/plotting.jl:8-12); rand: rand(FiniteGP(X, 0.1)) = L z
+    (gaplac_rand; CLI/src/sample.jl:25). configs[2] kernel and inputs; replicas over ranks."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    from gaplac_amd.backend import Context
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    N, M = args.n, args.m
+    X, v = make_inputs(N)
+    rng = np.random.default_rng(5)
+    Xs = np.column_stack([rng.uniform(0.0, 10.0, M), rng.integers(0, max(1, N // 3), M).astype(np.float64)])
+    ctx = Context(local_rank)
+    post = args.mode == "posterior"
+
+    def step(i):
+        lval = LENGTHSCALES[(i + rank) % len(LENGTHSCALES)]
+        if post:
+            return ctx.posterior_mean_var(X, terms_for(lval), 0.1, v, Xs)
+        return ctx.rand(X, terms_for(lval), 0.1, v)
+
+    for i in range(args.warmup):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    value = args.steps * world / elapsed
+    # potrf N^3/3, plus the M cross-covariance rows through the factor (N^2 M) / L z (N^2)
+    flops = N ** 3 / 3.0 + (float(N) * N * M if post else float(N) * N)
+    tf = flops * value / world / 1e12
+    cpu = None
+    if world == 1 and not args.skip_cpu:
+        from oracle import restatement as R
+        t1 = time.perf_counter()
+        if post:
+            R.posterior_mean_var(X, terms_for(1.5), 0.1, v, Xs)
+        else:
+            R.rand_from(X, terms_for(1.5), 0.1, v)
+        dt = time.perf_counter() - t1
+        cpu = {"value": 1.0 / dt, "unit": "evals/s", "cores": _blas_threads(), "kind": "port",
+               "sample": f"1 full evaluation at N={N}{f', M={M}' if post else ''} (same workload), {dt:.1f} s: numpy Gram"
+                         f" + scipy-openblas dpotrf + " + ("dpotrs / dtrsm" if post else "dtrmv")}
+    what = f"posterior mean_and_var at M={M} test points" if post else "rand(FiniteGP) draws"
+    out = {
+        "metric": f"{what}: evals/sec at N={N} fp64",
+        "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded t~U(0,10), subject~randint(0,N/3); host inputs, PCIe-inclusive)",
+        "config": {"workload": f"BASELINE configs[2] kernel, N={N}" + (f", M={M}" if post else ""), "N": N,
+                   "M": M if post else None, "parallelism": "replicas" if world > 1 else "single"},
+        "roofline": None, "cpu_baseline": cpu,
+        "extra": {"flops_per_eval": flops, "achieved_tflops_per_gpu": round(tf, 3),
+                  "frac_of_fp64_peak": round(tf / PEAK_F64_TFLOPS, 4)},
     }
     print(json.dumps(out), flush=True)
     if world > 1:
