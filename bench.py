@@ -204,6 +204,18 @@ def main():
         ctx.set_profiling(False)
         st = ctx.stats()
 
+    # Throughput with two chains per GPU (extra, not the headline): independent evaluations
+    # in flight on two lanes (gaplac_logpdf_batch), filling the latency-bound tail of one
+    # evaluation's panel chain with the other's bulk updates.
+    two = None
+    if not args.no_profile and rank == 0:
+        models = [terms_for(LENGTHSCALES[i % len(LENGTHSCALES)]) for i in range(8)]
+        ctx.logpdf_batch(X, models[:2], 0.1, v)
+        tb = time.perf_counter()
+        for _ in range(2):
+            ctx.logpdf_batch(X, models, 0.1, v)
+        two = 16 / (time.perf_counter() - tb)
+
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -249,6 +261,7 @@ def main():
         },
         "gram": None,
         "last_logpdf": lp,
+        "two_chains_evals_per_s": two,
     }
     if st and st["gram_launches"] > 0 and st["gram_ms"] > 0:
         gbs = st["gram_bytes"] / (st["gram_ms"] / 1e3) / 1e9
