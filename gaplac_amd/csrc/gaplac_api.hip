@@ -23,6 +23,8 @@ using namespace gaplac;
 struct gaplac_ctx {
     int device = 0;
     hipStream_t s_main = nullptr, s_panel = nullptr;
+    hipStream_t s_extra = nullptr;  // extra rows (gradient / posterior), beside the bulk updates
+    hipEvent_t ev_xinit = nullptr, ev_xdone = nullptr;
     int diag_cus = 0;  // CUs masked out of s_main for the diagonal kernel (0: no mask)
     hipEvent_t ev_P[2] = {}, ev_R[2] = {}, ev_C[2] = {}, ev_D[2] = {}, ev_gram = nullptr, ev_gram2 = nullptr;
     double* A = nullptr;
@@ -429,7 +431,17 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             }
         }
         HIPCK(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
-        if (ctx->xr_mode) extra_rows_step(ctx, sm, lda, nt, p);
+        if (ctx->xr_mode) {
+            // extra rows on their own stream: they only need SP p final (P(p)) and touch
+            // rows no other stream writes, so they fill the bulk stream's idle time
+            hipStream_t sx = ctx->serial ? sm : ctx->s_extra;
+            if (sx != sm) HIPCK(ctx, hipStreamWaitEvent(sx, ctx->ev_P[p & 1], 0));
+            extra_rows_step(ctx, sx, lda, nt, p);
+        }
+    }
+    if (ctx->xr_mode && !ctx->serial) {
+        HIPCK(ctx, hipEventRecord(ctx->ev_xdone, ctx->s_extra));
+        HIPCK(ctx, hipStreamWaitEvent(sm, ctx->ev_xdone, 0));
     }
     launch_reduce(sm, ctx->A, lda, N, (int64_t)nt * NB, ColMap{1, 0, 1}, ctx->dres);
     HIPCK(ctx, hipGetLastError());
@@ -475,6 +487,10 @@ int enqueue_eval(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt) {
     if (ctx->xr_mode == 2)
         launch_cross_gram(ctx->s_main, ctx->A, lda, Np, nt, N, ctx->xr_M, ctx->xr_tiles, ctx->dX, N, ctx->dXs,
                           ctx->xr_M, ctx->dtp);
+    if (ctx->xr_mode && !ctx->serial) {  // the extra-row stream starts after their init
+        HIPCK(ctx, hipEventRecord(ctx->ev_xinit, ctx->s_main));
+        HIPCK(ctx, hipStreamWaitEvent(ctx->s_extra, ctx->ev_xinit, 0));
+    }
     int rc;
     if ((rc = factor_and_reduce(ctx, N, lda, nt))) return rc;
     if (ctx->xr_mode == 2)
@@ -870,6 +886,12 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
         return fail("event", e);
     if ((e = hipEventCreateWithFlags(&ctx->ev_gram2, hipEventDisableTiming)) != hipSuccess)
         return fail("event", e);
+    if ((e = hipEventCreateWithFlags(&ctx->ev_xinit, hipEventDisableTiming)) != hipSuccess)
+        return fail("event", e);
+    if ((e = hipEventCreateWithFlags(&ctx->ev_xdone, hipEventDisableTiming)) != hipSuccess)
+        return fail("event", e);
+    if ((e = hipStreamCreateWithPriority(&ctx->s_extra, hipStreamNonBlocking, least)) != hipSuccess)
+        return fail("stream", e);
     if ((e = hipMalloc(reinterpret_cast<void**>(&ctx->dres), sizeof(EvalResult))) != hipSuccess)
         return fail("hipMalloc", e);
     if ((e = hipHostMalloc(reinterpret_cast<void**>(&ctx->hres), sizeof(EvalResult), 0)) != hipSuccess)
@@ -898,6 +920,7 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->s_main) (void)hipStreamSynchronize(ctx->s_main);
     if (ctx->s_panel) (void)hipStreamSynchronize(ctx->s_panel);
+    if (ctx->s_extra) (void)hipStreamSynchronize(ctx->s_extra);
     for (gaplac_ctx* c : ctx->lanes) gaplac_ctx_destroy(c);
     ctx->lanes.clear();
     if (ctx->borrowed_inputs) {
@@ -912,6 +935,8 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     }
     if (ctx->ev_gram) (void)hipEventDestroy(ctx->ev_gram);
     if (ctx->ev_gram2) (void)hipEventDestroy(ctx->ev_gram2);
+    if (ctx->ev_xinit) (void)hipEventDestroy(ctx->ev_xinit);
+    if (ctx->ev_xdone) (void)hipEventDestroy(ctx->ev_xdone);
     if (ctx->A) (void)hipFree(ctx->A);
     if (ctx->Dinv) (void)hipFree(ctx->Dinv);
     if (ctx->tiles) (void)hipFree(ctx->tiles);
@@ -939,6 +964,7 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     if (ctx->hres) (void)hipHostFree(ctx->hres);
     if (ctx->s_main) (void)hipStreamDestroy(ctx->s_main);
     if (ctx->s_panel) (void)hipStreamDestroy(ctx->s_panel);
+    if (ctx->s_extra) (void)hipStreamDestroy(ctx->s_extra);
     delete ctx;
     return 0;
 }
