@@ -1,4 +1,4 @@
-"""How long the bulk-update kernels (tile_gemm_kernel<0>) sit idle between launches
+"""How long the bulk-update kernels (tile_syrk_kernel) sit idle between launches
 (waiting for the panel chain) in the last evaluation of a rocprofv3 trace."""
 import csv
 import sys
@@ -8,7 +8,7 @@ tr.sort(key=lambda r: int(r["Start_Timestamp"]))
 grams = [i for i, r in enumerate(tr) if "gram_kernel" in r["Kernel_Name"]]
 ev = tr[grams[-1]:]
 t0 = int(ev[0]["Start_Timestamp"])
-rest = [(int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0) for r in ev if "tile_gemm_kernel<0>" in r["Kernel_Name"]]
+rest = [(int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0) for r in ev if "tile_syrk_kernel" in r["Kernel_Name"]]
 end = max(int(r["End_Timestamp"]) for r in ev) - t0
 busy = sum(b - a for a, b in rest)
 gaps = [(rest[i + 1][0] - rest[i][1]) for i in range(len(rest) - 1)]
