@@ -9,6 +9,8 @@
 // (details at factor_and_reduce)
 #include "gaplac_internal.h"
 
+#include <cstddef>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
@@ -524,7 +526,7 @@ int enqueue_eval(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt) {
         HIPCK(ctx, hipMemcpyAsync(ctx->hgout, ctx->gout, sizeof(double) * (GAPLAC_MAX_TERMS + 1),
                                   hipMemcpyDeviceToHost, sm));
     }
-    HIPCK(ctx, hipMemcpyAsync(ctx->hres, ctx->dres, sizeof(EvalResult), hipMemcpyDeviceToHost,
+    HIPCK(ctx, hipMemcpyAsync(ctx->hres, ctx->dres, offsetof(EvalResult, part), hipMemcpyDeviceToHost,
                               ctx->s_main));
     return 0;
 }

@@ -26,6 +26,8 @@
 // by its owner or received) before the updates that read it have run.
 #include "gaplac_internal.h"
 
+#include <cstddef>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
@@ -424,7 +426,7 @@ int gaplac_dist_finish(gaplac_dist* d, double* out_logdet, double* out_quad, int
     DCK(d, hipSetDevice(d->device));
     if (d->factored_any) DCK(d, hipStreamWaitEvent(d->s_main, d->ev_panel_done, 0));
     launch_reduce(d->s_main, d->C, d->Np, d->N, (int64_t)d->nloc * NB, cmap(d), d->dres);
-    DCK(d, hipMemcpyAsync(d->hres, d->dres, sizeof(EvalResult), hipMemcpyDeviceToHost, d->s_main));
+    DCK(d, hipMemcpyAsync(d->hres, d->dres, offsetof(EvalResult, part), hipMemcpyDeviceToHost, d->s_main));
     DCK(d, hipStreamSynchronize(d->s_main));
     DCK(d, hipStreamSynchronize(d->s_panel));
     DCK(d, hipStreamSynchronize(d->s_comm));

@@ -27,11 +27,13 @@ struct TermPack {
 };
 
 // Device-side result record of one evaluation.
+constexpr int REDUCE_BLOCKS = 64;  // workgroups of the logdet / quad reduction
 struct EvalResult {
     double logpdf;
     double logdet;
     double quad;
     unsigned long long info;  // min over failing pivots of (j+1); ULLONG_MAX = none
+    double part[2][REDUCE_BLOCKS];  // per-workgroup partial sums of the reduction
 };
 
 // Per-launch device timestamps (profiling): 100 MHz s_memrealtime ticks.

@@ -14,7 +14,7 @@
 //   tile_syrk_kernel   bulk trailing update C -= P Q^T, fp64 MFMA (v_mfma_f64_16x16x4f64)
 //                      on 128x128 tiles; quad_bulk_kernel / col_update_kernel: the same
 //                      on 64x64 quadrants (small updates, critical-path column updates)
-//   reduce_kernel      logdet = 2 sum log L_jj, quad = ||z||^2, logpdf
+//   reduce_*_kernel    logdet = 2 sum log L_jj, quad = ||z||^2, logpdf
 #include "gaplac_internal.h"
 #include <math.h>
 
@@ -817,48 +817,58 @@ __global__ __launch_bounds__(256) void quad_bulk_kernel(BulkArgs a, KTime* __res
 // only those < N contribute. With the identity map this is the whole-matrix reduction;
 // on a distributed rank it is that rank's partial logdet / quad (summed across ranks by
 // the host; res->logpdf then only holds this rank's share).
-__global__ __launch_bounds__(1024) void reduce_kernel(const double* __restrict__ C, int64_t ldc,
-                                                      int64_t N, int64_t ncols, ColMap cm,
-                                                      EvalResult* __restrict__ res) {
-    __shared__ double s1[1024], s2[1024];
+// Two launches, both with a fixed summation order (deterministic): REDUCE_BLOCKS
+// workgroups each sum a contiguous range of columns (the loads are scattered, one cache
+// line each, so spreading them over many CUs is what makes this fast), then one wave sums
+// the partials in order.
+__global__ __launch_bounds__(256) void reduce_partial_kernel(const double* __restrict__ C, int64_t ldc,
+                                                             int64_t N, int64_t ncols, ColMap cm,
+                                                             EvalResult* __restrict__ res) {
+    __shared__ double s1[256], s2[256];
     const int tid = threadIdx.x;
+    const int64_t per = (ncols + REDUCE_BLOCKS - 1) / REDUCE_BLOCKS;
+    const int64_t e_lo = (int64_t)blockIdx.x * per;
+    const int64_t e_hi = e_lo + per < ncols ? e_lo + per : ncols;
     double ld = 0.0, q = 0.0;
-    // 8 strided loads in flight per thread per round (one memory latency per round)
-    for (int64_t e0 = tid; e0 < ncols; e0 += 8 * 1024) {
-        double dg[8], zz[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int64_t e = e0 + (int64_t)u * 1024;
-            const int64_t j = e < ncols ? (int64_t)cm.global((int)(e / NB)) * NB + e % NB : N;
-            dg[u] = j < N ? C[e * ldc + j] : 1.0;
-            zz[u] = j < N ? C[e * ldc + N] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            ld += log(dg[u]);
-            q += zz[u] * zz[u];
+    for (int64_t e = e_lo + tid; e < e_hi; e += 256) {
+        const int64_t j = (int64_t)cm.global((int)(e / NB)) * NB + e % NB;
+        if (j < N) {
+            ld += log(C[e * ldc + j]);
+            const double z = C[e * ldc + N];
+            q += z * z;
         }
     }
     s1[tid] = ld;
     s2[tid] = q;
     __syncthreads();
-    for (int s = 512; s > 0; s >>= 1) {
-        if (tid < s) {
-            s1[tid] += s1[tid + s];
-            s2[tid] += s2[tid + s];
+    for (int st = 128; st > 0; st >>= 1) {
+        if (tid < st) {
+            s1[tid] += s1[tid + st];
+            s2[tid] += s2[tid + st];
         }
         __syncthreads();
     }
     if (tid == 0) {
-        const double logdet = s1[0] + s1[0];
-        const double quad = s2[0];
-        const double log2pi = 1.8378770664093453;  // Julia's log2π
-        double lp = -(((double)N * log2pi + logdet) + quad) / 2.0;
-        if (res->info != ~0ull) lp = __builtin_nan("");
-        res->logdet = logdet;
-        res->quad = quad;
-        res->logpdf = lp;
+        res->part[0][blockIdx.x] = s1[0];
+        res->part[1][blockIdx.x] = s2[0];
     }
+}
+
+__global__ __launch_bounds__(64) void reduce_final_kernel(int64_t N, EvalResult* __restrict__ res) {
+    if (threadIdx.x != 0) return;
+    double s1 = 0.0, s2 = 0.0;
+    for (int b = 0; b < REDUCE_BLOCKS; ++b) {
+        s1 += res->part[0][b];
+        s2 += res->part[1][b];
+    }
+    const double logdet = s1 + s1;
+    const double quad = s2;
+    const double log2pi = 1.8378770664093453;  // Julia's log2π
+    double lp = -(((double)N * log2pi + logdet) + quad) / 2.0;
+    if (res->info != ~0ull) lp = __builtin_nan("");
+    res->logdet = logdet;
+    res->quad = quad;
+    res->logpdf = lp;
 }
 
 __global__ void kt_reset_kernel(KTime* kt, int n) {
@@ -1381,7 +1391,8 @@ void build_tile_list(int m, uint32_t* out) {
 
 void launch_reduce(hipStream_t s, const double* C, int64_t ldc, int64_t N, int64_t ncols, ColMap cm,
                    EvalResult* res) {
-    reduce_kernel<<<dim3(1), dim3(1024), 0, s>>>(C, ldc, N, ncols, cm, res);
+    reduce_partial_kernel<<<dim3(REDUCE_BLOCKS), dim3(256), 0, s>>>(C, ldc, N, ncols, cm, res);
+    reduce_final_kernel<<<dim3(1), dim3(64), 0, s>>>(N, res);
 }
 
 void launch_init_identity_rows(hipStream_t s, double* A, int64_t lda, int64_t Np, int nt, int W) {
