@@ -100,8 +100,8 @@ def cpu_baseline(N: int, budget_s: float = 25.0):
 
 # PMC traffic of the dominant kernel (tools/profile_round.sh: FETCH_SIZE / WRITE_SIZE
 # passes over the same command, corrected per MI355X_MICROARCH.md; per launch).
-TRAFFIC_FILE = os.path.join("profiles", "r01e_traffic_syrk.json")
-TRAFFIC_FILE_CINV = os.path.join("profiles", "r01e_traffic_cinv.json")
+TRAFFIC_FILE = os.path.join("profiles", "r01g_traffic_syrk.json")
+TRAFFIC_FILE_CINV = os.path.join("profiles", "r01g_traffic_cinv.json")
 
 
 def load_traffic(name=TRAFFIC_FILE):
@@ -208,7 +208,8 @@ def main():
     # in flight on two lanes (gaplac_logpdf_batch), filling the latency-bound tail of one
     # evaluation's panel chain with the other's bulk updates.
     two = None
-    if not args.no_profile and rank == 0:
+    if not args.no_profile and not args.skip_cpu and rank == 0:  # full runs only: keeps profiled
+        # runs (--skip-cpu) to the timed schedule, so rocprof averages match the event timing
         models = [terms_for(LENGTHSCALES[i % len(LENGTHSCALES)]) for i in range(8)]
         ctx.logpdf_batch(X, models[:2], 0.1, v)
         tb = time.perf_counter()
