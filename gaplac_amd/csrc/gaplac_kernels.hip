@@ -470,15 +470,7 @@ __device__ __forceinline__ void trsm_subst_kernel_body(double* __restrict__ Acol
     const int fr = lane >> 4, fc = lane & 15;
     const int64_t k0 = (int64_t)k * NB;
     const double* L = Acol + k0;  // L_kk, column-major, lda
-    // this wave's 16 rows of tile (bi, k); all of them are loaded up front (the stores of
-    // block b would otherwise order the loads of block b+1 behind them)
     double* B = Acol + (int64_t)bi * NB + 64 * (blockIdx.x & 1) + 16 * wave;
-    d4 Bt[NDB];
-#pragma unroll
-    for (int b = 0; b < NDB; ++b)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)  // B_b^T in accumulator layout: [j][r] = B[r][16b + j]
-            Bt[b][q] = B[(int64_t)(16 * b + fr + 4 * q) * lda + fc];
     {
         // block (b, c), c < b, at p = b(b-1)/2 + c: Ls[p*256 + m*16 + j] = L(16b + j, 16c + m)
         const double* Lt = L + (int64_t)(tid >> 4) * lda + (tid & 15);
@@ -494,6 +486,14 @@ __device__ __forceinline__ void trsm_subst_kernel_body(double* __restrict__ Acol
 #pragma unroll
         for (int q = 0; q < NDB; ++q) Ls[(TRSM_LBLK + q) * 256 + tid] = dv[q];
     }
+    // this wave's 16 rows of tile (bi, k), loaded after the L / Dinv staging so that the two
+    // sets of registers are never live together (216 -> 169 VGPRs), all up front
+    d4 Bt[NDB];
+#pragma unroll
+    for (int b = 0; b < NDB; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)  // B_b^T in accumulator layout: [j][r] = B[r][16b + j]
+            Bt[b][q] = B[(int64_t)(16 * b + fr + 4 * q) * lda + fc];
     __syncthreads();
     d4 Y[NDB];
 #pragma unroll
@@ -524,7 +524,8 @@ __device__ __forceinline__ void trsm_subst_kernel_body(double* __restrict__ Acol
     }
 }
 
-__global__ __launch_bounds__(256) void trsm_subst_kernel(double* __restrict__ Acol, int64_t lda, int k,
+__global__ __launch_bounds__(256) void trsm_subst_kernel(
+    double* __restrict__ Acol, int64_t lda, int k,
                                                          int bi0, const double* __restrict__ Dinv,
                                                          KTime* __restrict__ kt) {
     kt_begin(kt);
@@ -549,7 +550,11 @@ __global__ __launch_bounds__(256) void trsm_subst_kernel(double* __restrict__ Ac
 // ~64 resident tiles stay in that XCD's 4 MiB L2. Placement only affects speed; any
 // blockIdx -> tile bijection is correct.
 // ---------------------------------------------------------------------------------
-constexpr int KB = 16;
+#ifndef GAPLAC_KB
+#define GAPLAC_KB 16
+#endif
+constexpr int KB = GAPLAC_KB;  // k-chunk staged in LDS (8 or 16)
+static_assert(KB == 8 || KB == 16, "k-chunk of the tile kernels: 8 or 16");
 constexpr int LR = NB + 16;  // LDS k-row stride: lanes 16..31 land on banks 32..63
 
 __device__ __forceinline__ void tile_decode(const BulkArgs& a, int idx, int& bi, int& bj, int& lj) {
@@ -601,12 +606,14 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
         const int64_t o_ = (int64_t)(ch) * KB * ldp;                                   \
         p0 = *reinterpret_cast<const double2*>(Pr + o_);                               \
         p1 = *reinterpret_cast<const double2*>(Pr + o_ + s4);                          \
-        p2 = *reinterpret_cast<const double2*>(Pr + o_ + 2 * s4);                      \
-        p3 = *reinterpret_cast<const double2*>(Pr + o_ + 3 * s4);                      \
         q0 = *reinterpret_cast<const double2*>(Qr + o_);                               \
         q1 = *reinterpret_cast<const double2*>(Qr + o_ + s4);                          \
-        q2 = *reinterpret_cast<const double2*>(Qr + o_ + 2 * s4);                      \
-        q3 = *reinterpret_cast<const double2*>(Qr + o_ + 3 * s4);                      \
+        if constexpr (KB == 16) {                                                      \
+            p2 = *reinterpret_cast<const double2*>(Pr + o_ + 2 * s4);                  \
+            p3 = *reinterpret_cast<const double2*>(Pr + o_ + 3 * s4);                  \
+            q2 = *reinterpret_cast<const double2*>(Qr + o_ + 2 * s4);                  \
+            q3 = *reinterpret_cast<const double2*>(Qr + o_ + 3 * s4);                  \
+        }                                                                              \
     } while (0)
 #define GAPLAC_LSTORE(buf)                                                             \
     do {                                                                               \
@@ -614,12 +621,14 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
         double* sq_ = &sm[buf][1][krow][2 * lane];                                     \
         *reinterpret_cast<double2*>(sp_) = make_double2(-p0.x, -p0.y);                 \
         *reinterpret_cast<double2*>(sp_ + 4 * LR) = make_double2(-p1.x, -p1.y);        \
-        *reinterpret_cast<double2*>(sp_ + 8 * LR) = make_double2(-p2.x, -p2.y);        \
-        *reinterpret_cast<double2*>(sp_ + 12 * LR) = make_double2(-p3.x, -p3.y);       \
         *reinterpret_cast<double2*>(sq_) = q0;                                         \
         *reinterpret_cast<double2*>(sq_ + 4 * LR) = q1;                                \
-        *reinterpret_cast<double2*>(sq_ + 8 * LR) = q2;                                \
-        *reinterpret_cast<double2*>(sq_ + 12 * LR) = q3;                               \
+        if constexpr (KB == 16) {                                                      \
+            *reinterpret_cast<double2*>(sp_ + 8 * LR) = make_double2(-p2.x, -p2.y);    \
+            *reinterpret_cast<double2*>(sp_ + 12 * LR) = make_double2(-p3.x, -p3.y);   \
+            *reinterpret_cast<double2*>(sq_ + 8 * LR) = q2;                            \
+            *reinterpret_cast<double2*>(sq_ + 12 * LR) = q3;                           \
+        }                                                                              \
     } while (0)
 
     GAPLAC_GLOAD(0);
@@ -711,7 +720,14 @@ __global__ __launch_bounds__(256, 2) void tile_syrk_kernel(BulkArgs a, KTime* __
 // update on the critical path and the small trailing updates at the end of the
 // factorisation (a 128x128x256 tile alone on a CU takes ~50 us; a quadrant ~4x less).
 // ---------------------------------------------------------------------------------
-constexpr int QG = 8;  // k-steps per prefetch group
+// k-steps per prefetch group. 2 keeps the quadrant kernels at 96 VGPRs: exactly what two
+// resident bulk-update waves (2 x 208) leave on a SIMD, so the critical-path column updates
+// start on CUs that are busy with bulk tiles instead of waiting for one to retire
+// (measured: 8 -> 2 cuts their in-situ time from ~17 to ~11 ms per N=16384 evaluation).
+#ifndef GAPLAC_QG
+#define GAPLAC_QG 2
+#endif
+constexpr int QG = GAPLAC_QG;
 // Bulk updates with at most this many 128x128 tiles run as quadrants (4 WGs per tile).
 constexpr int QUAD_BULK_MAX_TILES = 512;
 
