@@ -549,6 +549,13 @@ int ensure_workspace(gaplac_ctx* ctx, int64_t N) {
     int rc;
     HIPCK(ctx, hipSetDevice(ctx->device));
     if ((rc = ensure(ctx, &ctx->A, &ctx->A_elems, (size_t)(Np + (int64_t)NB * ctx->xr_tiles) * Np))) return rc;
+    if (ctx->xr_mode && !ctx->s_extra) {
+        // created on first use only: a plain logpdf context keeps two streams, so the
+        // batch lanes (2 contexts) fit the 4 hardware queues a process gets by default
+        int least = 0, greatest = 0;
+        HIPCK(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIPCK(ctx, hipStreamCreateWithPriority(&ctx->s_extra, hipStreamNonBlocking, least));
+    }
     if (ctx->xr_mode == 2) {
         const size_t M = (size_t)ctx->xr_M;
         if ((rc = ensure(ctx, &ctx->gpart, &ctx->gpart_elems, 2 * M * (size_t)((N + 511) / 512)))) return rc;
@@ -892,8 +899,6 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
         return fail("event", e);
     if ((e = hipEventCreateWithFlags(&ctx->ev_xdone, hipEventDisableTiming)) != hipSuccess)
         return fail("event", e);
-    if ((e = hipStreamCreateWithPriority(&ctx->s_extra, hipStreamNonBlocking, least)) != hipSuccess)
-        return fail("stream", e);
     if ((e = hipMalloc(reinterpret_cast<void**>(&ctx->dres), sizeof(EvalResult))) != hipSuccess)
         return fail("hipMalloc", e);
     if ((e = hipHostMalloc(reinterpret_cast<void**>(&ctx->hres), sizeof(EvalResult), 0)) != hipSuccess)
