@@ -28,7 +28,10 @@ struct gaplac_ctx {
     hipStream_t s_extra = nullptr;  // extra rows (gradient / posterior), beside the bulk updates
     hipEvent_t ev_xinit = nullptr, ev_xdone = nullptr;
     int diag_cus = 0;  // CUs masked out of s_main for the diagonal kernel (0: no mask)
-    hipEvent_t ev_P[2] = {}, ev_R[2] = {}, ev_C[2] = {}, ev_D[2] = {}, ev_gram = nullptr, ev_gram2 = nullptr;
+    hipEvent_t ev_P[2] = {}, ev_R[2] = {}, ev_L[2] = {}, ev_gram = nullptr, ev_gram2 = nullptr;
+    // bulk updates of at most this many tiles wait for the step's lookahead column update
+    // (GAPLAC_LA_FIRST): late in the factorisation the panel chain is the critical path
+    int la_first = 0;
     double* A = nullptr;
     size_t A_elems = 0;
     double* Dinv = nullptr;  // per diagonal block: 8 inverses of its 16x16 sub-blocks
@@ -403,11 +406,14 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             const int ncols = std::min(c0 + 2 * W, nt) - (c0 + W);
             launch_col_update(sp, ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nt, c0 + W,
                               c0 + W, ncols, kd, slot(ctx, 5, 0));
+            HIPCK(ctx, hipEventRecord(ctx->ev_L[p & 1], sp));
             factor_superpanel(ctx, sp, N, lda, nt, p + 1);
             HIPCK(ctx, hipEventRecord(ctx->ev_P[(p + 1) & 1], sp));
         }
         HIPCK(ctx, hipStreamWaitEvent(sm, ctx->ev_P[p & 1], 0));
         const int jb = c0 + 2 * W;
+        if (p + 1 < nsp && jb < nt && sp != sm && (nt - jb) * (nt - jb + 1) / 2 <= ctx->la_first)
+            HIPCK(ctx, hipStreamWaitEvent(sm, ctx->ev_L[p & 1], 0));
         if (jb < nt) {
             const int m = nt - jb;
             const BulkArgs ba{ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0},
@@ -845,6 +851,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     gaplac_ctx* ctx = new gaplac_ctx();
     ctx->device = device;
     if (const char* s = std::getenv("GAPLAC_SERIAL")) ctx->serial = s[0] == '1';
+    if (const char* s = std::getenv("GAPLAC_LA_FIRST")) ctx->la_first = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     auto fail = [&](const char* what, hipError_t e) {
@@ -886,9 +893,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
             return fail("event", e);
         if ((e = hipEventCreateWithFlags(&ctx->ev_R[q], hipEventDisableTiming)) != hipSuccess)
             return fail("event", e);
-        if ((e = hipEventCreateWithFlags(&ctx->ev_C[q], hipEventDisableTiming)) != hipSuccess)
-            return fail("event", e);
-        if ((e = hipEventCreateWithFlags(&ctx->ev_D[q], hipEventDisableTiming)) != hipSuccess)
+        if ((e = hipEventCreateWithFlags(&ctx->ev_L[q], hipEventDisableTiming)) != hipSuccess)
             return fail("event", e);
     }
     if ((e = hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming)) != hipSuccess)
@@ -937,8 +942,7 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     for (int q = 0; q < 2; ++q) {
         if (ctx->ev_P[q]) (void)hipEventDestroy(ctx->ev_P[q]);
         if (ctx->ev_R[q]) (void)hipEventDestroy(ctx->ev_R[q]);
-        if (ctx->ev_C[q]) (void)hipEventDestroy(ctx->ev_C[q]);
-        if (ctx->ev_D[q]) (void)hipEventDestroy(ctx->ev_D[q]);
+        if (ctx->ev_L[q]) (void)hipEventDestroy(ctx->ev_L[q]);
     }
     if (ctx->ev_gram) (void)hipEventDestroy(ctx->ev_gram);
     if (ctx->ev_gram2) (void)hipEventDestroy(ctx->ev_gram2);
