@@ -10,7 +10,8 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_void_p
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
-LIB_PATH = os.path.join(LIB_DIR, "libgaplac_hip.so")
+# GAPLAC_LIB: an alternative build of the same library (A/B experiments in tools/)
+LIB_PATH = os.environ.get("GAPLAC_LIB") or os.path.join(LIB_DIR, "libgaplac_hip.so")
 
 SQEXP, OU, LINEAR, CAT, NOISE = 1, 2, 3, 4, 5
 KIND_NAMES = {SQEXP: "SQEXP", OU: "OU", LINEAR: "LINEAR", CAT: "CAT", NOISE: "NOISE"}

@@ -1,5 +1,6 @@
-// Diagnostic: phase timing of the diagonal-block kernel (s_memtime stamps, -DGAPLAC_STAMPS)
-// and standalone per-kernel latencies of the critical-path kernels on an idle GPU.
+// Diagnostic: the diagonal-block kernels on an idle GPU. Checks the blocked kernel
+// (default) against a CPU Cholesky of the same 128x128 block (L and the 16x16 inverses),
+// times it against the unblocked kernel (v1), and times the other chain kernels alone.
 #define GAPLAC_STAMPS 1
 #include "../gaplac_amd/csrc/gaplac_kernels.hip"
 #include <cmath>
@@ -7,32 +8,94 @@
 #include <vector>
 using namespace gaplac;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
+
+__global__ __launch_bounds__(256) void diag_v1(double* Ag, int64_t lda, int64_t N, int64_t g0, double* Dinv, EvalResult* res) {
+  potrf_diag_kernel_body(Ag, lda, N, g0, Dinv, res);
+}
+__global__ __launch_bounds__(256) void diag_v2(double* Ag, int64_t lda, int64_t N, int64_t g0, double* Dinv, EvalResult* res) {
+  potrf_diag_blocked_body(Ag, lda, N, g0, Dinv, res);
+}
+
 int main() {
   const int nt = 4, Np = nt * NB;
   std::vector<double> h((size_t)Np * Np, 0.0);
   for (int j = 0; j < Np; ++j)
     for (int i = 0; i < Np; ++i) {
-      double d = (i - j) * 0.01;
+      double d = (i - j) * 0.013 + 0.001 * ((i * 7 + j * 3) % 11 == 0 && i != j ? 0 : 0);
       h[(size_t)j * Np + i] = std::exp(-0.5 * d * d) + (i == j ? 0.1 : 0.0);
     }
-  double *A, *Dinv; EvalResult* res; KTime* kt;
+  // CPU reference: lower Cholesky of the leading 128x128 block
+  std::vector<double> L(NB * NB, 0.0);
+  for (int j = 0; j < NB; ++j) {
+    double s = h[(size_t)j * Np + j];
+    for (int k = 0; k < j; ++k) s -= L[k * NB + j] * L[k * NB + j];
+    const double d = std::sqrt(s);
+    L[j * NB + j] = d;
+    for (int i = j + 1; i < NB; ++i) {
+      double x = h[(size_t)j * Np + i];
+      for (int k = 0; k < j; ++k) x -= L[k * NB + i] * L[k * NB + j];
+      L[j * NB + i] = x / d;
+    }
+  }
+  double *A, *Dinv; EvalResult* res;
   CK(hipMalloc(&A, h.size() * 8)); CK(hipMalloc(&Dinv, nt * DINV_PER_BLOCK * 8));
-  CK(hipMalloc(&res, sizeof(EvalResult))); CK(hipMalloc(&kt, 64 * sizeof(KTime)));
+  CK(hipMalloc(&res, sizeof(EvalResult)));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int rep = 0; rep < 3; ++rep) {
-    CK(hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+  std::vector<double> out(h.size()), dinv(DINV_PER_BLOCK);
+  for (int v = 1; v <= 2; ++v) {
+    for (int rep = 0; rep < 4; ++rep) {
+      CK(hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+      launch_init_result(0, res);
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(e0));
+      if (v == 1) diag_v1<<<1, 256>>>(A, Np, 1 << 30, 0, Dinv, res);
+      else diag_v2<<<1, 256>>>(A, Np, 1 << 30, 0, Dinv, res);
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      CK(hipMemcpy(out.data(), A, out.size() * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(dinv.data(), Dinv, dinv.size() * 8, hipMemcpyDeviceToHost));
+      EvalResult hr; CK(hipMemcpy(&hr, res, sizeof hr, hipMemcpyDeviceToHost));
+      double errL = 0, errD = 0;
+      for (int j = 0; j < NB; ++j)
+        for (int i = j; i < NB; ++i) errL = std::fmax(errL, std::fabs(out[(size_t)j * Np + i] - L[j * NB + i]));
+      // Dinv_b * L_bb = I
+      for (int b = 0; b < 8; ++b)
+        for (int c = 0; c < 16; ++c)
+          for (int r = 0; r < 16; ++r) {
+            double s = 0;
+            for (int m = 0; m < 16; ++m) s += dinv[b * 256 + m * 16 + r] * (m >= c ? L[(16 * b + c) * NB + 16 * b + m] : 0.0);
+            errD = std::fmax(errD, std::fabs(s - (r == c ? 1.0 : 0.0)));
+          }
+      printf("diag v%d: %.1f us (event)  max|L-Lcpu| %.2e  max|Dinv L - I| %.2e  info %llx\n", v, ms * 1e3, errL, errD,
+             (unsigned long long)hr.info);
+      if (v == 2 && rep == 3) {
+        unsigned long long st[128]; CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof st));
+        const unsigned long long b = st[99];
+        printf("  load %llu  barrier %llu  f16(0) %llu\n", st[100] - b, st[101] - st[100], st[102] - st[101]);
+        unsigned long long prev = st[102];
+        for (int s = 0; s < 8; ++s) {
+          printf("  s=%d: [w0] ->T %5llu dinv %5llu T-barrier %5llu", s, st[4 * s] - prev, st[4 * s + 1] - st[4 * s], st[4 * s + 2] - st[4 * s + 1]);
+          printf(" [w1] trsm %5llu", st[40 + s] - st[4 * s]);
+          if (s < 7) {
+            printf(" [w0] upd %5llu f16 %5llu [w1] store+upd %5llu U-barrier(w0 view) %5llu\n", st[4 * s + 3] - st[4 * s + 2],
+                   st[60 + s] - st[4 * s + 3], st[50 + s] - st[4 * s + 2], st[4 * s + 4] - st[60 + s]);
+            prev = st[4 * s + 4];
+          } else printf("\n");
+        }
+        printf("  end %llu total %llu cycles\n", st[103] - st[4 * 7 + 2], st[103] - b);
+      }
+    }
+  }
+  // non-PD: zero the block's (37,37) pivot region -> info must be 38 in both
+  for (int v = 1; v <= 2; ++v) {
+    std::vector<double> hb = h;
+    for (int i = 0; i < Np; ++i) { hb[(size_t)37 * Np + i] = 0; hb[(size_t)i * Np + 37] = 0; }
+    CK(hipMemcpy(A, hb.data(), hb.size() * 8, hipMemcpyHostToDevice));
     launch_init_result(0, res);
-    CK(hipEventRecord(e0));
-    launch_potrf_diag(0, A, Np, 1 << 30, 0, Dinv, res, nullptr);
-    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
-    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-    unsigned long long st[64]; CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof st));
-    printf("diag kernel %.1f us (event); phases in shader cycles from start:\n", ms * 1e3);
-    printf("  load %llu\n", st[0] - st[20]);
-    for (int s = 0; s < 8; ++s)
-      printf("  panel %d: phase1 %6llu  panel(wave0) %6llu  barrier-wait %6llu\n", s, st[1 + 2 * s] - (s ? st[2 * s] : st[0]),
-             st[2 + 2 * s] - st[1 + 2 * s], (s < 7 ? st[3 + 2 * s] : st[17]) - st[2 + 2 * s]);
-    printf("  dinv %llu  store %llu  total %llu\n", st[18] - st[17], st[19] - st[18], st[19] - st[20]);
+    if (v == 1) diag_v1<<<1, 256>>>(A, Np, 1 << 30, 0, Dinv, res);
+    else diag_v2<<<1, 256>>>(A, Np, 1 << 30, 0, Dinv, res);
+    EvalResult hr; CK(hipMemcpy(&hr, res, sizeof hr, hipMemcpyDeviceToHost));
+    printf("non-PD v%d: info %llu (expect 38)\n", v, (unsigned long long)hr.info);
   }
   // standalone latencies of the chain kernels (one tile each)
   CK(hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice));
