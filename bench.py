@@ -18,6 +18,7 @@ Prints ONE JSON line (rank 0).
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import platform
@@ -29,25 +30,14 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-N_DEFAULT = 16384
-SQEXP, OU, LINEAR, CAT, NOISE = 1, 2, 3, 4, 5
+from gaplac_amd import configs as CF  # noqa: E402  (synthetic inputs of the BASELINE configs)
+
+N_DEFAULT = CF.N2
 PEAK_F64_TFLOPS = 78.6   # MI355X FP64 matrix, spec
 PEAK_HBM_GBS = 8000.0    # MI355X HBM3E, spec (MI355X_MICROARCH.md)
-LENGTHSCALES = (1.0, 1.5, 2.0, 3.0)
-
-
-def make_inputs(N: int, seed: int = 2):
-    rng = np.random.default_rng(seed)
-    t = rng.uniform(0.0, 10.0, N)
-    subject = rng.integers(0, max(1, N // 3), N).astype(np.float64)
-    v = rng.standard_normal(N)
-    X = np.column_stack([t, subject])  # N x 2, unique columns (t, subject)
-    return X, v
-
-
-def terms_for(l_sqexp: float):
-    # SqExp(:t; l) + OU(:t; l=3) + Cat(:subject) + Noise  — each term its own group (sum)
-    return [(SQEXP, 0, l_sqexp, 0), (OU, 0, 3.0, 1), (CAT, 1, 0.0, 2), (NOISE, -1, 1.0, 3)]
+LENGTHSCALES = CF.LENGTHSCALES_2
+make_inputs = CF.config2_inputs
+terms_for = CF.config2_terms
 
 
 def _blas_threads() -> int:
@@ -135,6 +125,8 @@ def main():
     ap.add_argument("--loopback", type=int, default=0,
                     help="dist mode on ONE GPU: emulate this many ranks in-process (schedule timing only)")
     ap.add_argument("--spw", type=int, default=4, help="dist mode: super-panel width in 128-column tiles")
+    ap.add_argument("--no-dist", action="store_true",
+                    help="replicas mode with --gpus > 1: skip the configs[3] distributed extra line")
     args = ap.parse_args()
     if args.mode in ("dist", "single"):
         return main_dist(args)
@@ -154,7 +146,8 @@ def main():
 
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank),
+                                timeout=datetime.timedelta(seconds=300))
 
     from gaplac_amd.backend import Context
 
@@ -168,16 +161,12 @@ def main():
     def step(i):
         # replicas: every rank walks its own lengthscale sequence
         lval = LENGTHSCALES[(i + rank) % len(LENGTHSCALES)]
-        return ctx.logpdf_device(N, 2, dX.data_ptr(), N, terms_for(lval), 0.1, dv.data_ptr())
+        return ctx.logpdf_device(N, 2, dX.data_ptr(), N, terms_for(lval), CF.NOISE_VAR, dv.data_ptr())
 
     for i in range(args.warmup):
         step(i)
 
-    # hipEvents on s_main around every bulk trailing-update launch of the timed steps
-    # (the production schedule; gaplac_set_profiling mode 2) give the roofline's
-    # per-launch duration.
-    ctx.reset_stats()
-    ctx.set_profiling(0 if args.no_profile else 2)
+    # The timed region: the production schedule, no instrumentation.
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -189,12 +178,20 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ctx.set_profiling(0)
-    st_ev = ctx.stats()
 
-    # Per-kernel breakdown (extra): a separate pass right after the timed region, same
-    # inputs, with per-launch device timestamps wired into every kernel (first workgroup
-    # start / last wave end on the 100 MHz s_memrealtime clock).
+    # Roofline pass: the same steps with hipEvents recorded on s_main (the launching
+    # stream) around every bulk tile_syrk launch (gaplac_set_profiling mode 2).
+    st_ev = None
+    if not args.no_profile:
+        ctx.reset_stats()
+        ctx.set_profiling(2)
+        for i in range(max(1, min(args.steps, 5))):
+            step(i)
+        ctx.set_profiling(0)
+        st_ev = ctx.stats()
+
+    # Per-kernel breakdown (extra): per-launch device timestamps wired into every kernel
+    # (first workgroup start / last wave end on the 100 MHz s_memrealtime clock).
     st = None
     if not args.no_profile and args.profile_steps > 0:
         ctx.reset_stats()
@@ -204,23 +201,32 @@ def main():
         ctx.set_profiling(False)
         st = ctx.stats()
 
+    full_run = not args.no_profile and not args.skip_cpu  # profiled runs keep to the timed schedule
     # Throughput with two chains per GPU (extra, not the headline): independent evaluations
     # in flight on two lanes (gaplac_logpdf_batch), filling the latency-bound tail of one
     # evaluation's panel chain with the other's bulk updates.
     two = None
-    if not args.no_profile and not args.skip_cpu and rank == 0:  # full runs only: keeps profiled
-        # runs (--skip-cpu) to the timed schedule, so rocprof averages match the event timing
+    n4096 = None
+    if full_run and rank == 0:
         models = [terms_for(LENGTHSCALES[i % len(LENGTHSCALES)]) for i in range(8)]
-        ctx.logpdf_batch(X, models[:2], 0.1, v)
+        ctx.logpdf_batch(X, models[:2], CF.NOISE_VAR, v)
         tb = time.perf_counter()
         for _ in range(2):
-            ctx.logpdf_batch(X, models, 0.1, v)
+            ctx.logpdf_batch(X, models, CF.NOISE_VAR, v)
         two = 16 / (time.perf_counter() - tb)
+        n4096 = measure_config1(ctx, torch)
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # BASELINE configs[3] across the job's GPUs (N=65536, one evaluation spread over all
+    # ranks, panel broadcasts over RCCL): an extra line beside the replicas headline.
+    dist_line = None
+    if world > 1 and not args.no_dist:
+        ctx.close()  # free the N=16384 workspace before the 65536 one
+        dist_line = measure_config3_dist(rank, world, local_rank, torch, dist)
 
     total_evals = args.steps * world
     value = total_evals / elapsed
@@ -232,7 +238,7 @@ def main():
         return
 
     roofline = None
-    if st_ev["syrk_launches"] > 0 and st_ev["syrk_ms"] > 0:
+    if st_ev and st_ev["syrk_launches"] > 0 and st_ev["syrk_ms"] > 0:
         flops_per_launch = st_ev["syrk_flops"] / st_ev["syrk_launches"]
         avg_s = st_ev["syrk_ms"] / st_ev["syrk_launches"] / 1e3
         achieved = flops_per_launch / avg_s / 1e12
@@ -250,7 +256,9 @@ def main():
             "flops_per_launch": flops_per_launch,
             "avg_launch_ms": st_ev["syrk_ms"] / st_ev["syrk_launches"],
             "launches": st_ev["syrk_launches"],
-            "timing": "hipEvents recorded on the launching stream (s_main) around every tile_syrk_kernel launch inside the timed region; cf. profiles/*kernel_stats.csv (rocprofv3 --kernel-trace --stats of the same command)",
+            "timing": "hipEvents recorded on the launching stream (s_main) around every tile_syrk_kernel launch, "
+                      "in a pass of the same steps right after the (uninstrumented) timed region; cf. "
+                      "profiles/*kernel_stats.csv (rocprofv3 --kernel-trace --stats of the same command)",
         }
     eval_flops = N ** 3 / 3.0 + N ** 2
     eval_tflops = eval_flops * (value / world) / 1e12
@@ -263,6 +271,8 @@ def main():
         "gram": None,
         "last_logpdf": lp,
         "two_chains_evals_per_s": two,
+        "n4096": n4096,
+        "dist": dist_line,
     }
     if st and st["gram_launches"] > 0 and st["gram_ms"] > 0:
         gbs = st["gram_bytes"] / (st["gram_ms"] / 1e3) / 1e9
@@ -308,6 +318,80 @@ def main():
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def measure_config1(ctx, torch, steps: int = 8):
+    """BASELINE configs[1] (SqExp(:x), N=4096, l swept over {0.5, 1, 1.5, 3}) on this GPU:
+    evals/s with inputs resident in HBM, and the whole evaluation against the fp64 MFMA
+    peak (at nt = 33 tile columns every trailing update is small: the quadrant kernel)."""
+    x, v = CF.config1_inputs()
+    N = x.shape[0]
+    dx = torch.from_numpy(x).to("cuda")
+    dvv = torch.from_numpy(v).to("cuda")
+
+    def one(i):
+        return ctx.logpdf_device(N, 1, dx.data_ptr(), N, CF.config1_terms(CF.LENGTHSCALES_1[i % 4]), CF.NOISE_VAR,
+                                 dvv.data_ptr())
+
+    for i in range(2):
+        one(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        one(i)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    flops = N ** 3 / 3.0 + N ** 2
+    tf = flops / dt / 1e12
+    return {"workload": f"BASELINE configs[1]: SqExp(:x; l in {list(CF.LENGTHSCALES_1)}), N={N}, noise 0.1",
+            "evals_per_s": 1.0 / dt, "ms_per_eval": dt * 1e3, "achieved_tflops": round(tf, 3),
+            "roofline": {"bound": "mfma", "kernel": "whole evaluation (F = N^3/3 + N^2)", "achieved": round(tf, 3),
+                         "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / PEAK_F64_TFLOPS, 4)}}
+
+
+def measure_config3_dist(rank: int, world: int, local_rank: int, torch, dist, steps: int = 3):
+    """BASELINE configs[3]: SqExp(:x; l=1.5), N=65536, one evaluation over all ranks of the
+    job (1-D block-column cyclic Cholesky, panel broadcasts with RCCL over xGMI,
+    gaplac_amd/distributed.py). Strong scaling: the work per evaluation is fixed."""
+    from gaplac_amd import distributed as DI
+    x, v = CF.config3_inputs()
+    N = x.shape[0]
+    try:
+        dx = torch.from_numpy(x).to("cuda")
+        dvv = torch.from_numpy(v).to("cuda")
+        r = DI.DistRank(local_rank, world, rank, spw=DI.DEFAULT_SPW)
+        tr = DI.TorchTransport(device=torch.device("cuda", local_rank), timing=True)
+
+        def one():
+            return DI.logpdf_dist_device([r], tr, N, 1, dx.data_ptr(), N, CF.CONFIG3_TERMS, CF.NOISE_VAR,
+                                         dvv.data_ptr())
+
+        one()  # warmup (workspace, lists, RCCL communicator)
+        tr.reset_timing()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        lp = None
+        for _ in range(steps):
+            lp = one()
+        torch.cuda.synchronize()
+        dist.barrier()
+        el = time.perf_counter() - t0
+        t = torch.tensor([el, tr.bcast_ms() / steps], dtype=torch.float64, device="cuda")
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        r.close()
+        el = max(float(a[0].item()) for a in allt)
+        bc = [round(float(a[1].item()), 3) for a in allt]
+        flops = N ** 3 / 3.0 + N ** 2
+        tf = flops * steps / el / 1e12 / world
+        return {"workload": f"BASELINE configs[3]: SqExp(:x; l=1.5), N={N}, noise 0.1, one evaluation over {world} GPUs",
+                "value": steps / el, "unit": "evals/s", "ms_per_eval": el / steps * 1e3, "scaling": "strong",
+                "ranks_seen": len(allt), "bcast_ms_per_eval_per_rank": bc, "last_logpdf": lp,
+                "achieved_tflops_per_gpu": round(tf, 3), "frac_of_fp64_peak": round(tf / PEAK_F64_TFLOPS, 4),
+                "transport": "torch.distributed nccl (RCCL) broadcast on the library's comm stream"}
+    except Exception as e:  # the replicas headline stands on its own; report the failure
+        return {"error": repr(e)[:400]}
 
 
 def cpu_grad_baseline(N: int):
@@ -517,34 +601,8 @@ def main_post(args):
         dist.destroy_process_group()
 
 
-def make_inputs_dist(N: int, seed: int = 3):
-    """BASELINE configs[3]: SqExp(:x) l=1.5, x ~ U(-5, 5), v ~ N(0, 1)."""
-    rng = np.random.default_rng(seed)
-    x = rng.uniform(-5.0, 5.0, N)
-    v = rng.standard_normal(N)
-    return x, v
-
-
-def select_models():
-    """BASELINE configs[4]: 64 candidate formulas = 16 structures over the columns
-    (x, t, subject) x lengthscales {0.5, 1, 2, 4}. Columns: 0 x, 1 t,
-    2 subject; every term is its own group (GaPLAC formulas lower to sums)."""
-    x, t, g = 0, 1, 2
-    structures = [
-        lambda l: [(SQEXP, x, l)], lambda l: [(OU, x, l)], lambda l: [(SQEXP, t, l)], lambda l: [(OU, t, l)],
-        lambda l: [(SQEXP, x, l), (CAT, g, 0.0)], lambda l: [(OU, t, l), (CAT, g, 0.0)],
-        lambda l: [(SQEXP, x, l), (OU, t, 2 * l)], lambda l: [(SQEXP, t, l), (LINEAR, x, 0.5)],
-        lambda l: [(SQEXP, x, l), (SQEXP, t, l)], lambda l: [(OU, x, l), (CAT, g, 0.0)],
-        lambda l: [(SQEXP, t, l), (OU, t, 3.0), (CAT, g, 0.0)], lambda l: [(LINEAR, x, l), (CAT, g, 0.0)],
-        lambda l: [(SQEXP, x, l), (OU, x, l), (CAT, g, 0.0)], lambda l: [(OU, t, l), (LINEAR, t, 1.0)],
-        lambda l: [(SQEXP, x, l), (SQEXP, t, 2 * l), (CAT, g, 0.0)],
-        lambda l: [(SQEXP, t, l), (OU, x, l), (LINEAR, x, 0.0), (CAT, g, 0.0)],
-    ]
-    models = []
-    for mk in structures:
-        for l in (0.5, 1.0, 2.0, 4.0):
-            models.append([(k, c, p, i) for i, (k, c, p) in enumerate(mk(l))])
-    return models
+make_inputs_dist = CF.config3_inputs
+select_models = CF.select_models
 
 
 def main_select(args):
@@ -561,11 +619,8 @@ def main_select(args):
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    N = args.n if args.n != N_DEFAULT else 8192
-    rng = np.random.default_rng(4)
-    X = np.column_stack([rng.uniform(-5, 5, N), rng.uniform(0, 10, N),
-                         rng.integers(0, max(1, N // 3), N).astype(np.float64)])
-    y = rng.standard_normal(N)
+    N = args.n if args.n != N_DEFAULT else CF.N4
+    X, y = CF.config4_inputs(N)
     models = select_models()
     ctx = Context(local_rank)
     mine = replicas.shard(len(models), rank, world)
@@ -622,11 +677,11 @@ def main_dist(args):
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    N = args.n if args.n != N_DEFAULT else 65536
+    N = args.n if args.n != N_DEFAULT else CF.N3
     x, v = make_inputs_dist(N)
     dX = torch.from_numpy(x).to("cuda")
     dv = torch.from_numpy(v).to("cuda")
-    terms = [(SQEXP, 0, 1.5, 0)]
+    terms = CF.CONFIG3_TERMS
     nranks = args.loopback if args.loopback > 0 else world
     if args.mode == "single":
         ctx = Context(local_rank)

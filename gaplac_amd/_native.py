@@ -10,8 +10,7 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_void_p
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
-# GAPLAC_LIB: an alternative build of the same library (A/B experiments in tools/)
-LIB_PATH = os.environ.get("GAPLAC_LIB") or os.path.join(LIB_DIR, "libgaplac_hip.so")
+LIB_PATH = os.path.join(LIB_DIR, "libgaplac_hip.so")
 
 SQEXP, OU, LINEAR, CAT, NOISE = 1, 2, 3, 4, 5
 KIND_NAMES = {SQEXP: "SQEXP", OU: "OU", LINEAR: "LINEAR", CAT: "CAT", NOISE: "NOISE"}
@@ -37,6 +36,7 @@ EXPORTED = (
     "gaplac_set_profiling",
     "gaplac_get_stats",
     "gaplac_reset_stats",
+    "gaplac_plan_check",
     "gaplac_dist_create",
     "gaplac_dist_destroy",
     "gaplac_dist_last_error",
@@ -126,6 +126,7 @@ def load() -> ctypes.CDLL:
     lib.gaplac_get_stats.argtypes = [c_void_p, POINTER(Stats)]
     lib.gaplac_reset_stats.argtypes = [c_void_p]
     _I32P, _I64P, _VPP = POINTER(c_int32), POINTER(c_int64), POINTER(c_void_p)
+    lib.gaplac_plan_check.argtypes = [c_int64, c_int32, c_int64, c_int32, _I64P, _I64P, c_char_p, c_int64]
     lib.gaplac_dist_create.argtypes = [c_int, c_int, c_int, c_int, _VPP]
     lib.gaplac_dist_destroy.argtypes = [c_void_p]
     lib.gaplac_dist_last_error.argtypes = [c_void_p]

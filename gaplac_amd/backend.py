@@ -88,20 +88,22 @@ class Context:
         N, D = Xc.shape
         if v.shape[0] != N:
             raise ArgumentError(f"length of v ({v.shape[0]}) != N ({N})")
+        terms = list(terms)  # one pass: a generator must not reach the library as T = 0
         ta = term_array(terms)
         lp, ld, q = c_double(), c_double(), c_double()
         rc = self.lib.gaplac_logpdf(
-            self.h, N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), len(list(terms)), ta, float(noise),
+            self.h, N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), len(terms), ta, float(noise),
             v.ctypes.data_as(c_void_p), byref(lp), byref(ld), byref(q),
         )
         self._check(rc)
         return (lp.value, ld.value, q.value) if full else lp.value
 
     def logpdf_device(self, N: int, D: int, dX_ptr: int, ldx: int, terms, noise: float, dv_ptr: int, full=False):
+        terms = list(terms)
         ta = term_array(terms)
         lp, ld, q = c_double(), c_double(), c_double()
         rc = self.lib.gaplac_logpdf_device(
-            self.h, N, D, c_void_p(dX_ptr), ldx, len(list(terms)), ta, float(noise), c_void_p(dv_ptr),
+            self.h, N, D, c_void_p(dX_ptr), ldx, len(terms), ta, float(noise), c_void_p(dv_ptr),
             byref(lp), byref(ld), byref(q),
         )
         self._check(rc)
@@ -114,8 +116,9 @@ class Context:
         N, D = Xc.shape
         offs = [0]
         flat = []
+        models = [list(m) for m in models]
         for m in models:
-            flat.extend(list(m))
+            flat.extend(m)
             offs.append(len(flat))
         ta = term_array(flat)
         off_arr = (c_int32 * len(offs))(*offs)
@@ -210,8 +213,9 @@ class Context:
         Xc = _colmajor(X)
         N, D = Xc.shape
         out = np.empty((N, N), dtype=np.float64, order="F")
+        terms = list(terms)
         ta = term_array(terms)
-        rc = self.lib.gaplac_gram(self.h, N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), len(list(terms)), ta,
+        rc = self.lib.gaplac_gram(self.h, N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), len(terms), ta,
                                   float(noise), out.ctypes.data_as(c_void_p), max(N, 1))
         self._check(rc)
         return out
@@ -223,8 +227,9 @@ class Context:
         N, D = Xc.shape
         L = np.empty((N, N), dtype=np.float64, order="F")
         z = np.empty(N, dtype=np.float64)
+        terms = list(terms)
         ta = term_array(terms)
-        rc = self.lib.gaplac_factor(self.h, N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), len(list(terms)), ta,
+        rc = self.lib.gaplac_factor(self.h, N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), len(terms), ta,
                                     float(noise), v.ctypes.data_as(c_void_p), L.ctypes.data_as(c_void_p),
                                     max(N, 1), z.ctypes.data_as(c_void_p))
         self._check(rc)

@@ -64,6 +64,7 @@ struct gaplac_ctx {
     };
     std::vector<EvPair> evpairs;
     bool serial = false;  // GAPLAC_SERIAL=1: one stream, no overlap (per-kernel timing)
+    bool dry = false;     // host-only walk of the schedule (gaplac_plan_check): no HIP calls
     int spw = 4;          // GAPLAC_SPW: super-panel width in 128-column tiles (bulk K = 128 spw)
     gaplac_stats stats{};
     struct Slot {
@@ -140,6 +141,12 @@ int set_err(gaplac_ctx* ctx, int code, const char* fmt, ...) {
         hipError_t e_ = (call);                                                            \
         if (e_ != hipSuccess)                                                              \
             return set_err(ctx, GAPLAC_E_HIP, "%s failed: %s", #call, hipGetErrorString(e_)); \
+    } while (0)
+
+// HIP runtime calls of the schedule itself (events, waits, copies): skipped in a dry run.
+#define HIPQ(ctx, call)                    \
+    do {                                   \
+        if (!(ctx)->dry) HIPCK(ctx, call); \
     } while (0)
 
 int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
@@ -392,28 +399,28 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     hipStream_t sp = ctx->serial ? sm : ctx->s_panel;
     const int W = ctx->spw;
     const int nsp = (nt + W - 1) / W;
-    HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_gram, 0));  // first W tile columns built
+    HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_gram, 0));  // first W tile columns built
     factor_superpanel(ctx, sp, N, lda, nt, 0);
-    HIPCK(ctx, hipEventRecord(ctx->ev_P[0], sp));
+    HIPQ(ctx, hipEventRecord(ctx->ev_P[0], sp));
     for (int p = 0; p < nsp; ++p) {
         const int c0 = W * p;
         const int kd = (std::min(c0 + W, nt) - c0) * NB;  // depth of super-panel p
         if (p + 1 < nsp) {
             if (p >= 1)
-                HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_R[(p - 1) & 1], 0));
+                HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_R[(p - 1) & 1], 0));
             else
-                HIPCK(ctx, hipStreamWaitEvent(sp, ctx->ev_gram2, 0));  // rest of the Gram built
+                HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_gram2, 0));  // rest of the Gram built
             const int ncols = std::min(c0 + 2 * W, nt) - (c0 + W);
             launch_col_update(sp, ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nt, c0 + W,
                               c0 + W, ncols, kd, slot(ctx, 5, 0));
-            HIPCK(ctx, hipEventRecord(ctx->ev_L[p & 1], sp));
+            HIPQ(ctx, hipEventRecord(ctx->ev_L[p & 1], sp));
             factor_superpanel(ctx, sp, N, lda, nt, p + 1);
-            HIPCK(ctx, hipEventRecord(ctx->ev_P[(p + 1) & 1], sp));
+            HIPQ(ctx, hipEventRecord(ctx->ev_P[(p + 1) & 1], sp));
         }
-        HIPCK(ctx, hipStreamWaitEvent(sm, ctx->ev_P[p & 1], 0));
+        HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_P[p & 1], 0));
         const int jb = c0 + 2 * W;
         if (p + 1 < nsp && jb < nt && sp != sm && (nt - jb) * (nt - jb + 1) / 2 <= ctx->la_first)
-            HIPCK(ctx, hipStreamWaitEvent(sm, ctx->ev_L[p & 1], 0));
+            HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_L[p & 1], 0));
         if (jb < nt) {
             const int m = nt - jb;
             const BulkArgs ba{ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0},
@@ -427,32 +434,32 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
                 e0 = 2 * ctx->evpairs.size();
                 while (ctx->evpool.size() < e0 + 2) {
                     hipEvent_t e;
-                    HIPCK(ctx, hipEventCreate(&e));
+                    HIPQ(ctx, hipEventCreate(&e));
                     ctx->evpool.push_back(e);
                 }
-                HIPCK(ctx, hipEventRecord(ctx->evpool[e0], sm));
+                HIPQ(ctx, hipEventRecord(ctx->evpool[e0], sm));
             }
             launch_bulk(sm, ba, kt);
             if (ev) {
-                HIPCK(ctx, hipEventRecord(ctx->evpool[e0 + 1], sm));
+                HIPQ(ctx, hipEventRecord(ctx->evpool[e0 + 1], sm));
                 ctx->evpairs.push_back({e0, syrk_flops(m) * (kd / NB), syrk_bytes(m, kd), 0});
             }
         }
-        HIPCK(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
+        HIPQ(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
         if (ctx->xr_mode) {
             // extra rows on their own stream: they only need SP p final (P(p)) and touch
             // rows no other stream writes, so they fill the bulk stream's idle time
             hipStream_t sx = ctx->serial ? sm : ctx->s_extra;
-            if (sx != sm) HIPCK(ctx, hipStreamWaitEvent(sx, ctx->ev_P[p & 1], 0));
+            if (sx != sm) HIPQ(ctx, hipStreamWaitEvent(sx, ctx->ev_P[p & 1], 0));
             extra_rows_step(ctx, sx, lda, nt, p);
         }
     }
     if (ctx->xr_mode && !ctx->serial) {
-        HIPCK(ctx, hipEventRecord(ctx->ev_xdone, ctx->s_extra));
-        HIPCK(ctx, hipStreamWaitEvent(sm, ctx->ev_xdone, 0));
+        HIPQ(ctx, hipEventRecord(ctx->ev_xdone, ctx->s_extra));
+        HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_xdone, 0));
     }
     launch_reduce(sm, ctx->A, lda, N, (int64_t)nt * NB, ColMap{1, 0, 1}, ctx->dres);
-    HIPCK(ctx, hipGetLastError());
+    HIPQ(ctx, hipGetLastError());
     return 0;
 }
 
@@ -476,7 +483,7 @@ int ensure_tile_lists(gaplac_ctx* ctx, int nt) {
 // the result record (and the profiling slots), Gram build, factorisation schedule,
 // reduction, result copy to the pinned host record. Inputs: ctx->dX (ld N), ctx->dv,
 // ctx->dtp.
-int enqueue_eval(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt) {
+int enqueue_eval_body(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt) {
     const int64_t lda = Np + (int64_t)NB * ctx->xr_tiles;
     launch_init_result(ctx->s_main, ctx->dres);
     if (ctx->recording) launch_kt_reset(ctx->s_main, ctx->dkt, (int)ctx->kt_cap);
@@ -487,17 +494,17 @@ int enqueue_eval(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt) {
     const double frac = nt > 0 ? 1.0 - (double)rest * (rest + 1) / ((double)nt * (nt + 1)) : 1.0;
     launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 1, ctx->spw,
                 slot(ctx, 1, bytes * frac));
-    HIPCK(ctx, hipEventRecord(ctx->ev_gram, ctx->s_main));
+    HIPQ(ctx, hipEventRecord(ctx->ev_gram, ctx->s_main));
     launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 2, ctx->spw,
                 slot(ctx, 1, bytes * (1.0 - frac)));
-    HIPCK(ctx, hipEventRecord(ctx->ev_gram2, ctx->s_main));
+    HIPQ(ctx, hipEventRecord(ctx->ev_gram2, ctx->s_main));
     if (ctx->xr_mode == 1) launch_init_identity_rows(ctx->s_main, ctx->A, lda, Np, nt, ctx->spw);
     if (ctx->xr_mode == 2)
         launch_cross_gram(ctx->s_main, ctx->A, lda, Np, nt, N, ctx->xr_M, ctx->xr_tiles, ctx->dX, N, ctx->dXs,
                           ctx->xr_M, ctx->dtp);
     if (ctx->xr_mode && !ctx->serial) {  // the extra-row stream starts after their init
-        HIPCK(ctx, hipEventRecord(ctx->ev_xinit, ctx->s_main));
-        HIPCK(ctx, hipStreamWaitEvent(ctx->s_extra, ctx->ev_xinit, 0));
+        HIPQ(ctx, hipEventRecord(ctx->ev_xinit, ctx->s_main));
+        HIPQ(ctx, hipStreamWaitEvent(ctx->s_extra, ctx->ev_xinit, 0));
     }
     int rc;
     if ((rc = factor_and_reduce(ctx, N, lda, nt))) return rc;
@@ -515,25 +522,48 @@ int enqueue_eval(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt) {
             e0 = 2 * ctx->evpairs.size();
             while (ctx->evpool.size() < e0 + 2) {
                 hipEvent_t e;
-                HIPCK(ctx, hipEventCreate(&e));
+                HIPQ(ctx, hipEventCreate(&e));
                 ctx->evpool.push_back(e);
             }
-            HIPCK(ctx, hipEventRecord(ctx->evpool[e0], sm));
+            HIPQ(ctx, hipEventRecord(ctx->evpool[e0], sm));
         }
-        launch_cinv_tiles(sm, ctx->A, lda, Np, ctx->glist, ctx->glist_blocks, slot(ctx, 8, 0));
+        launch_cinv_tiles(sm, ctx->A, lda, Np, ctx->glist, ctx->glist_blocks, (int)((N + NB - 1) / NB),
+                          slot(ctx, 8, 0));
         if (ev) {
-            HIPCK(ctx, hipEventRecord(ctx->evpool[e0 + 1], sm));
+            HIPQ(ctx, hipEventRecord(ctx->evpool[e0 + 1], sm));
             ctx->evpairs.push_back({e0, 0.0, 0.0, 8});
         }
         launch_grad_contract(sm, ctx->A, lda, N, ctx->dX, N, ctx->galpha, ctx->dtp, ctx->dgp, ctx->gpart,
                              slot(ctx, 9, 0));
         const int m = (int)((N + NB - 1) / NB);
         launch_grad_reduce(sm, ctx->gpart, m * (m + 1) / 2, ctx->htp->T, ctx->gout);
-        HIPCK(ctx, hipMemcpyAsync(ctx->hgout, ctx->gout, sizeof(double) * (GAPLAC_MAX_TERMS + 1),
+        HIPQ(ctx, hipMemcpyAsync(ctx->hgout, ctx->gout, sizeof(double) * (GAPLAC_MAX_TERMS + 1),
                                   hipMemcpyDeviceToHost, sm));
     }
-    HIPCK(ctx, hipMemcpyAsync(ctx->hres, ctx->dres, offsetof(EvalResult, part), hipMemcpyDeviceToHost,
+    HIPQ(ctx, hipMemcpyAsync(ctx->hres, ctx->dres, offsetof(EvalResult, part), hipMemcpyDeviceToHost,
                               ctx->s_main));
+    return 0;
+}
+
+// The schedule under a footprint guard over ctx->A (unless the caller installed one, as
+// gaplac_plan_check's dry run does): a launch whose grid would touch elements outside
+// the workspace is not enqueued and the evaluation fails with GAPLAC_E_ARG.
+int enqueue_eval(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt) {
+    LaunchGuard local;
+    LaunchGuard* g = current_guard();
+    const bool own = g == nullptr;
+    if (own) {
+        local.base = ctx->A;
+        local.elems = (int64_t)ctx->A_elems;
+        g = &local;
+    }
+    GuardScope scope(g);
+    const int64_t v0 = g->violations;
+    const int rc = enqueue_eval_body(ctx, N, D, Np, nt);
+    if (rc) return rc;
+    if (g->violations > v0)
+        return set_err(ctx, GAPLAC_E_ARG, "launch footprint outside the workspace (N=%lld): %s", (long long)N,
+                       g->first.c_str());
     return 0;
 }
 
@@ -1047,6 +1077,8 @@ int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D, 
         return 0;
     }
     HIPCK(ctx, hipSetDevice(ctx->device));
+    // the lanes borrow dX / dv: nothing of an earlier call may still read them
+    for (gaplac_ctx* c : ctx->lanes) HIPCK(ctx, hipStreamSynchronize(c->s_main));
     if ((rc = upload(ctx, N, D, X, ldx, v))) return rc;
     HIPCK(ctx, hipStreamSynchronize(ctx->s_main));  // lanes read X / v on their own streams
     // Models in flight on up to batch_lanes lanes (lane 0 = this context): an order-8192
@@ -1079,16 +1111,27 @@ int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D, 
         pending[(size_t)l] = -1;
         return 0;
     };
+    // on an error, wait for every lane still in flight before returning: they read the
+    // borrowed dX / dv, which the next call's upload overwrites
+    auto quiesce = [&](int code) -> int {
+        for (int l = 0; l < nl; ++l) {
+            gaplac_ctx* c = lane[(size_t)l];
+            (void)hipStreamSynchronize(c->s_main);
+            (void)hipStreamSynchronize(c->s_panel);
+            if (c->s_extra) (void)hipStreamSynchronize(c->s_extra);
+        }
+        return code;
+    };
     for (int m = 0; m < nmodels; ++m) {
         const int l = m % nl;
-        if ((rc = drain(l))) return rc;
+        if ((rc = drain(l))) return quiesce(rc);
         packs[(size_t)m].noise = noise;
         if ((rc = eval_enqueue(lane[(size_t)l], N, D, packs[(size_t)m])))
-            return set_err(ctx, rc, "batch lane %d: %s", l, lane[(size_t)l]->err.c_str());
+            return quiesce(set_err(ctx, rc, "batch lane %d: %s", l, lane[(size_t)l]->err.c_str()));
         pending[(size_t)l] = m;
     }
     for (int l = 0; l < nl; ++l)
-        if ((rc = drain(l))) return rc;
+        if ((rc = drain(l))) return quiesce(rc);
     return 0;
 }
 
@@ -1109,7 +1152,14 @@ int gaplac_gram(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t 
     tp.noise = noise;
     *ctx->htp = tp;
     HIPCK(ctx, hipMemcpyAsync(ctx->dtp, ctx->htp, sizeof(TermPack), hipMemcpyHostToDevice, ctx->s_main));
-    launch_gram(ctx->s_main, ctx->A, Np, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 0, 0, nullptr);
+    {
+        LaunchGuard g;
+        g.base = ctx->A;
+        g.elems = (int64_t)ctx->A_elems;
+        GuardScope scope(&g);
+        launch_gram(ctx->s_main, ctx->A, Np, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 0, 0, nullptr);
+        if (g.violations) return set_err(ctx, GAPLAC_E_ARG, "launch footprint outside the workspace: %s", g.first.c_str());
+    }
     HIPCK(ctx, hipGetLastError());
     HIPCK(ctx, hipMemcpy2DAsync(out_C, (size_t)ldc * 8, ctx->A, (size_t)Np * 8, (size_t)N * 8,
                                 (size_t)N, hipMemcpyDeviceToHost, ctx->s_main));
@@ -1183,11 +1233,70 @@ int gaplac_rand(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t 
     if ((rc = ensure(ctx, &ctx->gpart, &ctx->gpart_elems, nk * (size_t)N))) return rc;
     if ((rc = ensure(ctx, &ctx->gdv, &ctx->gdv_elems, (size_t)N))) return rc;
     const int64_t Np = round_up(N + 1, NB);
-    launch_lower_mv(ctx->s_main, ctx->A, Np, N, ctx->dv, ctx->gpart, ctx->gdv);
+    {
+        LaunchGuard g;
+        g.base = ctx->A;
+        g.elems = (int64_t)ctx->A_elems;
+        GuardScope scope(&g);
+        launch_lower_mv(ctx->s_main, ctx->A, Np, N, ctx->dv, ctx->gpart, ctx->gdv);
+        if (g.violations) return set_err(ctx, GAPLAC_E_ARG, "launch footprint outside the workspace: %s", g.first.c_str());
+    }
     HIPCK(ctx, hipGetLastError());
     HIPCK(ctx, hipMemcpyAsync(out, ctx->gdv, (size_t)N * 8, hipMemcpyDeviceToHost, ctx->s_main));
     HIPCK(ctx, hipStreamSynchronize(ctx->s_main));
     return 0;
+}
+
+// Host-only walk of one evaluation's schedule (no device needed): every launch's element
+// range is checked against the workspace ensure_workspace would allocate for N.
+// mode 0: logpdf; 1: logpdf + gradient (identity rows); 2: posterior at M test points.
+int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* out_launches,
+                      int64_t* out_violations, char* msg, int64_t msglen) {
+    const bool short_ws = mode >= 8;  // negative control: a workspace one element short
+    if (short_ws) mode -= 8;
+    if (N < 1 || mode < 0 || mode > 2 || (mode == 2 && M < 1) || spw < 1 || spw > 8) return GAPLAC_E_ARG;
+    gaplac_ctx c;
+    c.dry = true;
+    c.spw = spw;
+    const int64_t Np = round_up(N + 1, NB);
+    const int nt = (int)(Np / NB);
+    c.xr_mode = mode;
+    c.xr_tiles = mode == 1 ? nt : mode == 2 ? (int)((M + NB - 1) / NB) : 0;
+    c.xr_M = mode == 2 ? M : 0;
+    // never dereferenced: the walk only does pointer arithmetic against the guard's base
+    double* const fake = reinterpret_cast<double*>((uintptr_t)1 << 44);
+    c.A = fake;
+    c.A_elems = (size_t)(Np + (int64_t)NB * c.xr_tiles) * (size_t)Np;  // as ensure_workspace
+    c.Dinv = fake;
+    c.tiles = reinterpret_cast<uint32_t*>(fake);
+    c.tile_off.assign((size_t)nt + 1, 0);
+    for (int m = 1; m <= nt; ++m) c.tile_off[(size_t)m] = c.tile_off[(size_t)m - 1] + (size_t)(m - 1) * m / 2;
+    c.tiles_nt = nt;
+    if (mode == 1) {
+        std::vector<uint32_t> gl;
+        build_grad_list((int)((N + NB - 1) / NB), gl);
+        c.glist_blocks = (int)gl.size();
+    }
+    TermPack tp{};
+    tp.T = 1;
+    c.htp = &tp;
+    LaunchGuard g;
+    g.base = fake;
+    g.elems = (int64_t)c.A_elems - (short_ws ? 1 : 0);
+    g.dry = true;
+    int rc;
+    {
+        GuardScope scope(&g);
+        rc = enqueue_eval(&c, N, 1, Np, nt);
+    }
+    c.htp = nullptr;
+    c.A = nullptr;
+    c.Dinv = nullptr;
+    c.tiles = nullptr;
+    if (out_launches) *out_launches = g.launches;
+    if (out_violations) *out_violations = g.violations;
+    if (msg && msglen > 0) std::snprintf(msg, (size_t)msglen, "%s", g.first.c_str());
+    return rc == GAPLAC_E_ARG && g.violations ? 0 : rc;
 }
 
 int gaplac_set_profiling(gaplac_ctx* ctx, int mode) {

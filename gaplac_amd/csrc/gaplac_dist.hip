@@ -160,6 +160,25 @@ int build_lists(gaplac_dist* d) {
     return 0;
 }
 
+// Footprint guard over this rank's column storage (Np x nloc*NB) for the launches of one
+// step (gaplac_internal.h).
+struct DistGuard {
+    gaplac_dist* d;
+    LaunchGuard g;
+    GuardScope scope;
+    explicit DistGuard(gaplac_dist* dd) : d(dd), g(make(dd)), scope(&g) {}
+    static LaunchGuard make(const gaplac_dist* dd) {
+        LaunchGuard x;
+        x.base = dd->C;
+        x.elems = dd->Np * (int64_t)dd->nloc * NB;
+        return x;
+    }
+    int check() {
+        if (!g.violations) return 0;
+        return derr(d, GAPLAC_E_ARG, "launch footprint outside the rank's storage: %s", g.first.c_str());
+    }
+};
+
 }  // namespace
 
 extern "C" {
@@ -322,7 +341,12 @@ int gaplac_dist_begin(gaplac_dist* d, int64_t N, int32_t D, const double* X, int
     *d->htp = tp;
     DCK(d, hipMemcpyAsync(d->dtp, d->htp, sizeof(TermPack), hipMemcpyHostToDevice, d->s_main));
     launch_init_result(d->s_main, d->dres);
-    launch_gram_list(d->s_main, d->C, Np, N, d->dX, N, d->dv, d->dtp, d->tiles, d->gram_count, cmap(d), nullptr);
+    {
+        DistGuard guard(d);
+        launch_gram_list(d->s_main, d->C, Np, N, d->dX, N, d->dv, d->dtp, d->tiles, d->gram_count, cmap(d), nt - 1,
+                         nloc - 1, nullptr);
+        if ((rc = guard.check())) return rc;
+    }
     DCK(d, hipEventRecord(d->ev_gram, d->s_main));
     DCK(d, hipStreamWaitEvent(d->s_panel, d->ev_gram, 0));
     DCK(d, hipGetLastError());
@@ -336,6 +360,7 @@ int gaplac_dist_factor(gaplac_dist* d, int32_t s) {
     if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "factor: step %d out of range", s);
     if (!owns(d, s)) return derr(d, GAPLAC_E_ARG, "factor: rank %d does not own super-panel %d", d->rank, s);
     DCK(d, hipSetDevice(d->device));
+    DistGuard guard(d);
     hipStream_t sp = d->s_panel;
     const int c0 = sp_first(d, s), w = sp_width(d, s), lc0 = sp_local(d, s);
     const int64_t ldc = d->Np;
@@ -364,7 +389,7 @@ int gaplac_dist_factor(gaplac_dist* d, int32_t s) {
     DCK(d, hipEventRecord(d->ev_panel_done, sp));
     d->factored_any = true;
     DCK(d, hipGetLastError());
-    return 0;
+    return guard.check();
 }
 
 // Device buffer, element count and root rank of the broadcast of panel s.
@@ -409,9 +434,14 @@ int gaplac_dist_update(gaplac_dist* d, int32_t s) {
     const int rel = s + 1 - d->rank;
     const int u = rel < 0 ? 0 : rel / d->nranks + 1;
     if (u < (int)d->bulk_cnt.size() && d->bulk_cnt[(size_t)u] > 0) {
-        const BulkArgs ba{d->C, d->Np, panel_of(d, s), d->tiles + d->bulk_off[(size_t)u], d->bulk_cnt[(size_t)u],
-                          sp_width(d, s) * NB, 0, 0, cmap(d)};
+        BulkArgs ba{d->C, d->Np, panel_of(d, s), d->tiles + d->bulk_off[(size_t)u], d->bulk_cnt[(size_t)u],
+                    sp_width(d, s) * NB, 0, 0, cmap(d)};
+        ba.max_r = d->nt - 1;    // list entries: global row block
+        ba.max_c = d->nloc - 1;  //              and local tile column
+        DistGuard guard(d);
         launch_bulk(d->s_main, ba, nullptr);
+        int rc;
+        if ((rc = guard.check())) return rc;
     }
     DCK(d, hipEventRecord(d->ev_free_main[s & 1], d->s_main));
     DCK(d, hipGetLastError());
@@ -425,7 +455,12 @@ int gaplac_dist_finish(gaplac_dist* d, double* out_logdet, double* out_quad, int
     if (!d) return GAPLAC_E_ARG;
     DCK(d, hipSetDevice(d->device));
     if (d->factored_any) DCK(d, hipStreamWaitEvent(d->s_main, d->ev_panel_done, 0));
-    launch_reduce(d->s_main, d->C, d->Np, d->N, (int64_t)d->nloc * NB, cmap(d), d->dres);
+    {
+        DistGuard guard(d);
+        launch_reduce(d->s_main, d->C, d->Np, d->N, (int64_t)d->nloc * NB, cmap(d), d->dres);
+        int rc;
+        if ((rc = guard.check())) return rc;
+    }
     DCK(d, hipMemcpyAsync(d->hres, d->dres, offsetof(EvalResult, part), hipMemcpyDeviceToHost, d->s_main));
     DCK(d, hipStreamSynchronize(d->s_main));
     DCK(d, hipStreamSynchronize(d->s_panel));

@@ -74,7 +74,34 @@ struct BulkArgs {
     int ntiles, kdepth, bi0, lj0;
     ColMap cm;
     int rect_rows = 0;
+    int max_r = -1, max_c = -1;  // largest lo16 / hi16 list entry (-1: an m x m triangle list)
 };
+
+// Host-side footprint guard. Before launching, every launcher computes the
+// element range [p + lo, p + hi) its grid will touch in the column storage it is given
+// and checks it against the guarded allocation; a launch outside it is skipped and
+// recorded (the API then returns GAPLAC_E_ARG). In dry mode nothing is launched at all:
+// the host walks the real schedule (gaplac_plan_check), so the footprints of every launch
+// of an evaluation can be checked without a GPU.
+struct LaunchGuard {
+    const double* base = nullptr;  // the guarded allocation (a context's column storage)
+    int64_t elems = 0;
+    bool dry = false;
+    int64_t launches = 0;
+    int64_t violations = 0;
+    std::string first;  // the first violation
+};
+LaunchGuard*& current_guard();  // this thread's guard (nullptr: unchecked)
+struct GuardScope {
+    LaunchGuard* prev;
+    explicit GuardScope(LaunchGuard* g) : prev(current_guard()) { current_guard() = g; }
+    ~GuardScope() { current_guard() = prev; }
+};
+// true if the launch may proceed: [p + lo, p + hi) inside the guard (when p is guarded,
+// i.e. derived from its base) and not a dry run
+bool guard_launch(const char* what, const double* p, int64_t lo, int64_t hi);
+// launches that touch no guarded storage: counted, skipped in a dry run
+bool guard_launch(const char* what);
 
 // Term validation + kernel-argument pack (gaplac_api.hip); on error returns GAPLAC_E_*
 // and sets *err.
@@ -88,10 +115,11 @@ int pack_terms(int32_t D, int32_t T, const gaplac_term* terms, TermPack* tp, std
 void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt,
                  const double* X, int64_t ldx, const double* v, const TermPack* dtp, int part, int w,
                  KTime* kt);
-// Gram tiles of a list (entry bi | lj << 16, absolute) into column storage C.
+// Gram tiles of a list (entry bi | lj << 16, absolute, bi <= max_bi, lj <= max_lj) into
+// column storage C.
 void launch_gram_list(hipStream_t s, double* C, int64_t ldc, int64_t N, const double* X, int64_t ldx,
                       const double* v, const TermPack* dtp, const uint32_t* tiles, int ntiles, ColMap cm,
-                      KTime* kt);
+                      int max_bi, int max_lj, KTime* kt);
 // Diagonal block at Ablk (global rows/cols g0..g0+127): L in place + Dinv (DINV_PER_BLOCK
 // doubles: 8 column-major 16x16 inverses of its diagonal sub-blocks).
 void launch_potrf_diag(hipStream_t s, double* Ablk, int64_t lda, int64_t N, int64_t g0,
@@ -140,7 +168,7 @@ struct GradTermPack {
 // M = -C^{-1} = -Y Y^T over the lower tiles I >= J (I, J < m) into the factor storage
 // (rows / columns < Np of A): tile (I, J) = -sum_{k >= I NB} Y_Ik Y_Jk^T. list[b] = I | J << 16
 // for workgroup b, 0xffffffff = idle (build_grad_list).
-void launch_cinv_tiles(hipStream_t s, double* A, int64_t lda, int64_t Np, const uint32_t* list, int nblocks,
+void launch_cinv_tiles(hipStream_t s, double* A, int64_t lda, int64_t Np, const uint32_t* list, int nblocks, int m,
                        KTime* kt);
 // Per lower tile of M: its share of sum_ij (alpha_i alpha_j - Cinv_ij) dC_ij/dtheta for every
 // term parameter (t < T) and the observation variance (t = T): partial[tile * (T+1) + t].

@@ -19,7 +19,9 @@
 #include <math.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <cstdint>
 
 namespace gaplac {
 
@@ -1209,7 +1211,7 @@ __global__ void kt_reset_kernel(KTime* kt, int n) {
 }
 
 void launch_kt_reset(hipStream_t s, KTime* kt, int n) {
-    if (n > 0) kt_reset_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s>>>(kt, n);
+    if (n > 0 && guard_launch("kt_reset_kernel")) kt_reset_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s>>>(kt, n);
 }
 
 __global__ void init_result_kernel(EvalResult* res) {
@@ -1647,43 +1649,102 @@ __global__ __launch_bounds__(256) void lower_mv_reduce_kernel(const double* __re
 }
 
 // ------------------------------- launchers ---------------------------------------
+// Every launcher first passes the element range its grid will touch to guard_launch
+// (gaplac_internal.h): derived from the same tile counts / decodes the
+// kernel uses, so a wrong grid (the round-1 part-2 Gram count for N < 255) is caught on
+// the host instead of writing past the allocation.
+LaunchGuard*& current_guard() {
+    static thread_local LaunchGuard* g = nullptr;
+    return g;
+}
+
+bool guard_launch(const char* what, const double* p, int64_t lo, int64_t hi) {
+    LaunchGuard* g = current_guard();
+    if (!g) return true;
+    ++g->launches;
+    if (g->base) {
+        const int64_t off = (int64_t)(((intptr_t)p - (intptr_t)g->base) / (intptr_t)sizeof(double));
+        if (lo > hi || off + lo < 0 || off + hi > g->elems) {
+            if (g->violations++ == 0) {
+                char buf[200];
+                snprintf(buf, sizeof buf, "%s touches elements [%lld, %lld) of a %lld-element workspace", what,
+                         (long long)(off + lo), (long long)(off + hi), (long long)g->elems);
+                g->first = buf;
+            }
+            return false;
+        }
+    }
+    return !g->dry;
+}
+
+bool guard_launch(const char* what) {
+    (void)what;
+    LaunchGuard* g = current_guard();
+    if (!g) return true;
+    ++g->launches;
+    return !g->dry;
+}
+
+// End (exclusive) of the elements a set of tiles with rows <= max_bi, columns <= max_bj
+// touches in column storage with leading dimension ld.
+static int64_t tiles_end(int64_t ld, int64_t max_bi, int64_t max_bj) {
+    return ((max_bj + 1) * NB - 1) * ld + (max_bi + 1) * NB;
+}
+
+// Largest b with b (b + 1) / 2 <= t (the row tri_index decodes for workgroup t).
+static int64_t tri_row(int64_t t) {
+    if (t <= 0) return 0;
+    int64_t b = (int64_t)((std::sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((b + 1) * (b + 2) / 2 <= t) ++b;
+    while (b * (b + 1) / 2 > t) --b;
+    return b;
+}
+
 void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const double* X,
                  int64_t ldx, const double* v, const TermPack* dtp, int part, int w, KTime* kt) {
-    int64_t ntiles;
+    int64_t ntiles, max_bi, max_bj;
     if (part == 1) {
         w = w < nt ? w : nt;
         ntiles = 0;
         for (int c = 0; c < w; ++c) ntiles += nt - c;
+        max_bi = nt - 1;
+        max_bj = w - 1;
     } else {
         if (part == 0) w = 0;
         const int64_t m = nt - w;  // part 2 with nt <= w: nothing left (m <= 0)
         ntiles = m > 0 ? m * (m + 1) / 2 : 0;
+        max_bi = max_bj = ntiles > 0 ? w + tri_row(ntiles - 1) : 0;
     }
     if (ntiles <= 0) return;
+    if (!guard_launch("gram_kernel", A, 0, tiles_end(lda, max_bi, max_bj))) return;
     gram_kernel<<<dim3((unsigned)ntiles), dim3(256), 0, s>>>(A, lda, N, X, ldx, v, dtp, nt, part, w, kt);
 }
 
 void launch_gram_list(hipStream_t s, double* C, int64_t ldc, int64_t N, const double* X, int64_t ldx,
                       const double* v, const TermPack* dtp, const uint32_t* tiles, int ntiles, ColMap cm,
-                      KTime* kt) {
+                      int max_bi, int max_lj, KTime* kt) {
     if (ntiles <= 0) return;
+    if (!guard_launch("gram_list_kernel", C, 0, tiles_end(ldc, max_bi, max_lj))) return;
     gram_list_kernel<<<dim3((unsigned)ntiles), dim3(256), 0, s>>>(C, ldc, N, X, ldx, v, dtp, tiles, cm, kt);
 }
 
 void launch_potrf_diag(hipStream_t s, double* Ablk, int64_t lda, int64_t N, int64_t g0, double* Dinv,
                        EvalResult* res, KTime* kt) {
+    if (!guard_launch("potrf_diag_kernel", Ablk, 0, tiles_end(lda, 0, 0))) return;
     potrf_diag_kernel<<<dim3(1), dim3(256), 0, s>>>(Ablk, lda, N, g0, Dinv, res, kt);
 }
 
 void launch_trsm(hipStream_t s, double* Acol, int64_t lda, int nt, int k, const double* Dinv, KTime* kt) {
     const int n = nt - k - 1;
     if (n <= 0) return;
+    if (!guard_launch("trsm_subst_kernel", Acol, 0, tiles_end(lda, nt - 1, 0))) return;
     trsm_subst_kernel<<<dim3(2 * n), dim3(256), 0, s>>>(Acol, lda, k, k + 1, Dinv, kt);
 }
 
 void launch_trsm_rows(hipStream_t s, double* Acol, int64_t lda, int k, int bi0, int nrows, const double* Dinv,
                       KTime* kt) {
     if (nrows <= 0) return;
+    if (!guard_launch("trsm_subst_kernel (rows)", Acol, 0, tiles_end(lda, std::max(k, bi0 + nrows - 1), 0))) return;
     trsm_subst_kernel<<<dim3(2 * nrows), dim3(256), 0, s>>>(Acol, lda, k, bi0, Dinv, kt);
 }
 
@@ -1715,6 +1776,17 @@ static int device_cus() {
 
 void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt) {
     if (a.ntiles <= 0) return;
+    int64_t max_r, max_c;
+    if (a.rect_rows > 0) {
+        max_r = a.rect_rows - 1;
+        max_c = a.ntiles / a.rect_rows - 1;
+    } else if (a.max_r >= 0) {
+        max_r = a.max_r;
+        max_c = a.max_c;
+    } else {
+        max_r = max_c = tri_row(a.ntiles - 1);  // an m x m triangle list: entries < m
+    }
+    if (!guard_launch("bulk update", a.C, 0, tiles_end(a.ldc, a.bi0 + max_r, a.lj0 + max_c))) return;
     int grid = ((a.ntiles + 7) >> 3) << 3;
     if (syrk_is_small(a.ntiles)) {
         quad_bulk_kernel<<<dim3((unsigned)(4 * grid)), dim3(256), 0, s>>>(a, kt);
@@ -1731,6 +1803,7 @@ void launch_col_update(hipStream_t s, double* C, int64_t ldc, const Panel& pn, i
     if (m0 <= 0 || ncols <= 0) return;
     int tiles = 0;
     for (int c = 0; c < ncols && c < m0; ++c) tiles += m0 - c;
+    if (!guard_launch("col_update_kernel", C, 0, tiles_end(ldc, nt - 1, lj0 + std::min(ncols, m0) - 1))) return;
     col_update_kernel<<<dim3((unsigned)(4 * tiles)), dim3(256), 0, s>>>(C, ldc, pn, jb, lj0, m0, kdepth, kt);
 }
 
@@ -1747,32 +1820,37 @@ void build_tile_list(int m, uint32_t* out) {
 
 void launch_reduce(hipStream_t s, const double* C, int64_t ldc, int64_t N, int64_t ncols, ColMap cm,
                    EvalResult* res) {
+    if (ncols <= 0 || !guard_launch("reduce_partial_kernel", C, 0, (ncols - 1) * ldc + N + 1)) return;
     reduce_partial_kernel<<<dim3(REDUCE_BLOCKS), dim3(256), 0, s>>>(C, ldc, N, ncols, cm, res);
     reduce_final_kernel<<<dim3(1), dim3(64), 0, s>>>(N, res);
 }
 
 void launch_init_identity_rows(hipStream_t s, double* A, int64_t lda, int64_t Np, int nt, int W) {
     if (nt <= 0) return;
+    if (!guard_launch("init_identity_rows_kernel", A, 0, ((int64_t)nt * NB - 1) * lda + Np + (int64_t)nt * NB)) return;
     init_identity_rows_kernel<<<dim3((unsigned)nt, (unsigned)nt), dim3(256), 0, s>>>(A, lda, Np, W);
 }
 
 void launch_zero_tail_cols(hipStream_t s, double* A, int64_t lda, int64_t Np, int64_t N) {
     if (Np <= N) return;
+    if (!guard_launch("zero_tail_cols_kernel", A, N * lda, (Np - 1) * lda + 2 * Np)) return;
     zero_tail_cols_kernel<<<dim3((unsigned)((Np + 255) / 256), (unsigned)(Np - N)), dim3(256), 0, s>>>(A, lda, Np, N);
 }
 
 void launch_alpha(hipStream_t s, const double* A, int64_t lda, int64_t Np, int64_t N, double* partial,
                   double* alpha, double* dv) {
     if (N <= 0) return;
+    if (!guard_launch("alpha_partial_kernel", A, 0, (N - 1) * lda + Np + N)) return;
     const int nk = (int)((N + 511) / 512);
     alpha_partial_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nk), dim3(256), 0, s>>>(A, lda, Np, N,
                                                                                              partial);
     alpha_reduce_kernel<<<dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s>>>(partial, N, nk, alpha, dv);
 }
 
-void launch_cinv_tiles(hipStream_t s, double* A, int64_t lda, int64_t Np, const uint32_t* list, int nblocks,
+void launch_cinv_tiles(hipStream_t s, double* A, int64_t lda, int64_t Np, const uint32_t* list, int nblocks, int m,
                        KTime* kt) {
     if (nblocks <= 0) return;
+    if (!guard_launch("cinv_tile_kernel", A, 0, (Np - 1) * lda + Np + (int64_t)m * NB)) return;
     cinv_tile_kernel<<<dim3((unsigned)nblocks), dim3(256), 0, s>>>(A, lda, Np, list, kt);
 }
 
@@ -1782,11 +1860,13 @@ void launch_grad_contract(hipStream_t s, const double* A, int64_t lda, int64_t N
     const int m = (int)((N + NB - 1) / NB);
     const int64_t tiles = (int64_t)m * (m + 1) / 2;
     if (tiles <= 0) return;
+    if (!guard_launch("grad_contract_kernel", A, 0, tiles_end(lda, m - 1, m - 1))) return;
     grad_contract_kernel<<<dim3((unsigned)tiles), dim3(256), 0, s>>>(A, lda, N, X, ldx, alpha, dtp, dgp, partial,
                                                                      kt);
 }
 
 void launch_grad_reduce(hipStream_t s, const double* partial, int nb, int T, double* out) {
+    if (!guard_launch("grad_reduce_kernel")) return;
     grad_reduce_kernel<<<dim3((unsigned)(T + 1)), dim3(256), 0, s>>>(partial, nb, T, out);
 }
 
@@ -1813,6 +1893,7 @@ void build_grad_list(int m, std::vector<uint32_t>& out) {
 void launch_cross_gram(hipStream_t s, double* A, int64_t lda, int64_t Np, int nt, int64_t N, int64_t M, int mt,
                        const double* X, int64_t ldx, const double* Xs, int64_t ldxs, const TermPack* dtp) {
     if (nt <= 0 || mt <= 0) return;
+    if (!guard_launch("cross_gram_kernel", A, 0, ((int64_t)nt * NB - 1) * lda + Np + (int64_t)mt * NB)) return;
     cross_gram_kernel<<<dim3((unsigned)nt, (unsigned)mt), dim3(256), 0, s>>>(A, lda, Np, N, M, X, ldx, Xs, ldxs, dtp);
 }
 
@@ -1820,6 +1901,7 @@ void launch_posterior(hipStream_t s, const double* A, int64_t lda, int64_t Np, i
                       const double* Xs, int64_t ldxs, const TermPack* dtp, double* partial, double* mean,
                       double* var) {
     if (M <= 0) return;
+    if (!guard_launch("post_partial_kernel", A, 0, (N - 1) * lda + Np + M)) return;
     const int nk = (int)((N + 511) / 512);
     double* pm = partial;
     double* pv = partial + (size_t)nk * M;
@@ -1832,6 +1914,7 @@ void launch_posterior(hipStream_t s, const double* A, int64_t lda, int64_t Np, i
 void launch_lower_mv(hipStream_t s, const double* A, int64_t lda, int64_t N, const double* z, double* partial,
                      double* out) {
     if (N <= 0) return;
+    if (!guard_launch("lower_mv_partial_kernel", A, 0, (N - 1) * lda + N)) return;
     const int nk = (int)((N + 511) / 512);
     lower_mv_partial_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nk), dim3(256), 0, s>>>(A, lda, N, z,
                                                                                                 partial);
@@ -1839,6 +1922,7 @@ void launch_lower_mv(hipStream_t s, const double* A, int64_t lda, int64_t N, con
 }
 
 void launch_init_result(hipStream_t s, EvalResult* res) {
+    if (!guard_launch("init_result_kernel")) return;
     init_result_kernel<<<dim3(1), dim3(1), 0, s>>>(res);
 }
 

@@ -154,16 +154,33 @@ class DistRank:
 class TorchTransport:
     """One rank per process; torch.distributed collectives on the rank's comm stream.
 
-    device: where the 3-number allreduce runs (default: the current CUDA device for the
-    nccl backend, the CPU otherwise)."""
+    device: where the 3-number allreduce runs (default: the rank's own GPU, DistRank.device,
+    for the nccl backend — not torch's current device, which a process-per-GPU caller may
+    not have set — and the CPU otherwise).
+    timing: record hipEvents on the comm stream around every broadcast (bcast_ms())."""
 
-    def __init__(self, group=None, device=None):
+    def __init__(self, group=None, device=None, timing: bool = False):
         self.group = group
         self.device = device
+        self.rank_device = None
+        self.timing = timing
+        self._ev = []
 
     def prepare(self, ranks: Sequence, N: int):
         (r,) = ranks
         r.use_torch_panel_buffers(N)
+        self.rank_device = r.device
+
+    def reset_timing(self):
+        self._ev = []
+
+    def bcast_ms(self) -> float:
+        """Sum of the recorded broadcasts' durations on the comm stream (synchronises)."""
+        tot = 0.0
+        for a, b in self._ev:
+            b.synchronize()
+            tot += a.elapsed_time(b)
+        return tot
 
     def bcast(self, ranks: Sequence, s: int):
         import torch
@@ -174,8 +191,15 @@ class TorchTransport:
         buf = r.panel_tensor(s, count)
         src = dist.get_global_rank(self.group, root) if self.group is not None else root
         if stream and buf.is_cuda:
-            with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=buf.device)):
+            st = torch.cuda.ExternalStream(stream, device=buf.device)
+            with torch.cuda.stream(st):
+                if self.timing:
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ev[0].record(st)
                 dist.broadcast(buf, src=src, group=self.group, async_op=True).wait()
+                if self.timing:
+                    ev[1].record(st)
+                    self._ev.append(ev)
         else:
             dist.broadcast(buf, src=src, group=self.group)
         r.comm_end(s)
@@ -186,7 +210,11 @@ class TorchTransport:
         (ld, q, info), = parts
         dev = device if device is not None else self.device
         if dev is None:
-            dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(self.group) == "nccl" else "cpu"
+            if dist.get_backend(self.group) == "nccl":
+                dev = torch.device("cuda", self.rank_device if self.rank_device is not None
+                                   else torch.cuda.current_device())
+            else:
+                dev = "cpu"
         sums = torch.tensor([ld, q], dtype=torch.float64, device=dev)
         imin = torch.tensor([info if info > 0 else np.iinfo(np.int64).max], dtype=torch.int64, device=dev)
         dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=self.group)

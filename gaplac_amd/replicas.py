@@ -55,16 +55,29 @@ def run_sharded(evaluate: Callable[[int], float], n_units: int, group=None, devi
     return gather_results(mine, vals, n_units, group=group, device=device)
 
 
-def select_batch(ctx, X, models, noise: float, v, group=None, device=None) -> np.ndarray:
+def select_batch(ctx, X, models, noise: float, v, group=None, device=None, raise_posdef: bool = True):
     """Batched `select` over many formulas, sharded across ranks (BASELINE configs[4]).
 
     models: list of term lists (lowered descriptors). Each rank runs its share through one
-    gaplac_logpdf_batch call; PD failures come back as NaN (their info is per model)."""
+    gaplac_logpdf_batch call; the values and the per-model potrf info are all-gathered.
+    Like the reference (CLI/src/select.jl:49-50: logpdf -> cholesky(check=true)), a
+    formula whose covariance is not positive definite raises PosDefException(info) — the
+    first such model's, on every rank. raise_posdef=False instead returns
+    (values, info) with NaN values where info > 0."""
     import torch.distributed as dist
+    from .backend import PosDefException
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     mine = shard(len(models), rank, world)
     if mine:
-        out, _info = ctx.logpdf_batch(X, [models[u] for u in mine], noise, v)
+        out, info = ctx.logpdf_batch(X, [models[u] for u in mine], noise, v)
     else:
-        out = []
-    return gather_results(mine, list(out), len(models), group=group, device=device)
+        out, info = [], []
+    vals = gather_results(mine, list(out), len(models), group=group, device=device)
+    infos = gather_results(mine, [float(i) for i in info], len(models), group=group, device=device)
+    infos = np.nan_to_num(infos, nan=0.0).astype(np.int64)
+    if raise_posdef:
+        bad = np.nonzero(infos > 0)[0]
+        if bad.size:
+            raise PosDefException(int(infos[bad[0]]))
+        return vals
+    return vals, infos

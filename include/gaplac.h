@@ -203,6 +203,20 @@ int gaplac_set_profiling(gaplac_ctx* ctx, int mode);
 int gaplac_get_stats(gaplac_ctx* ctx, gaplac_stats* out);
 int gaplac_reset_stats(gaplac_ctx* ctx);
 
+/* Launch-footprint check of one evaluation's schedule, on the host only (no device, no
+ * context): walks every launch gaplac_logpdf (mode 0), gaplac_logpdf_grad (mode 1) or
+ * gaplac_posterior_mean_var at M test points (mode 2) would enqueue for order N with
+ * super-panel width spw, and checks the element range each launch's grid touches against
+ * the workspace the context allocates for N. Every launcher applies the same check before
+ * a real launch (a violating launch is not enqueued; the entry returns GAPLAC_E_ARG).
+ * Returns 0 (the counts are valid) or GAPLAC_E_ARG for bad arguments; *out_violations is
+ * the number of launches outside the workspace and msg (msglen bytes) the first one.
+ * mode + 8: the same walk against a workspace one element short (the guard's negative
+ * control: the last Gram tile must be reported).
+ * Not in the reference (an internal guard). */
+int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* out_launches,
+                      int64_t* out_violations, char* msg, int64_t msglen);
+
 /* ------------------------------------------------------------------------------------
  * Distributed evaluation (BASELINE configs[3]: N = 65536 over the GPUs of one node; one
  * process per GPU). 1-D block-column cyclic Cholesky: super-panels of spw 128-wide

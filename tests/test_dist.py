@@ -12,6 +12,7 @@ import pytest
 import torch.multiprocessing as mp
 
 from gaplac_amd import replicas
+from gaplac_amd.backend import PosDefException
 
 
 def _free_port():
@@ -60,7 +61,16 @@ def _worker(rank, world, port, q):
                                                                  [(4, 1, 0.0, 0)], [(3, 0, 0.5, 0)]]
         res = replicas.select_batch(_OracleCtx(), X, models, 0.1, v)
         vals = replicas.run_sharded(lambda u: float(u) * 10 + rank * 0, 5)
-        q.put((rank, res.tolist(), vals.tolist()))
+        # a non-PD candidate (Cat only, no observation noise): PosDefException on every
+        # rank, as select.jl's logpdf would raise; or NaN + info with raise_posdef=False
+        bad = [m + [(5, -1, 0.1, 1)] for m in models[:3]] + [[(4, 1, 0.0, 0)]]  # Noise terms keep 0..2 PD
+        try:
+            replicas.select_batch(_OracleCtx(), X, bad, 0.0, v)
+            raised = None
+        except PosDefException as e:
+            raised = e.info
+        bv, binfo = replicas.select_batch(_OracleCtx(), X, bad, 0.0, v, raise_posdef=False)
+        q.put((rank, res.tolist(), vals.tolist(), raised, binfo.tolist(), bool(np.isnan(bv[3]))))
     finally:
         dist.destroy_process_group()
 
@@ -84,6 +94,10 @@ def test_gloo_world2_select_batch_matches_single_process():
     models = [[(1, 0, l, 0)] for l in (0.5, 1.0, 2.0, 4.0)] + [[(2, 0, 1.0, 0), (4, 1, 0.0, 1)],
                                                              [(4, 1, 0.0, 0)], [(3, 0, 0.5, 0)]]
     expect = [R.logpdf(X, m, 0.1, v)[0] for m in models]
-    for rank, res, vals in got:
+    with pytest.raises(R.PosDefException) as ref:
+        R.logpdf(X, [(4, 1, 0.0, 0)], 0.0, v)
+    for rank, res, vals, raised, binfo, isnan in got:
         assert np.allclose(res, expect, rtol=1e-12, atol=0)
         assert vals == [0.0, 10.0, 20.0, 30.0, 40.0]
+        assert raised == ref.value.info
+        assert binfo[:3] == [0, 0, 0] and binfo[3] == ref.value.info and isnan

@@ -1,0 +1,60 @@
+"""Launch-footprint guard, on the CPU: gaplac_plan_check walks the real
+host schedule of one evaluation without a device — every launch gaplac_logpdf /
+gaplac_logpdf_grad / gaplac_posterior_mean_var would enqueue — and checks the element
+range each launch's grid touches (derived from the same tile counts and decodes as the
+kernels) against the workspace the context allocates. The sweep covers N = 1..300, where
+the round-1 fault lived (the second Gram launch's tile count for N < 255), the padding
+edges and larger orders; the negative control shrinks the workspace by one element, which
+the last Gram tile must hit.
+"""
+import ctypes
+
+import pytest
+
+from gaplac_amd import _native
+
+SIZES = list(range(1, 301)) + [383, 384, 385, 511, 512, 513, 1000, 2047, 4095, 4096, 4097, 16384, 65536]
+
+
+def plan(N, mode, M=0, spw=4):
+    lib = _native.load()
+    launches, violations = ctypes.c_int64(), ctypes.c_int64()
+    msg = ctypes.create_string_buffer(256)
+    rc = lib.gaplac_plan_check(N, mode, M, spw, ctypes.byref(launches), ctypes.byref(violations), msg, 256)
+    assert rc == 0, (N, mode, M, spw, rc)
+    return launches.value, violations.value, msg.value.decode()
+
+
+@pytest.mark.parametrize("spw", [1, 2, 4, 5, 8])
+@pytest.mark.parametrize("mode,M", [(0, 0), (1, 0), (2, 1), (2, 130), (2, 1000)])
+def test_every_launch_inside_the_workspace(mode, M, spw):
+    for N in SIZES:
+        if mode == 1 and N > 16384:
+            continue  # the gradient's identity rows double the workspace; 64k is covered by logpdf
+        launches, violations, msg = plan(N, mode, M, spw)
+        assert launches > 0
+        assert violations == 0, (N, mode, M, spw, msg)
+
+
+def test_launch_counts_follow_the_schedule():
+    # N = 16384 (nt = 129): one diagonal block per tile column plus TRSMs, column updates,
+    # bulk updates, the Gram in two parts and the reduction
+    l0, v0, _ = plan(16384, 0)
+    assert v0 == 0 and 129 * 3 < l0 < 129 * 6
+    l1, _, _ = plan(16384, 1)
+    assert l1 > l0  # the gradient adds the identity-row launches and the C^-1 tiles
+
+
+@pytest.mark.parametrize("N", [1, 127, 128, 129, 254, 255, 300, 4096])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_negative_control_short_workspace_is_reported(N, mode):
+    launches, violations, msg = plan(N, mode + 8, M=64 if mode == 2 else 0)
+    assert violations >= 1
+    assert "outside" not in msg and "touches elements" in msg
+
+
+def test_bad_arguments():
+    lib = _native.load()
+    z = ctypes.c_int64()
+    for args in ((0, 0, 0, 4), (10, 3, 0, 4), (10, 2, 0, 4), (10, 0, 0, 0), (10, 0, 0, 9)):
+        assert lib.gaplac_plan_check(*args, ctypes.byref(z), ctypes.byref(z), None, 0) == _native.E_ARG
