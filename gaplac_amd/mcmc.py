@@ -41,6 +41,30 @@ ELL_LO, ELL_HI = 0.0, 20.0  # ℓ ~ Uniform(0, 20)
 NOISE_VAR = 0.1             # FiniteGP(GP(gp), RowVecs(X), 0.1)
 
 
+class GradMemo:
+    """The last gaplac_logpdf_grad result, keyed on the primal inputs.
+
+    ForwardDiff evaluates the log density of a NUTS step in ceil((N+1)/chunk) chunked Dual
+    passes whose primal values (ℓ and fx) are identical; only the seeded partials differ.
+    The Julia glue answers every pass from ONE library call through
+    this memo; this is its Python mirror. `calls` counts library calls."""
+
+    def __init__(self):
+        self.key = None
+        self.v = None
+        self.val = None
+        self.calls = 0
+
+    def __call__(self, ctx, X, terms, noise: float, v):
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        key = (X.ctypes.data, X.shape, tuple(map(tuple, terms)), float(noise), hash(v.tobytes()))
+        if key != self.key or self.v is None or not np.array_equal(v, self.v):
+            self.val = ctx.logpdf_grad(X, terms, noise, v)
+            self.key, self.v = key, v.copy()
+            self.calls += 1
+        return self.val
+
+
 class MCMCModel:
     """inference_engine(y, x, formula, inferable) of CLI/src/mcmc.jl:31-39 on a table."""
 
@@ -53,6 +77,7 @@ class MCMCModel:
         self.y = np.asarray(table[F.response(spec)], dtype=np.float64)  # mcmc.jl:25
         self.X = AG.design_matrix(table, vars_)         # mcmc.jl:26 Matrix(df[!, vars])
         self.ctx = ctx
+        self.memo = GradMemo()
 
     @property
     def N(self) -> int:
@@ -85,7 +110,7 @@ class MCMCModel:
             return -math.inf, math.nan, np.full(self.N, math.nan)
         terms = self.terms(ell)
         ctx = self.ctx or backend.default_context()
-        lp_gp, dv, dparam, _ = ctx.logpdf_grad(self.X, terms, NOISE_VAR, fx)
+        lp_gp, dv, dparam, _ = self.memo(ctx, self.X, terms, NOISE_VAR, fx)
         r = self.y - fx
         lik = float(np.sum(-(LOG2PI + r * r) / 2))
         prior = -math.log(ELL_HI - ELL_LO)
@@ -101,3 +126,31 @@ class MCMCModel:
         lp_gp = ctx.logpdf(self.X, self.terms(ell), NOISE_VAR, fx)
         r = self.y - fx
         return -math.log(ELL_HI - ELL_LO) + lp_gp + float(np.sum(-(LOG2PI + r * r) / 2))
+
+    def dual_pass(self, ell: float, fx, d_ell, d_fx):
+        """One ForwardDiff chunk pass of the log joint: the value and its directional
+        derivatives along the seeded partials (d_ell: (k,), d_fx: (N, k)) — what the Julia
+        Dual method of INTEGRATION.md §1b returns, T(lp, ∂) with
+        ∂ = Σ_i dv_i ∂fx_i + Σ_t dparam_t ∂θ_t (+ the Normal likelihood's (y - fx)·∂fx).
+        Every pass at the same primal point reuses one library call (GradMemo)."""
+        lp, dell, dfx = self.logdensity_and_gradient(ell, fx)
+        d_ell = np.asarray(d_ell, dtype=np.float64)
+        d_fx = np.asarray(d_fx, dtype=np.float64)
+        return lp, dell * d_ell + dfx @ d_fx
+
+    def gradient_chunked(self, ell: float, fx, chunk: int = 12):
+        """ForwardDiff's chunked gradient over θ = (ℓ, fx) (Turing 0.21's default AD): one
+        dual_pass per chunk of `chunk` seeded inputs. Returns (lp, dℓ, dfx, passes)."""
+        fx = np.asarray(fx, dtype=np.float64)
+        n = self.N + 1
+        g = np.empty(n)
+        lp = None
+        passes = 0
+        for c0 in range(0, n, chunk):
+            k = min(chunk, n - c0)
+            seeds = np.zeros((n, k))
+            seeds[c0 + np.arange(k), np.arange(k)] = 1.0
+            lp, part = self.dual_pass(ell, fx, seeds[0], seeds[1:])
+            g[c0:c0 + k] = part
+            passes += 1
+        return lp, float(g[0]), g[1:], passes
