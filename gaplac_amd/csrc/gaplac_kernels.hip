@@ -55,6 +55,48 @@ __device__ __forceinline__ void kt_end(KTime* kt) {
     if (kt && (threadIdx.x & 63) == 0) atomicMax(&kt->end, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
+// ---------------------------------------------------------------------------------
+// CU-local priority for the critical path. Standalone the panel chain
+// (diagonal block, TRSM, column updates) costs ~3 ms of chip time per N=16384 evaluation,
+// but beside MFMA-saturating bulk waves on the same SIMDs it runs 2-4x slower and slows
+// the bulk update in turn. So chain waves announce themselves on their CU (a counter per
+// CU, indexed by XCC id and the SE/SH/CU bits of HW_ID; placement only, never correctness)
+// and the bulk waves of that CU step aside: they read the counter once per k-chunk (the
+// value is used one chunk later, so the load never stalls the MFMA stream) and, while a
+// chain wave is present, sleep in a bounded loop. Vector atomics only.
+// ---------------------------------------------------------------------------------
+__device__ int g_cu_busy[2048];
+
+__device__ __forceinline__ int cu_key() {
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // HW_REG_XCC_ID [3:0]
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);   // HW_REG_HW_ID
+    return (int)(((xcc & 7u) << 8) | ((hw >> 8) & 0xffu));  // CU_ID [11:8], SH_ID [12], SE_ID [15:13]
+}
+__device__ __forceinline__ void chain_enter() {
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(&g_cu_busy[cu_key()], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void chain_leave() {
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(&g_cu_busy[cu_key()], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int cu_busy_load(int key) {
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(&g_cu_busy[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// Bulk side: sleep while a chain wave shares this CU (bounded: ~2k cycles per round).
+__device__ __noinline__ void yield_to_chain(int key) {
+    for (int it = 0; it < 8192; ++it) {
+        __builtin_amdgcn_s_sleep(32);
+        if (cu_busy_load(key) <= 0) break;
+    }
+}
+// Which critical-path kernels claim their CU (bit mask): 1 diagonal block, 2 TRSM,
+// 4 column updates inside a super-panel (K = 128), 8 lookahead column update (K = 128 W).
+// Default 0 (off): measured at N = 16384 every setting is slower end to end (1: the
+// diagonal blocks drop from 7.85 to 4.46 ms per eval but the bulk update loses more,
+// 31.1 vs 30.7 ms; 15: 32.8 ms) -- DESIGN.md §3. Kept for the experiment (-DGAPLAC_YIELD=n).
+#ifndef GAPLAC_YIELD
+#define GAPLAC_YIELD 0
+#endif
+
 // Row-major triangular tile index: t = bi*(bi+1)/2 + bj, 0 <= bj <= bi.
 __device__ __forceinline__ void tri_index(int64_t t, int& bi, int& bj) {
     int b = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
@@ -62,6 +104,172 @@ __device__ __forceinline__ void tri_index(int64_t t, int& bi, int& bj) {
     while ((int64_t)b * (b + 1) / 2 > t) --b;
     bi = b;
     bj = (int)(t - (int64_t)b * (b + 1) / 2);
+}
+
+// ---------------------------------------------------------------------------------
+// exp(x) for the Gram kernel's arguments (x = -u^2/2 or -|u|, so x <= 0), table-driven:
+// x = (256 k + j) ln2/256 + r with |r| <~ ln2/512, exp(x) = 2^k 2^(j/256) (1 + p(r)),
+// p the degree-4 Taylor polynomial of exp(r) - 1 (truncation r^5/120 < 4e-17).
+// n = round(x 256/ln2) comes from the low word of x 256/ln2 + 1.5 2^52 (one fma; the
+// nearest integer to the exact product, so |r| may exceed ln2/512 by an ulp's worth),
+// ln2/256 is split Cody-Waite style into a 33-bit head (n * head exact for |n| < 2^20)
+// and a tail. 2^(j/256) is correctly rounded from a 60-digit evaluation (decimal module).
+// Within 1 ulp of the library exp (tools/exp_probe.hip, 2^27 points per range) at ~15
+// instead of ~30 VALU instructions: the multi-term Gram build is VALU-bound on its exps.
+// Results below 2^-1074 flush to 0 (x < -745.2); NaN propagates.
+// ---------------------------------------------------------------------------------
+__constant__ double kExp2Tbl256[256] = {
+    0x1.0000000000000p+0, 0x1.00b1afa5abcbfp+0, 0x1.0163da9fb3335p+0, 0x1.02168143b0281p+0,
+    0x1.02c9a3e778061p+0, 0x1.037d42e11bbccp+0, 0x1.04315e86e7f85p+0, 0x1.04e5f72f654b1p+0,
+    0x1.059b0d3158574p+0, 0x1.0650a0e3c1f89p+0, 0x1.0706b29ddf6dep+0, 0x1.07bd42b72a836p+0,
+    0x1.0874518759bc8p+0, 0x1.092bdf66607e0p+0, 0x1.09e3ecac6f383p+0, 0x1.0a9c79b1f3919p+0,
+    0x1.0b5586cf9890fp+0, 0x1.0c0f145e46c85p+0, 0x1.0cc922b7247f7p+0, 0x1.0d83b23395decp+0,
+    0x1.0e3ec32d3d1a2p+0, 0x1.0efa55fdfa9c5p+0, 0x1.0fb66affed31bp+0, 0x1.1073028d7233ep+0,
+    0x1.11301d0125b51p+0, 0x1.11edbab5e2ab6p+0, 0x1.12abdc06c31ccp+0, 0x1.136a814f204abp+0,
+    0x1.1429aaea92de0p+0, 0x1.14e95934f312ep+0, 0x1.15a98c8a58e51p+0, 0x1.166a45471c3c2p+0,
+    0x1.172b83c7d517bp+0, 0x1.17ed48695bbc0p+0, 0x1.18af9388c8deap+0, 0x1.1972658375d2fp+0,
+    0x1.1a35beb6fcb75p+0, 0x1.1af99f8138a1cp+0, 0x1.1bbe084045cd4p+0, 0x1.1c82f95281c6bp+0,
+    0x1.1d4873168b9aap+0, 0x1.1e0e75eb44027p+0, 0x1.1ed5022fcd91dp+0, 0x1.1f9c18438ce4dp+0,
+    0x1.2063b88628cd6p+0, 0x1.212be3578a819p+0, 0x1.21f49917ddc96p+0, 0x1.22bdda27912d1p+0,
+    0x1.2387a6e756238p+0, 0x1.2451ffb82140ap+0, 0x1.251ce4fb2a63fp+0, 0x1.25e85711ece75p+0,
+    0x1.26b4565e27cddp+0, 0x1.2780e341ddf29p+0, 0x1.284dfe1f56381p+0, 0x1.291ba7591bb70p+0,
+    0x1.29e9df51fdee1p+0, 0x1.2ab8a66d10f13p+0, 0x1.2b87fd0dad990p+0, 0x1.2c57e39771b2fp+0,
+    0x1.2d285a6e4030bp+0, 0x1.2df961f641589p+0, 0x1.2ecafa93e2f56p+0, 0x1.2f9d24abd886bp+0,
+    0x1.306fe0a31b715p+0, 0x1.31432edeeb2fdp+0, 0x1.32170fc4cd831p+0, 0x1.32eb83ba8ea32p+0,
+    0x1.33c08b26416ffp+0, 0x1.3496266e3fa2dp+0, 0x1.356c55f929ff1p+0, 0x1.36431a2de883bp+0,
+    0x1.371a7373aa9cbp+0, 0x1.37f26231e754ap+0, 0x1.38cae6d05d866p+0, 0x1.39a401b7140efp+0,
+    0x1.3a7db34e59ff7p+0, 0x1.3b57fbfec6cf4p+0, 0x1.3c32dc313a8e5p+0, 0x1.3d0e544ede173p+0,
+    0x1.3dea64c123422p+0, 0x1.3ec70df1c5175p+0, 0x1.3fa4504ac801cp+0, 0x1.40822c367a024p+0,
+    0x1.4160a21f72e2ap+0, 0x1.423fb2709468ap+0, 0x1.431f5d950a897p+0, 0x1.43ffa3f84b9d4p+0,
+    0x1.44e086061892dp+0, 0x1.45c2042a7d232p+0, 0x1.46a41ed1d0057p+0, 0x1.4786d668b3237p+0,
+    0x1.486a2b5c13cd0p+0, 0x1.494e1e192aed2p+0, 0x1.4a32af0d7d3dep+0, 0x1.4b17dea6db7d7p+0,
+    0x1.4bfdad5362a27p+0, 0x1.4ce41b817c114p+0, 0x1.4dcb299fddd0dp+0, 0x1.4eb2d81d8abffp+0,
+    0x1.4f9b2769d2ca7p+0, 0x1.508417f4531eep+0, 0x1.516daa2cf6642p+0, 0x1.5257de83f4eefp+0,
+    0x1.5342b569d4f82p+0, 0x1.542e2f4f6ad27p+0, 0x1.551a4ca5d920fp+0, 0x1.56070dde910d2p+0,
+    0x1.56f4736b527dap+0, 0x1.57e27dbe2c4cfp+0, 0x1.58d12d497c7fdp+0, 0x1.59c0827ff07ccp+0,
+    0x1.5ab07dd485429p+0, 0x1.5ba11fba87a03p+0, 0x1.5c9268a5946b7p+0, 0x1.5d84590998b93p+0,
+    0x1.5e76f15ad2148p+0, 0x1.5f6a320dceb71p+0, 0x1.605e1b976dc09p+0, 0x1.6152ae6cdf6f4p+0,
+    0x1.6247eb03a5585p+0, 0x1.633dd1d1929fdp+0, 0x1.6434634ccc320p+0, 0x1.652b9febc8fb7p+0,
+    0x1.6623882552225p+0, 0x1.671c1c70833f6p+0, 0x1.68155d44ca973p+0, 0x1.690f4b19e9538p+0,
+    0x1.6a09e667f3bcdp+0, 0x1.6b052fa75173ep+0, 0x1.6c012750bdabfp+0, 0x1.6cfdcddd47645p+0,
+    0x1.6dfb23c651a2fp+0, 0x1.6ef9298593ae5p+0, 0x1.6ff7df9519484p+0, 0x1.70f7466f42e87p+0,
+    0x1.71f75e8ec5f74p+0, 0x1.72f8286ead08ap+0, 0x1.73f9a48a58174p+0, 0x1.74fbd35d7cbfdp+0,
+    0x1.75feb564267c9p+0, 0x1.77024b1ab6e09p+0, 0x1.780694fde5d3fp+0, 0x1.790b938ac1cf6p+0,
+    0x1.7a11473eb0187p+0, 0x1.7b17b0976cfdbp+0, 0x1.7c1ed0130c132p+0, 0x1.7d26a62ff86f0p+0,
+    0x1.7e2f336cf4e62p+0, 0x1.7f3878491c491p+0, 0x1.80427543e1a12p+0, 0x1.814d2add106d9p+0,
+    0x1.82589994cce13p+0, 0x1.8364c1eb941f7p+0, 0x1.8471a4623c7adp+0, 0x1.857f4179f5b21p+0,
+    0x1.868d99b4492edp+0, 0x1.879cad931a436p+0, 0x1.88ac7d98a6699p+0, 0x1.89bd0a478580fp+0,
+    0x1.8ace5422aa0dbp+0, 0x1.8be05bad61778p+0, 0x1.8cf3216b5448cp+0, 0x1.8e06a5e0866d9p+0,
+    0x1.8f1ae99157736p+0, 0x1.902fed0282c8ap+0, 0x1.9145b0b91ffc6p+0, 0x1.925c353aa2fe2p+0,
+    0x1.93737b0cdc5e5p+0, 0x1.948b82b5f98e5p+0, 0x1.95a44cbc8520fp+0, 0x1.96bdd9a7670b3p+0,
+    0x1.97d829fde4e50p+0, 0x1.98f33e47a22a2p+0, 0x1.9a0f170ca07bap+0, 0x1.9b2bb4d53fe0dp+0,
+    0x1.9c49182a3f090p+0, 0x1.9d674194bb8d5p+0, 0x1.9e86319e32323p+0, 0x1.9fa5e8d07f29ep+0,
+    0x1.a0c667b5de565p+0, 0x1.a1e7aed8eb8bbp+0, 0x1.a309bec4a2d33p+0, 0x1.a42c980460ad8p+0,
+    0x1.a5503b23e255dp+0, 0x1.a674a8af46052p+0, 0x1.a799e1330b358p+0, 0x1.a8bfe53c12e59p+0,
+    0x1.a9e6b5579fdbfp+0, 0x1.ab0e521356ebap+0, 0x1.ac36bbfd3f37ap+0, 0x1.ad5ff3a3c2774p+0,
+    0x1.ae89f995ad3adp+0, 0x1.afb4ce622f2ffp+0, 0x1.b0e07298db666p+0, 0x1.b20ce6c9a8952p+0,
+    0x1.b33a2b84f15fbp+0, 0x1.b468415b749b1p+0, 0x1.b59728de5593ap+0, 0x1.b6c6e29f1c52ap+0,
+    0x1.b7f76f2fb5e47p+0, 0x1.b928cf22749e4p+0, 0x1.ba5b030a1064ap+0, 0x1.bb8e0b79a6f1fp+0,
+    0x1.bcc1e904bc1d2p+0, 0x1.bdf69c3f3a207p+0, 0x1.bf2c25bd71e09p+0, 0x1.c06286141b33dp+0,
+    0x1.c199bdd85529cp+0, 0x1.c2d1cd9fa652cp+0, 0x1.c40ab5fffd07ap+0, 0x1.c544778fafb22p+0,
+    0x1.c67f12e57d14bp+0, 0x1.c7ba88988c933p+0, 0x1.c8f6d9406e7b5p+0, 0x1.ca3405751c4dbp+0,
+    0x1.cb720dcef9069p+0, 0x1.ccb0f2e6d1675p+0, 0x1.cdf0b555dc3fap+0, 0x1.cf3155b5bab74p+0,
+    0x1.d072d4a07897cp+0, 0x1.d1b532b08c968p+0, 0x1.d2f87080d89f2p+0, 0x1.d43c8eacaa1d6p+0,
+    0x1.d5818dcfba487p+0, 0x1.d6c76e862e6d3p+0, 0x1.d80e316c98398p+0, 0x1.d955d71ff6075p+0,
+    0x1.da9e603db3285p+0, 0x1.dbe7cd63a8315p+0, 0x1.dd321f301b460p+0, 0x1.de7d5641c0658p+0,
+    0x1.dfc97337b9b5fp+0, 0x1.e11676b197d17p+0, 0x1.e264614f5a129p+0, 0x1.e3b333b16ee12p+0,
+    0x1.e502ee78b3ff6p+0, 0x1.e653924676d76p+0, 0x1.e7a51fbc74c83p+0, 0x1.e8f7977cdb740p+0,
+    0x1.ea4afa2a490dap+0, 0x1.eb9f4867cca6ep+0, 0x1.ecf482d8e67f1p+0, 0x1.ee4aaa2188510p+0,
+    0x1.efa1bee615a27p+0, 0x1.f0f9c1cb6412ap+0, 0x1.f252b376bba97p+0, 0x1.f3ac948dd7274p+0,
+    0x1.f50765b6e4540p+0, 0x1.f6632798844f8p+0, 0x1.f7bfdad9cbe14p+0, 0x1.f91d802243c89p+0,
+    0x1.fa7c1819e90d8p+0, 0x1.fbdba3692d514p+0, 0x1.fd3c22b8f71f1p+0, 0x1.fe9d96b2a23d9p+0};
+
+__device__ __forceinline__ double exp_nonpos(double x, const double* __restrict__ tbl) {
+    const double kd = fma(x, 0x1.71547652b82fep+8, 0x1.8p52);  // x * 256 / ln2 + 1.5 2^52
+    const int n = (int)(uint32_t)__double_as_longlong(kd);
+    const double nf = kd - 0x1.8p52;
+    double r = fma(-nf, 0x1.62e42fee00000p-9, x);
+    r = fma(-nf, 0x1.a39ef35793c76p-41, r);
+    double p = fma(r, 1.0 / 24.0, 1.0 / 6.0);
+    p = fma(p, r, 0.5);
+    p = p * r;
+    p = fma(p, r, r);  // exp(r) - 1
+    const double t = tbl[n & 255];
+    const double y = __builtin_ldexp(fma(t, p, t), n >> 8);
+    return x < -745.2 ? 0.0 : y;
+}
+
+// ---------------------------------------------------------------------------------
+// Gram term evaluation, specialised at compile time on the term kind and on how the term
+// combines with its group (KernelProduct inside a group, KernelSum across groups):
+//   GM_SUM_FIRST  singleton group, first group      tot  = k
+//   GM_SUM        singleton group                   tot += k
+//   GM_PR_FIRST   first term of a product group     pr   = k
+//   GM_PR         inner term of a product group     pr  *= k
+//   GM_PR_LAST0   last term, first group            tot  = pr * k
+//   GM_PR_LAST    last term                         tot += pr * k
+// which is the left fold tot = 0 + (1 * k1 * k2 ...) + ... without the exact no-op
+// operations (1 * k = k, 0 + x = x): the same values, ~2 VALU instructions per element
+// and term fewer for the common all-singleton formulas (configs[2]: SqExp + OU + Cat).
+// ---------------------------------------------------------------------------------
+enum GramMode { GM_SUM_FIRST, GM_SUM, GM_PR_FIRST, GM_PR, GM_PR_LAST0, GM_PR_LAST };
+#ifndef GAPLAC_GRAM_CB
+#define GAPLAC_GRAM_CB 4
+#endif
+constexpr int GRAM_CB = GAPLAC_GRAM_CB;  // tile columns per batch and wave
+
+template <int KIND>
+__device__ __forceinline__ double gram_term(double xi, double xj, double p, int64_t i, int64_t j,
+                                            const double* __restrict__ etbl) {
+#pragma clang fp contract(off)
+    if constexpr (KIND == GAPLAC_SQEXP) {
+        const double d = xi - xj;  // coordinates pre-scaled by p = 1/l
+        return exp_nonpos(-(d * d) * 0.5, etbl);
+    } else if constexpr (KIND == GAPLAC_OU) {
+        return exp_nonpos(-fabs(xi - xj), etbl);
+    } else if constexpr (KIND == GAPLAC_LINEAR) {
+        return xi * xj + p;
+    } else if constexpr (KIND == GAPLAC_CAT) {
+        return (xi == xj) ? 1.0 : 0.0;
+    } else {  // GAPLAC_NOISE: index identity
+        return (i == j) ? p : 0.0;
+    }
+}
+
+template <int KIND, int MODE>
+__device__ __forceinline__ void gram_batch(double (&tot0)[GRAM_CB], double (&tot1)[GRAM_CB],
+                                           double (&pr0)[GRAM_CB], double (&pr1)[GRAM_CB],
+                                           const double* __restrict__ xc, double2 xr, double p,
+                                           int64_t i0, int64_t j0, const double* __restrict__ etbl) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int q = 0; q < GRAM_CB; ++q) {
+        const double xj = xc[4 * q];
+        const int64_t j = j0 + 4 * q;
+        const double k0 = gram_term<KIND>(xr.x, xj, p, i0, j, etbl);
+        const double k1 = gram_term<KIND>(xr.y, xj, p, i0 + 1, j, etbl);
+        if constexpr (MODE == GM_SUM_FIRST) { tot0[q] = k0; tot1[q] = k1; }
+        else if constexpr (MODE == GM_SUM) { tot0[q] += k0; tot1[q] += k1; }
+        else if constexpr (MODE == GM_PR_FIRST) { pr0[q] = k0; pr1[q] = k1; }
+        else if constexpr (MODE == GM_PR) { pr0[q] *= k0; pr1[q] *= k1; }
+        else if constexpr (MODE == GM_PR_LAST0) { tot0[q] = pr0[q] * k0; tot1[q] = pr1[q] * k1; }
+        else { tot0[q] += pr0[q] * k0; tot1[q] += pr1[q] * k1; }
+    }
+}
+
+template <int KIND>
+__device__ __forceinline__ void gram_batch_mode(int mode, double (&tot0)[GRAM_CB], double (&tot1)[GRAM_CB],
+                                                double (&pr0)[GRAM_CB], double (&pr1)[GRAM_CB],
+                                                const double* __restrict__ xc, double2 xr, double p,
+                                                int64_t i0, int64_t j0, const double* __restrict__ etbl) {
+    switch (mode) {
+        case GM_SUM_FIRST: gram_batch<KIND, GM_SUM_FIRST>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        case GM_SUM: gram_batch<KIND, GM_SUM>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        case GM_PR_FIRST: gram_batch<KIND, GM_PR_FIRST>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        case GM_PR: gram_batch<KIND, GM_PR>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        case GM_PR_LAST0: gram_batch<KIND, GM_PR_LAST0>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        default: gram_batch<KIND, GM_PR_LAST>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -87,97 +295,107 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
     const TermPack& tp = *tpp;  // uniform: scalar loads (device copy refreshed per eval)
     const double noise = tp.noise;
     const int64_t r0 = (int64_t)bi * NB, c0 = (int64_t)bj * NB;
+    // Coordinates of the tile's columns (xcol) and rows (xrow) per term, staged once.
+    // SqExp / OU coordinates are stored already scaled (p * x, rounded exactly as the
+    // in-loop product would be); Linear / Cat keep the raw coordinate.
     __shared__ double xcol[GAPLAC_MAX_TERMS][NB];
+    __shared__ double xrow[GAPLAC_MAX_TERMS][NB];
     __shared__ double vcol[NB];
+    __shared__ double etbl[256];
     const int tid = threadIdx.x;
     const int T = tp.T;
-    for (int idx = tid; idx < T * NB; idx += 256) {
-        const int t = idx / NB, c = idx % NB;
-        const int64_t j = c0 + c;
-        double val = 0.0;
-        if (j < N && tp.kind[t] != GAPLAC_NOISE) val = X[(int64_t)tp.col[t] * ldx + j];
-        xcol[t][c] = val;
-    }
-    if (tid < NB) {
-        const int64_t j = c0 + tid;
-        vcol[tid] = (j < N) ? v[j] : 0.0;
-    }
-    const int lane = tid & 63, w = tid >> 6;
-    const int64_t i0 = r0 + 2 * lane, i1 = i0 + 1;
-    double xa[GAPLAC_MAX_TERMS], xb[GAPLAC_MAX_TERMS];
+    // Staging: thread tid owns coordinate slot c = tid % NB of the columns (tid < NB) or
+    // the rows (tid >= NB); the term index is uniform (scalar TermPack loads) and every
+    // global load is issued before the first one is consumed (one latency per tile).
+    {
+        const int c = tid & (NB - 1);
+        const bool is_row = tid >= NB;
+        const int64_t j = (is_row ? r0 : c0) + c;
+        const bool in = j < N;
+        const double e = kExp2Tbl256[tid];
+        const double vj = (!is_row && in) ? v[j] : 0.0;
+        double val[GAPLAC_MAX_TERMS];
 #pragma unroll
-    for (int t = 0; t < GAPLAC_MAX_TERMS; ++t) {
-        xa[t] = 0.0;
-        xb[t] = 0.0;
-        if (t < T && tp.kind[t] != GAPLAC_NOISE) {
-            const double* xc = X + (int64_t)tp.col[t] * ldx;
-            if (i0 < N) xa[t] = xc[i0];
-            if (i1 < N) xb[t] = xc[i1];
+        for (int t = 0; t < GAPLAC_MAX_TERMS; ++t) {
+            val[t] = 0.0;
+            if (t < T && in && tp.kind[t] != GAPLAC_NOISE) val[t] = X[(int64_t)tp.col[t] * ldx + j];
         }
-    }
-    __syncthreads();
-
-    for (int cc = w; cc < NB; cc += 4) {
-        const int64_t j = c0 + cc;
-        double tot0 = 0.0, tot1 = 0.0, pr0 = 1.0, pr1 = 1.0;
+        etbl[tid] = e;
+        if (!is_row) vcol[c] = vj;
+        double (*dst)[NB] = is_row ? xrow : xcol;
 #pragma unroll
         for (int t = 0; t < GAPLAC_MAX_TERMS; ++t) {
             if (t < T) {
-                const double xj = xcol[t][cc];
-                const double p = tp.p[t];
-                double k0, k1;
-                switch (tp.kind[t]) {
-                    case GAPLAC_SQEXP: {
-                        const double sj = p * xj;
-                        const double d0 = p * xa[t] - sj, d1 = p * xb[t] - sj;
-                        k0 = exp(-(d0 * d0) * 0.5);
-                        k1 = exp(-(d1 * d1) * 0.5);
-                        break;
-                    }
-                    case GAPLAC_OU: {
-                        const double sj = p * xj;
-                        k0 = exp(-fabs(p * xa[t] - sj));
-                        k1 = exp(-fabs(p * xb[t] - sj));
-                        break;
-                    }
-                    case GAPLAC_LINEAR:
-                        k0 = xa[t] * xj + p;
-                        k1 = xb[t] * xj + p;
-                        break;
-                    case GAPLAC_CAT:
-                        k0 = (xa[t] == xj) ? 1.0 : 0.0;
-                        k1 = (xb[t] == xj) ? 1.0 : 0.0;
-                        break;
-                    default:  // GAPLAC_NOISE
-                        k0 = (i0 == j) ? p : 0.0;
-                        k1 = (i1 == j) ? p : 0.0;
-                        break;
-                }
-                pr0 *= k0;
-                pr1 *= k1;
-                if (tp.last_in_group[t]) {
-                    tot0 += pr0;
-                    tot1 += pr1;
-                    pr0 = 1.0;
-                    pr1 = 1.0;
-                }
+                const int kind = tp.kind[t];
+                dst[t][c] = (kind == GAPLAC_SQEXP || kind == GAPLAC_OU) ? tp.p[t] * val[t] : val[t];
             }
         }
-        double o0, o1;
-        if (j < N) {
-            o0 = (i0 < N) ? tot0 + ((i0 == j) ? noise : 0.0) : ((i0 == N) ? vcol[cc] : 0.0);
-            o1 = (i1 < N) ? tot1 + ((i1 == j) ? noise : 0.0) : ((i1 == N) ? vcol[cc] : 0.0);
-        } else {
-            o0 = 0.0;
-            o1 = 0.0;
+    }
+    const int lane = tid & 63, w = tid >> 6;
+    const int64_t i0 = r0 + 2 * lane, i1 = i0 + 1;
+    __syncthreads();
+
+    // Wave w: tile columns cc = w + 4 (cb + q), in batches of GRAM_CB columns. Kind and
+    // group position are switched on once per term and batch (uniform branches); each
+    // term gives 2 GRAM_CB independent evaluations for the VALU pipeline to overlap.
+    // Off the diagonal a singleton Noise group is all zeros and is skipped; interior
+    // off-diagonal tiles (no padding row/column, no diagonal, no v row) store the sums
+    // as they are.
+    const bool diag_tile = bi == bj;
+    const bool plain = !diag_tile && r0 + NB <= N && c0 + NB <= N;
+    for (int cb = 0; cb < NB / 4; cb += GRAM_CB) {
+        double tot0[GRAM_CB], tot1[GRAM_CB], pr0[GRAM_CB], pr1[GRAM_CB];
+        bool have_tot = false;
+        const int j0l = w + 4 * cb;  // tile column of q = 0
+        for (int t = 0; t < T; ++t) {
+            const int kind = tp.kind[t];
+            const bool first = t == 0 || tp.last_in_group[t - 1];
+            const bool last = tp.last_in_group[t];
+            if (kind == GAPLAC_NOISE && first && last && !diag_tile) continue;
+            const int mode = first ? (last ? (have_tot ? GM_SUM : GM_SUM_FIRST) : GM_PR_FIRST)
+                                   : (last ? (have_tot ? GM_PR_LAST : GM_PR_LAST0) : GM_PR);
+            have_tot = have_tot || last;
+            const double p = tp.p[t];
+            const double* xc = &xcol[t][j0l];
+            const double2 xr = *reinterpret_cast<const double2*>(&xrow[t][2 * lane]);
+            const int64_t j0 = c0 + j0l;
+            switch (kind) {
+                case GAPLAC_SQEXP: gram_batch_mode<GAPLAC_SQEXP>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                case GAPLAC_OU: gram_batch_mode<GAPLAC_OU>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                case GAPLAC_LINEAR: gram_batch_mode<GAPLAC_LINEAR>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                case GAPLAC_CAT: gram_batch_mode<GAPLAC_CAT>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                default: gram_batch_mode<GAPLAC_NOISE>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+            }
         }
-        *reinterpret_cast<double2*>(Ccol + (int64_t)cc * lda + i0) = make_double2(o0, o1);
+        if (!have_tot) {
+#pragma unroll
+            for (int q = 0; q < GRAM_CB; ++q) tot0[q] = tot1[q] = 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < GRAM_CB; ++q) {
+            const int cc = j0l + 4 * q;
+            const int64_t j = c0 + cc;
+            double o0 = tot0[q], o1 = tot1[q];
+            if (!plain) {
+                if (j < N) {
+                    o0 = (i0 < N) ? o0 + ((i0 == j) ? noise : 0.0) : ((i0 == N) ? vcol[cc] : 0.0);
+                    o1 = (i1 < N) ? o1 + ((i1 == j) ? noise : 0.0) : ((i1 == N) ? vcol[cc] : 0.0);
+                } else {
+                    o0 = 0.0;
+                    o1 = 0.0;
+                }
+            }
+#ifdef GAPLAC_GRAM_NOSTORE  // tools/gram_probe: compute-only timing (never true for real data)
+            if (o0 == 1.2345e300)
+#endif
+            *reinterpret_cast<double2*>(Ccol + (int64_t)cc * lda + i0) = make_double2(o0, o1);
+        }
     }
 }
 
 // Single-GPU layout. part 1: the first w tile columns; part 2: the lower triangle of tile
 // blocks w..nt-1; part 0: everything.
-__global__ __launch_bounds__(256) void gram_kernel(double* __restrict__ A, int64_t lda,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gram_kernel(double* __restrict__ A, int64_t lda,
                                                    int64_t N, const double* __restrict__ X,
                                                    int64_t ldx, const double* __restrict__ v,
                                                    const TermPack* __restrict__ tpp, int nt, int part, int w0,
@@ -202,7 +420,7 @@ __global__ __launch_bounds__(256) void gram_kernel(double* __restrict__ A, int64
 }
 
 // Distributed layout: tiles[b] = bi | lj << 16 (global row block, local tile column).
-__global__ __launch_bounds__(256) void gram_list_kernel(double* __restrict__ C, int64_t ldc, int64_t N,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gram_list_kernel(double* __restrict__ C, int64_t ldc, int64_t N,
                                                         const double* __restrict__ X, int64_t ldx,
                                                         const double* __restrict__ v,
                                                         const TermPack* __restrict__ tpp,
@@ -612,10 +830,12 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ Ag
                                                          EvalResult* __restrict__ res,
                                                          KTime* __restrict__ kt) {
     kt_begin(kt);
+    if (GAPLAC_YIELD & 1) chain_enter();
     if constexpr (GAPLAC_DIAG_V1)
         potrf_diag_kernel_body(Ag, lda, N, g0, Dinv, res);
     else
         potrf_diag_blocked_body(Ag, lda, N, g0, Dinv, res);
+    if (GAPLAC_YIELD & 1) chain_leave();
     kt_end(kt);
 }
 
@@ -703,7 +923,9 @@ __global__ __launch_bounds__(256) void trsm_subst_kernel(
                                                          int bi0, const double* __restrict__ Dinv,
                                                          KTime* __restrict__ kt) {
     kt_begin(kt);
+    if (GAPLAC_YIELD & 2) chain_enter();
     trsm_subst_kernel_body(Acol, lda, k, bi0, Dinv);
+    if (GAPLAC_YIELD & 2) chain_leave();
     kt_end(kt);
 }
 
@@ -764,7 +986,8 @@ __device__ __forceinline__ void tile_decode(const BulkArgs& a, int idx, int& bi,
 // entry (row 64 wi + 16 mi + (lane & 15), column 64 wj + 16 mj + (lane >> 4) + 4 rg).
 // Inactive waves (upper quadrant of a diagonal tile) only help with the staging.
 __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const double* __restrict__ Q,
-                                             int64_t ldp, int kdepth, bool active, d4 (&acc)[4][4]) {
+                                             int64_t ldp, int kdepth, bool active, d4 (&acc)[4][4],
+                                             bool yield = false) {
     __shared__ double sm[2][2][KB][LR];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wi = w & 1, wj = w >> 1;
@@ -809,9 +1032,15 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
     GAPLAC_LSTORE(0);
     __syncthreads();
     const int NCH = kdepth / KB;
+    const int key = (GAPLAC_YIELD && yield) ? cu_key() : 0;
+    int busy = 0;  // this CU's chain-wave count, read one chunk earlier
     for (int ch = 0; ch < NCH; ++ch) {
         const int buf = ch & 1;
         const bool more = ch + 1 < NCH;
+        if (GAPLAC_YIELD && yield) {
+            if (busy > 0) yield_to_chain(key);
+            busy = cu_busy_load(key);
+        }
         if (more) GAPLAC_GLOAD(ch + 1);
         if (active) {
 #pragma unroll
@@ -866,7 +1095,7 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a) {
                     acc[mi][mj][rg] = Ci[(int64_t)(64 * wj + 16 * mj + fr + 4 * rg) * ldc];
         }
     }
-    tile_mma_neg(P, Q, a.pn.ld, a.kdepth, active, acc);
+    tile_mma_neg(P, Q, a.pn.ld, a.kdepth, active, acc, true);
     if (!active) return;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
@@ -1112,6 +1341,8 @@ __global__ __launch_bounds__(256) void col_update_kernel(double* __restrict__ C,
                                                          int jb0, int lj0, int m0, int kdepth,
                                                          KTime* __restrict__ kt) {
     kt_begin(kt);
+    const bool claim = (GAPLAC_YIELD & (kdepth <= NB ? 4 : 8)) != 0;
+    if (claim) chain_enter();
     __builtin_amdgcn_s_setprio(2);
     const int q = (int)blockIdx.x & 3;
     int t = (int)blockIdx.x >> 2, c = 0;
@@ -1121,6 +1352,7 @@ __global__ __launch_bounds__(256) void col_update_kernel(double* __restrict__ C,
     }
     const int jb = jb0 + c, bi = jb + t, qi = q >> 1, qj = q & 1;
     if (!(bi == jb && qj > qi)) quad_update(C, ldc, pn, bi, jb, lj0 + c, qi, qj, kdepth);
+    if (claim) chain_leave();
     kt_end(kt);
 }
 
