@@ -223,8 +223,8 @@ __device__ __forceinline__ double gram_term(double xi, double xj, double p, int6
                                             const double* __restrict__ etbl) {
 #pragma clang fp contract(off)
     if constexpr (KIND == GAPLAC_SQEXP) {
-        const double d = xi - xj;  // coordinates pre-scaled by p = 1/l
-        return exp_nonpos(-(d * d) * 0.5, etbl);
+        const double d = xi - xj;  // coordinates pre-scaled by (1/l)/sqrt(2)
+        return exp_nonpos(-(d * d), etbl);
     } else if constexpr (KIND == GAPLAC_OU) {
         return exp_nonpos(-fabs(xi - xj), etbl);
     } else if constexpr (KIND == GAPLAC_LINEAR) {
@@ -296,8 +296,9 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
     const double noise = tp.noise;
     const int64_t r0 = (int64_t)bi * NB, c0 = (int64_t)bj * NB;
     // Coordinates of the tile's columns (xcol) and rows (xrow) per term, staged once.
-    // SqExp / OU coordinates are stored already scaled (p * x, rounded exactly as the
-    // in-loop product would be); Linear / Cat keep the raw coordinate.
+    // SqExp / OU coordinates are stored already scaled (OU: p * x, rounded exactly as
+    // KernelFunctions' ScaleTransform; SqExp: by p/sqrt(2), within an ulp of it);
+    // Linear / Cat keep the raw coordinate.
     __shared__ double xcol[GAPLAC_MAX_TERMS][NB];
     __shared__ double xrow[GAPLAC_MAX_TERMS][NB];
     __shared__ double vcol[NB];
@@ -327,7 +328,10 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
         for (int t = 0; t < GAPLAC_MAX_TERMS; ++t) {
             if (t < T) {
                 const int kind = tp.kind[t];
-                dst[t][c] = (kind == GAPLAC_SQEXP || kind == GAPLAC_OU) ? tp.p[t] * val[t] : val[t];
+                // SqExp: scaled by (1/l)/sqrt(2), so the kernel is exp(-d^2) (one multiply
+                // fewer per element; equal coordinates still give exactly d = 0).
+                const double sc = kind == GAPLAC_SQEXP ? tp.p[t] * 0x1.6a09e667f3bcdp-1 : tp.p[t];
+                dst[t][c] = (kind == GAPLAC_SQEXP || kind == GAPLAC_OU) ? sc * val[t] : val[t];
             }
         }
     }
@@ -340,13 +344,85 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
     // term gives 2 GRAM_CB independent evaluations for the VALU pipeline to overlap.
     // Off the diagonal a singleton Noise group is all zeros and is skipped; interior
     // off-diagonal tiles (no padding row/column, no diagonal, no v row) store the sums
-    // as they are.
+    // as they are. Formulas whose groups are all single terms (the common case) take a
+    // path with one running sum and no group bookkeeping.
     const bool diag_tile = bi == bj;
     const bool plain = !diag_tile && r0 + NB <= N && c0 + NB <= N;
+    bool all_single = true;
+    for (int t = 0; t < T; ++t) all_single = all_single && tp.last_in_group[t];
+    // Stores through a buffer resource over the tile's columns: the lane's row offset is
+    // the voffset, the wave-uniform column offset the soffset (no per-store 64-bit address
+    // arithmetic). The descriptor inputs are made provably uniform (readfirstlane).
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const uint64_t tbase = (uint64_t)(Ccol + r0);
+    const int64_t span = ((int64_t)(NB - 1) * lda + NB) * 8;
+    const bool use_buf = span < ((int64_t)1 << 31);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((uint64_t)__builtin_amdgcn_readfirstlane((unsigned)(tbase >> 32)) << 32) |
+                (uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)tbase)),
+        0, use_buf ? (int)span : 0, 0x00020000);
+    auto store2 = [&](int cc, double o0, double o1) {
+#ifdef GAPLAC_GRAM_NOSTORE  // tools/gram_probe: compute-only timing (never true for real data)
+        if (o0 != 1.2345e300) return;
+#endif
+        if (use_buf) {
+            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+            const double2 d = make_double2(o0, o1);
+            u32x4 bits;
+            __builtin_memcpy(&bits, &d, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, 16 * lane,
+                                                   __builtin_amdgcn_readfirstlane((int)((int64_t)cc * lda * 8)), 0);
+        } else {
+            *reinterpret_cast<double2*>(Ccol + (int64_t)cc * lda + i0) = make_double2(o0, o1);
+        }
+    };
+    auto store_batch = [&](int j0l, const double (&tot0)[GRAM_CB], const double (&tot1)[GRAM_CB]) {
+#pragma unroll
+        for (int q = 0; q < GRAM_CB; ++q) {
+            const int cc = j0l + 4 * q;
+            const int64_t j = c0 + cc;
+            double o0 = tot0[q], o1 = tot1[q];
+            if (!plain) {
+                if (j < N) {
+                    o0 = (i0 < N) ? o0 + ((i0 == j) ? noise : 0.0) : ((i0 == N) ? vcol[cc] : 0.0);
+                    o1 = (i1 < N) ? o1 + ((i1 == j) ? noise : 0.0) : ((i1 == N) ? vcol[cc] : 0.0);
+                } else {
+                    o0 = 0.0;
+                    o1 = 0.0;
+                }
+            }
+            store2(cc, o0, o1);
+        }
+    };
+    if (all_single) {
+        for (int cb = 0; cb < NB / 4; cb += GRAM_CB) {
+            double tot0[GRAM_CB], tot1[GRAM_CB], pr0[GRAM_CB], pr1[GRAM_CB];
+#pragma unroll
+            for (int q = 0; q < GRAM_CB; ++q) tot0[q] = tot1[q] = 0.0;  // 0 + k = k
+            const int j0l = wu + 4 * cb;
+            for (int t = 0; t < T; ++t) {
+                const int kind = tp.kind[t];
+                if (kind == GAPLAC_NOISE && !diag_tile) continue;
+                const double p = tp.p[t];
+                const double* xc = &xcol[t][j0l];
+                const double2 xr = *reinterpret_cast<const double2*>(&xrow[t][2 * lane]);
+                const int64_t j0 = c0 + j0l;
+                switch (kind) {
+                    case GAPLAC_SQEXP: gram_batch<GAPLAC_SQEXP, GM_SUM>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                    case GAPLAC_OU: gram_batch<GAPLAC_OU, GM_SUM>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                    case GAPLAC_LINEAR: gram_batch<GAPLAC_LINEAR, GM_SUM>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                    case GAPLAC_CAT: gram_batch<GAPLAC_CAT, GM_SUM>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                    default: gram_batch<GAPLAC_NOISE, GM_SUM>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                }
+            }
+            store_batch(j0l, tot0, tot1);
+        }
+        return;
+    }
     for (int cb = 0; cb < NB / 4; cb += GRAM_CB) {
         double tot0[GRAM_CB], tot1[GRAM_CB], pr0[GRAM_CB], pr1[GRAM_CB];
         bool have_tot = false;
-        const int j0l = w + 4 * cb;  // tile column of q = 0
+        const int j0l = wu + 4 * cb;  // tile column of q = 0
         for (int t = 0; t < T; ++t) {
             const int kind = tp.kind[t];
             const bool first = t == 0 || tp.last_in_group[t - 1];
@@ -371,25 +447,7 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
 #pragma unroll
             for (int q = 0; q < GRAM_CB; ++q) tot0[q] = tot1[q] = 0.0;
         }
-#pragma unroll
-        for (int q = 0; q < GRAM_CB; ++q) {
-            const int cc = j0l + 4 * q;
-            const int64_t j = c0 + cc;
-            double o0 = tot0[q], o1 = tot1[q];
-            if (!plain) {
-                if (j < N) {
-                    o0 = (i0 < N) ? o0 + ((i0 == j) ? noise : 0.0) : ((i0 == N) ? vcol[cc] : 0.0);
-                    o1 = (i1 < N) ? o1 + ((i1 == j) ? noise : 0.0) : ((i1 == N) ? vcol[cc] : 0.0);
-                } else {
-                    o0 = 0.0;
-                    o1 = 0.0;
-                }
-            }
-#ifdef GAPLAC_GRAM_NOSTORE  // tools/gram_probe: compute-only timing (never true for real data)
-            if (o0 == 1.2345e300)
-#endif
-            *reinterpret_cast<double2*>(Ccol + (int64_t)cc * lda + i0) = make_double2(o0, o1);
-        }
+        store_batch(j0l, tot0, tot1);
     }
 }
 
