@@ -32,6 +32,7 @@ struct gaplac_ctx {
     // bulk updates of at most this many tiles wait for the step's lookahead column update
     // (GAPLAC_LA_FIRST): late in the factorisation the panel chain is the critical path
     int la_first = 0;
+    int yield_m = 0;  // bulk updates of trailing matrices of <= yield_m tile rows yield to the chain
     double* A = nullptr;
     size_t A_elems = 0;
     double* Dinv = nullptr;  // per diagonal block: 8 inverses of its 16x16 sub-blocks
@@ -423,9 +424,10 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_L[p & 1], 0));
         if (jb < nt) {
             const int m = nt - jb;
-            const BulkArgs ba{ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0},
-                              ctx->tiles + ctx->tile_off[(size_t)m], m * (m + 1) / 2, kd, jb, jb,
-                              ColMap{1, 0, W}};
+            BulkArgs ba{ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0},
+                        ctx->tiles + ctx->tile_off[(size_t)m], m * (m + 1) / 2, kd, jb, jb,
+                        ColMap{1, 0, W}};
+            ba.yield = (m <= ctx->yield_m && sp != sm) ? 1 : 0;
             const bool small = syrk_is_small(ba.ntiles);
             KTime* kt = small ? slot(ctx, 6, 0) : slot(ctx, 0, syrk_flops(m) * (kd / NB), syrk_bytes(m, kd));
             const bool ev = ctx->prof_mode == 2 && !small;
@@ -479,6 +481,16 @@ int ensure_tile_lists(gaplac_ctx* ctx, int nt) {
     return 0;
 }
 
+// Second Gram launch as a work queue with this many workgroups per CU, leaving room for
+// the panel chain (GAPLAC_GRAM_QUEUE; 0 = the plain grid, for A/B runs).
+static int gram_queue_mode() {
+    static const int k = [] {
+        const char* e = std::getenv("GAPLAC_GRAM_QUEUE");
+        return e ? std::max(0, std::min(4, std::atoi(e))) : 2;
+    }();
+    return k;
+}
+
 // Everything one evaluation puts on the streams (eager launch or graph capture): reset
 // the result record (and the profiling slots), Gram build, factorisation schedule,
 // reduction, result copy to the pinned host record. Inputs: ctx->dX (ld N), ctx->dv,
@@ -495,8 +507,12 @@ int enqueue_eval_body(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt)
     launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 1, ctx->spw,
                 slot(ctx, 1, bytes * frac));
     HIPQ(ctx, hipEventRecord(ctx->ev_gram, ctx->s_main));
-    launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 2, ctx->spw,
-                slot(ctx, 1, bytes * (1.0 - frac)));
+    if (gram_queue_mode())
+        launch_gram_queue(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, ctx->spw,
+                          gram_queue_mode(), ctx->dres, slot(ctx, 1, bytes * (1.0 - frac)));
+    else
+        launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 2, ctx->spw,
+                    slot(ctx, 1, bytes * (1.0 - frac)));
     HIPQ(ctx, hipEventRecord(ctx->ev_gram2, ctx->s_main));
     if (ctx->xr_mode == 1) launch_init_identity_rows(ctx->s_main, ctx->A, lda, Np, nt, ctx->spw);
     if (ctx->xr_mode == 2)
@@ -882,6 +898,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     ctx->device = device;
     if (const char* s = std::getenv("GAPLAC_SERIAL")) ctx->serial = s[0] == '1';
     if (const char* s = std::getenv("GAPLAC_LA_FIRST")) ctx->la_first = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_YIELD_M")) ctx->yield_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     auto fail = [&](const char* what, hipError_t e) {

@@ -34,6 +34,7 @@ struct EvalResult {
     double quad;
     unsigned long long info;  // min over failing pivots of (j+1); ULLONG_MAX = none
     double part[2][REDUCE_BLOCKS];  // per-workgroup partial sums of the reduction
+    unsigned gram_ticket;           // work queue of the second Gram launch (zeroed per eval)
 };
 
 // Per-launch device timestamps (profiling): 100 MHz s_memrealtime ticks.
@@ -75,6 +76,7 @@ struct BulkArgs {
     ColMap cm;
     int rect_rows = 0;
     int max_r = -1, max_c = -1;  // largest lo16 / hi16 list entry (-1: an m x m triangle list)
+    int yield = 0;  // step aside on CUs where panel-chain waves run
 };
 
 // Host-side footprint guard. Before launching, every launcher computes the
@@ -112,6 +114,10 @@ int pack_terms(int32_t D, int32_t T, const gaplac_term* terms, TermPack* tp, std
 // roundup(N+1, NB)): rows/cols 0..N-1 hold C, row N holds v^T.
 // part 0: all lower tiles; part 1: the first w tile columns; part 2: tiles with both
 // block indices >= w (parts 1 + 2 = part 0).
+// Tiles of part 2 as a work queue with per_cu workgroups per CU (room for the panel
+// chain beside them); res->gram_ticket must be zero (init_result_kernel) on the same stream.
+void launch_gram_queue(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const double* X, int64_t ldx,
+                       const double* v, const TermPack* dtp, int w, int per_cu, EvalResult* res, KTime* kt);
 void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt,
                  const double* X, int64_t ldx, const double* v, const TermPack* dtp, int part, int w,
                  KTime* kt);

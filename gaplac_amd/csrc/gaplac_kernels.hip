@@ -90,9 +90,12 @@ __device__ __noinline__ void yield_to_chain(int key) {
 }
 // Which critical-path kernels claim their CU (bit mask): 1 diagonal block, 2 TRSM,
 // 4 column updates inside a super-panel (K = 128), 8 lookahead column update (K = 128 W).
-// Default 0 (off): measured at N = 16384 every setting is slower end to end (1: the
-// diagonal blocks drop from 7.85 to 4.46 ms per eval but the bulk update loses more,
-// 31.1 vs 30.7 ms; 15: 32.8 ms) -- DESIGN.md §3. Kept for the experiment (-DGAPLAC_YIELD=n).
+// A claim is two relaxed atomics per wave and matters only to bulk launches that yield
+// (BulkArgs::yield, set by the host for trailing matrices of <= GAPLAC_YIELD_M tile rows).
+// Off by default: measured at N = 16384, yielding in every step is slower end to end (32.8
+// vs 30.7 ms: the bulk is the critical path while the trailing matrix is large), and
+// yielding only in the chain-bound steps (GAPLAC_YIELD_M = 40..100, claims 15) gains
+// nothing (30.6-31.9 vs 30.7 ms) -- DESIGN.md §3. Build with -DGAPLAC_YIELD=15 to try.
 #ifndef GAPLAC_YIELD
 #define GAPLAC_YIELD 0
 #endif
@@ -474,6 +477,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
         bj += w0;
     }
     gram_tile(A + (int64_t)bj * NB * lda, lda, N, X, ldx, v, tpp, bi, bj);
+    kt_end(kt);
+}
+
+// Second Gram launch as a work queue (head of the evaluation). The panel
+// chain's first super-panel (diagonal block: 264 registers per wave and 75 KB of LDS;
+// TRSM: 146 registers, 74 KB; column updates: up to ~1500 workgroups) runs beside this
+// launch. A plain grid keeps four Gram workgroups on every CU and refills each freed slot
+// with its next tile, so the chain waited for the whole launch to drain (a 35 us diagonal
+// block took 389 us at N = 16384). Here a fixed number of workgroups per CU take tiles from
+// a per-evaluation ticket (EvalResult::gram_ticket, zeroed by init_result_kernel on the
+// same stream) until the tiles run out; at two per CU a chain workgroup fits beside them
+// on every CU.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gram_queue_kernel(
+    double* __restrict__ A, int64_t lda, int64_t N, const double* __restrict__ X, int64_t ldx,
+    const double* __restrict__ v, const TermPack* __restrict__ tpp, int w0, int ntiles,
+    EvalResult* __restrict__ res, KTime* __restrict__ kt) {
+    kt_begin(kt);
+    __shared__ int s_tile;
+    for (;;) {
+        __syncthreads();  // the previous tile's LDS reads are complete
+        if (threadIdx.x == 0) s_tile = (int)atomicAdd(&res->gram_ticket, 1u);
+        __syncthreads();
+        const int t = s_tile;
+        if (t >= ntiles) break;
+        int bi, bj;
+        tri_index(t, bi, bj);
+        bi += w0;
+        bj += w0;
+        gram_tile(A + (int64_t)bj * NB * lda, lda, N, X, ldx, v, tpp, bi, bj);
+    }
     kt_end(kt);
 }
 
@@ -1090,12 +1123,12 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
     GAPLAC_LSTORE(0);
     __syncthreads();
     const int NCH = kdepth / KB;
-    const int key = (GAPLAC_YIELD && yield) ? cu_key() : 0;
+    const int key = yield ? cu_key() : 0;
     int busy = 0;  // this CU's chain-wave count, read one chunk earlier
     for (int ch = 0; ch < NCH; ++ch) {
         const int buf = ch & 1;
         const bool more = ch + 1 < NCH;
-        if (GAPLAC_YIELD && yield) {
+        if (yield) {
             if (busy > 0) yield_to_chain(key);
             busy = cu_busy_load(key);
         }
@@ -1153,7 +1186,7 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a) {
                     acc[mi][mj][rg] = Ci[(int64_t)(64 * wj + 16 * mj + fr + 4 * rg) * ldc];
         }
     }
-    tile_mma_neg(P, Q, a.pn.ld, a.kdepth, active, acc, true);
+    tile_mma_neg(P, Q, a.pn.ld, a.kdepth, active, acc, a.yield != 0);
     if (!active) return;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
@@ -1334,7 +1367,7 @@ constexpr int QG = GAPLAC_QG;
 constexpr int QUAD_BULK_MAX_TILES = 512;
 
 __device__ __forceinline__ void quad_update(double* __restrict__ C, int64_t ldc, const Panel& pn, int bi,
-                                            int bj, int lj, int qi, int qj, int kdepth) {
+                                            int bj, int lj, int qi, int qj, int kdepth, bool yield = false) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wi = wave & 1, wj = wave >> 1;
     const int fr = lane >> 4, fc = lane & 15;
@@ -1374,8 +1407,14 @@ __device__ __forceinline__ void quad_update(double* __restrict__ C, int64_t ldc,
         }
     };
     const int ng = kdepth / (4 * QG);  // 4 per 128 panel columns
+    const int key = yield ? cu_key() : 0;
+    int busy = 0;  // as in tile_mma_neg: read one group pair earlier, used now
     load(0, 0);
     for (int g = 0; g < ng; g += 2) {
+        if (yield) {
+            if (busy > 0) yield_to_chain(key);
+            busy = cu_busy_load(key);
+        }
         if (g + 1 < ng) load(1, g + 1);
         compute(0);
         if (g + 1 < ng) {
@@ -1425,7 +1464,7 @@ __global__ __launch_bounds__(256) void quad_bulk_kernel(BulkArgs a, KTime* __res
         int bi, bj, lj;
         tile_decode(a, idx, bi, bj, lj);
         const int qi = q >> 1, qj = q & 1;
-        if (!(bi == bj && qj > qi)) quad_update(a.C, a.ldc, a.pn, bi, bj, lj, qi, qj, a.kdepth);
+        if (!(bi == bj && qj > qi)) quad_update(a.C, a.ldc, a.pn, bi, bj, lj, qi, qj, a.kdepth, a.yield != 0);
     }
     kt_end(kt);
 }
@@ -1509,6 +1548,7 @@ __global__ void init_result_kernel(EvalResult* res) {
     res->logdet = 0.0;
     res->quad = 0.0;
     res->info = ~0ull;
+    res->gram_ticket = 0u;
 }
 
 // ---------------------------------------------------------------------------------
@@ -2008,6 +2048,19 @@ void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const
     if (ntiles <= 0) return;
     if (!guard_launch("gram_kernel", A, 0, tiles_end(lda, max_bi, max_bj))) return;
     gram_kernel<<<dim3((unsigned)ntiles), dim3(256), 0, s>>>(A, lda, N, X, ldx, v, dtp, nt, part, w, kt);
+}
+
+static int device_cus();
+
+void launch_gram_queue(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const double* X, int64_t ldx,
+                       const double* v, const TermPack* dtp, int w, int per_cu, EvalResult* res, KTime* kt) {
+    const int64_t m = nt - w;
+    const int64_t ntiles = m > 0 ? m * (m + 1) / 2 : 0;
+    if (ntiles <= 0) return;
+    const int64_t max_b = w + tri_row(ntiles - 1);
+    if (!guard_launch("gram_queue_kernel", A, 0, tiles_end(lda, max_b, max_b))) return;
+    const int grid = (int)std::min<int64_t>(ntiles, (int64_t)per_cu * device_cus());
+    gram_queue_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(A, lda, N, X, ldx, v, dtp, w, (int)ntiles, res, kt);
 }
 
 void launch_gram_list(hipStream_t s, double* C, int64_t ldc, int64_t N, const double* X, int64_t ldx,
