@@ -32,6 +32,7 @@ EXPORTED = (
     "gaplac_posterior_mean_var",
     "gaplac_rand",
     "gaplac_gram",
+    "gaplac_gram_time",
     "gaplac_factor",
     "gaplac_set_profiling",
     "gaplac_get_stats",
@@ -120,6 +121,10 @@ def load() -> ctypes.CDLL:
     lib.gaplac_rand.argtypes = common + [c_void_p]
     lib.gaplac_gram.argtypes = [
         c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, POINTER(Term), c_double, c_void_p, c_int64,
+    ]
+    lib.gaplac_gram_time.argtypes = [
+        c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, POINTER(Term), c_double, c_void_p, c_int32,
+        _DP, _DP,
     ]
     lib.gaplac_factor.argtypes = common + [c_void_p, c_int64, c_void_p]
     lib.gaplac_set_profiling.argtypes = [c_void_p, c_int]

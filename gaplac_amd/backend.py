@@ -220,6 +220,20 @@ class Context:
         self._check(rc)
         return out
 
+    def gram_time(self, X, terms, noise: float, v, reps: int = 5):
+        """(best_ms, bytes): one plain-grid Gram launch into the workspace, timed with
+        hipEvents (best of reps), and its algorithmic HBM bytes (bench.py extra.gram)."""
+        Xc = _colmajor(X)
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        N, D = Xc.shape
+        terms = list(terms)
+        ta = term_array(terms)
+        ms, nbytes = c_double(0.0), c_double(0.0)
+        rc = self.lib.gaplac_gram_time(self.h, N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), len(terms), ta,
+                                       float(noise), v.ctypes.data_as(c_void_p), int(reps), byref(ms), byref(nbytes))
+        self._check(rc)
+        return ms.value, nbytes.value
+
     def factor(self, X, terms, noise: float, v):
         """(L, z): lower Cholesky factor of C and z = L^{-1} v."""
         Xc = _colmajor(X)

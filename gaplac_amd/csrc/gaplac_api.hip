@@ -1187,6 +1187,53 @@ int gaplac_gram(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t 
     return 0;
 }
 
+int gaplac_gram_time(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx, int32_t T,
+                     const gaplac_term* terms, double noise, const double* v, int32_t reps, double* best_ms,
+                     double* bytes) {
+    int rc = check_common(ctx, N, D, X, ldx, noise, v);
+    if (rc) return rc;
+    if (N == 0 || reps < 1 || !best_ms || !bytes) return set_err(ctx, GAPLAC_E_ARG, "N = 0, reps < 1 or NULL outputs");
+    TermPack tp;
+    if ((rc = pack_terms(ctx, D, T, terms, &tp))) return rc;
+    HIPCK(ctx, hipSetDevice(ctx->device));
+    if ((rc = upload(ctx, N, D, X, ldx, v))) return rc;
+    const int64_t Np = round_up(N + 1, NB);
+    const int nt = (int)(Np / NB);
+    if ((rc = ensure(ctx, &ctx->A, &ctx->A_elems, (size_t)Np * Np))) return rc;
+    tp.noise = noise;
+    *ctx->htp = tp;
+    HIPCK(ctx, hipMemcpyAsync(ctx->dtp, ctx->htp, sizeof(TermPack), hipMemcpyHostToDevice, ctx->s_main));
+    hipEvent_t e0, e1;
+    HIPCK(ctx, hipEventCreate(&e0));
+    if (hipEventCreate(&e1) != hipSuccess) {
+        (void)hipEventDestroy(e0);
+        return set_err(ctx, GAPLAC_E_HIP, "hipEventCreate failed");
+    }
+    double best = 1e300;
+    {
+        LaunchGuard g;
+        g.base = ctx->A;
+        g.elems = (int64_t)ctx->A_elems;
+        GuardScope scope(&g);
+        for (int r = 0; r < reps && rc == 0; ++r) {
+            float ms = 0.f;
+            if (hipEventRecord(e0, ctx->s_main) != hipSuccess) rc = GAPLAC_E_HIP;
+            launch_gram(ctx->s_main, ctx->A, Np, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 0, 0, nullptr);
+            if (rc == 0 && (hipEventRecord(e1, ctx->s_main) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+                            hipEventElapsedTime(&ms, e0, e1) != hipSuccess))
+                rc = GAPLAC_E_HIP;
+            if (rc == 0) best = std::min(best, (double)ms);
+        }
+        if (g.violations) rc = GAPLAC_E_ARG;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (rc) return set_err(ctx, rc, "gram timing failed");
+    *best_ms = best;
+    *bytes = 8.0 * (double)Np * (double)(Np + 1) / 2.0 + 8.0 * (double)N * (D + 1);
+    return 0;
+}
+
 int gaplac_factor(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx, int32_t T,
                   const gaplac_term* terms, double noise, const double* v, double* out_L,
                   int64_t ldl, double* out_z) {

@@ -162,6 +162,13 @@ int gaplac_rand(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t 
  * (replaces KernelFunctions.kernelmatrix + Diagonal(Fill(noise, N))). */
 int gaplac_gram(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx,
                 int32_t T, const gaplac_term* terms, double noise, double* out_C, int64_t ldc);
+/* Measurement (bench.py extra.gram): the same Gram built from host inputs into the
+ * context's workspace by one plain-grid launch, reps times, each bracketed by hipEvents on
+ * the launching stream; best_ms = the fastest launch, bytes = its algorithmic HBM bytes
+ * (8 Np(Np+1)/2 written + 8 N (D+1) read, Np = N+1 rounded up to 128). */
+int gaplac_gram_time(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx,
+                     int32_t T, const gaplac_term* terms, double noise, const double* v,
+                     int32_t reps, double* best_ms, double* bytes);
 /* Lower Cholesky factor L = U^T of the same C (dense N×N column-major, upper part
  * zeroed) and z = L^{-1} v (replaces cholesky(Symmetric(C)).U' and U' \ v). */
 int gaplac_factor(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64_t ldx,

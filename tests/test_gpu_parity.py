@@ -51,6 +51,23 @@ def test_golden_fixtures(ctx, case):
         assert rel(lp, case["logpdf"]) <= 1e-12
 
 
+def test_gram_time_measures_the_same_gram(ctx):
+    # gaplac_gram_time (bench.py extra.gram) builds the Gram into the workspace: its bytes
+    # follow the documented formula and a logpdf right after it still matches the oracle
+    rng = np.random.default_rng(5)
+    N = 1000
+    X = np.column_stack([rng.uniform(0, 10, N), rng.integers(0, 7, N).astype(float)])
+    v = rng.standard_normal(N)
+    terms = [(SQEXP, 0, 1.5, 0), (OU, 0, 3.0, 1), (CAT, 1, 0.0, 2), (NOISE, -1, 1.0, 3)]
+    ms, nbytes = ctx.gram_time(X, terms, 0.1, v, reps=3)
+    Np = (N + 1 + 127) // 128 * 128
+    assert nbytes == 8.0 * Np * (Np + 1) / 2 + 8.0 * N * 3
+    assert 0.0 < ms < 1000.0
+    assert rel(ctx.logpdf(X, terms, 0.1, v), R.logpdf(X, terms, 0.1, v)[0]) <= 1e-12
+    with pytest.raises(ArgumentError):
+        ctx.gram_time(X, terms, 0.1, v, reps=0)
+
+
 @pytest.mark.parametrize("case", [c for c in CASES if c["N"] <= 1024 and not c["info"]][:12],
                          ids=lambda c: c["name"][:60])
 def test_gram_entrywise(ctx, case):
