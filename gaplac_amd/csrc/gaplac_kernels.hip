@@ -543,6 +543,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
 // (OpenBLAS potf2's test; NaN pivots propagate, as in the reference).
 // The eight 16x16 inverses are computed after the loop (off the per-panel barriers).
 // ---------------------------------------------------------------------------------
+// Diagonal kernel phase 2: wave 3 only inverts, waves 1-2 take the trailing tiles in
+// interleaved pairs (1), or all three waves share the trailing tiles (0).
+#ifndef GAPLAC_DIAG_SPLIT
+#define GAPLAC_DIAG_SPLIT 1
+#endif
 constexpr int DB = 16;                    // sub-block edge
 constexpr int NDB = NB / DB;              // 8
 constexpr int NPK = NDB * (NDB + 1) / 2;  // 36 packed blocks
@@ -574,6 +579,34 @@ __device__ __forceinline__ void dblk_update(double* Ab, int I, int J, int k, int
     for (int q = 0; q < 4; ++q) C[(fr + 4 * q) * 16 + fc] = acc[q];
 }
 
+// Two independent updates C_I1J1 -= L_I1k L_J1k^T and C_I2J2 -= L_I2k L_J2k^T with their
+// MFMA chains interleaved (the dependent-accumulator latency of one hides the other's).
+__device__ __forceinline__ void dblk_update2(double* Ab, int I1, int J1, int I2, int J2, int k, int lane) {
+    double* C1 = Ab + bidx(I1, J1) * 256;
+    double* C2 = Ab + bidx(I2, J2) * 256;
+    const double* LI1 = Ab + bidx(I1, k) * 256;
+    const double* LJ1 = Ab + bidx(J1, k) * 256;
+    const double* LI2 = Ab + bidx(I2, k) * 256;
+    const double* LJ2 = Ab + bidx(J2, k) * 256;
+    const int fr = lane >> 4, fc = lane & 15;
+    d4 a1, a2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        a1[q] = C1[(fr + 4 * q) * 16 + fc];
+        a2[q] = C2[(fr + 4 * q) * 16 + fc];
+    }
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+        a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(-LJ1[(4 * kk + fr) * 16 + fc], LI1[(4 * kk + fr) * 16 + fc], a1, 0, 0, 0);
+        a2 = __builtin_amdgcn_mfma_f64_16x16x4f64(-LJ2[(4 * kk + fr) * 16 + fc], LI2[(4 * kk + fr) * 16 + fc], a2, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        C1[(fr + 4 * q) * 16 + fc] = a1[q];
+        C2[(fr + 4 * q) * 16 + fc] = a2[q];
+    }
+}
+
 // Dinv_s = L_ss^{-1} (column-major 16x16 into global), 16 lanes each one column.
 __device__ __forceinline__ void dinv_diag(const double* Ab, double* __restrict__ Dinv,
                                           const double* rdiag, int s, int lane) {
@@ -597,7 +630,7 @@ __device__ __forceinline__ void dinv_diag(const double* Ab, double* __restrict__
 
 // Wave-level factorisation of panel s: rows 16s..127 x 16 columns, two rows per lane.
 // Per column the critical chain is kept short: pivot (v_readlane) -> 1/sqrt (v_rsq_f64
-// + two Goldschmidt steps) -> scale -> update of the NEXT column only (one v_readlane
+// + one third-order step) -> scale -> update of the NEXT column only (one v_readlane
 // broadcast) -> next pivot. Column c's updates of the later columns (c+2..15) are
 // deferred into iteration c+1, where they fill the latency of that pivot's 1/sqrt chain;
 // their L(c2, c) factors come from an LDS broadcast (lanes 0..7 publish the scaled
@@ -633,9 +666,12 @@ __device__ __forceinline__ void dpanel(double* Ab, double* rdiag, double* colbuf
         // pivot is not reported and propagates to a NaN logpdf, as in the reference.
         bad = (!pad && piv <= 0.0 && bad == 16) ? c : bad;
         const double p = pad ? 1.0 : piv;
-        // Goldschmidt from v_rsq_f64: g -> sqrt(p), h -> 1/(2 sqrt(p))
+        // v_rsq_f64 (~24 bits) refined by one third-order step: e = 1 - p y^2,
+        // 1/sqrt(p) = y + y e (1/2 + 3/8 e), sqrt(p) = t + t e (1/2 + 3/8 e) with t = p y
+        // (<= 2 ulp, tools/rsq_probe.hip; 1/sqrt(p) at dependency level 4, where two
+        // Goldschmidt steps took 6)
         const double y = __builtin_amdgcn_rsq(p);
-        double g = p * y, h = 0.5 * y;
+        const double t = p * y;
         // deferred updates of columns c+1..15 by column c-1
         if (c >= 1) {
 #pragma unroll
@@ -644,13 +680,10 @@ __device__ __forceinline__ void dpanel(double* Ab, double* rdiag, double* colbuf
                 v1[c2] = fma(-v1[c - 1], lc[c2], v1[c2]);
             }
         }
-        double r = fma(-g, h, 0.5);
-        g = fma(g, r, g);
-        h = fma(h, r, h);
-        r = fma(-g, h, 0.5);
-        g = fma(g, r, g);
-        h = fma(h, r, h);
-        const double d = g, rd = h + h;
+        const double e = fma(-t, y, 1.0);
+        const double cc = fma(e, 0.375, 0.5);
+        const double rd = fma(y * e, cc, y);
+        const double d = fma(t * e, cc, t);
         myrd = lane == c ? rd : myrd;
         v0[c] = rel0 > c ? v0[c] * rd : (rel0 == c ? d : v0[c]);
         v1[c] = rel1 > c ? v1[c] * rd : (rel1 == c ? d : v1[c]);
@@ -716,18 +749,47 @@ __device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ Ag, 
         if (wave == 0) {
             dpanel(Ab, rdiag, colbuf, s, lane, g0, N, res);
         } else if (s >= 1) {
-            if (wave == 3) dinv_diag(Ab, Dinv, rdiag, s - 1, lane);  // off the barrier path
             const int ntr = (NDB - 1 - s) * (NDB - s) / 2;  // tiles (I,J), s+1 <= J <= I <= 7
-            for (int task = wave - 1; task < ntr; task += 3) {
-                int J = s + 1, rem = task;
+            auto tile_of = [&](int task, int& I, int& J) {
+                int rem = task;
+                J = s + 1;
                 while (rem >= NDB - J) {
                     rem -= NDB - J;
                     ++J;
                 }
-                dblk_update(Ab, J + rem, J, s - 1, lane);
+                I = J + rem;
+            };
+#if GAPLAC_DIAG_SPLIT
+            // wave 3 inverts block s-1 (~4K cycles, the length of wave 0's panel sweep);
+            // waves 1 and 2 take the trailing tiles, two at a time (interleaved MFMA chains)
+            if (wave == 3) {
+                dinv_diag(Ab, Dinv, rdiag, s - 1, lane);
+            } else {
+                int task = wave - 1;
+                for (; task + 2 < ntr; task += 4) {
+                    int I1, J1, I2, J2;
+                    tile_of(task, I1, J1);
+                    tile_of(task + 2, I2, J2);
+                    dblk_update2(Ab, I1, J1, I2, J2, s - 1, lane);
+                }
+                if (task < ntr) {
+                    int I, J;
+                    tile_of(task, I, J);
+                    dblk_update(Ab, I, J, s - 1, lane);
+                }
             }
+#else
+            if (wave == 3) dinv_diag(Ab, Dinv, rdiag, s - 1, lane);  // off the barrier path
+            for (int task = wave - 1; task < ntr; task += 3) {
+                int I, J;
+                tile_of(task, I, J);
+                dblk_update(Ab, I, J, s - 1, lane);
+            }
+#endif
         }
         if (wave == 0) STAMP(2 + 2 * s);
+        STAMPT(192, 21 + s);  // wave 3: inverse of block s-1 + its trailing share
+        STAMPT(64, 29 + s);   // wave 1: its trailing share
         __syncthreads();
     }
     STAMP(17);

@@ -68,6 +68,16 @@ int main() {
           }
       printf("diag v%d: %.1f us (event)  max|L-Lcpu| %.2e  max|Dinv L - I| %.2e  info %llx\n", v, ms * 1e3, errL, errD,
              (unsigned long long)hr.info);
+      if (v == 1 && rep == 3) {  // v1: per panel s, phase 2 of each wave (cycles, s_memtime)
+        unsigned long long st[128]; CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof st));
+        printf("  v1 load %llu\n", st[0] - st[20]);
+        for (int s = 0; s < 8; ++s) {
+          const unsigned long long p2 = st[1 + 2 * s];
+          printf("  v1 s=%d: phase1+barrier %5llu | phase2 w0 dpanel %5llu w1 trailing %5llu w3 dinv+trailing %5llu\n", s,
+                 p2 - (s ? st[2 * s] : st[0]), st[2 + 2 * s] - p2, st[29 + s] - p2, st[21 + s] - p2);
+        }
+        printf("  v1 last dinv+store %llu total %llu cycles\n", st[19] - st[17], st[19] - st[20]);
+      }
       if (v == 2 && rep == 3) {
         unsigned long long st[128]; CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof st));
         const unsigned long long b = st[99];
