@@ -67,6 +67,9 @@ struct gaplac_ctx {
     bool serial = false;  // GAPLAC_SERIAL=1: one stream, no overlap (per-kernel timing)
     bool dry = false;     // host-only walk of the schedule (gaplac_plan_check): no HIP calls
     int spw = 4;          // GAPLAC_SPW: super-panel width in 128-column tiles (bulk K = 128 spw)
+    int tail_m = 0;       // GAPLAC_TAIL_M / GAPLAC_TAIL_W: once at most tail_m tile columns remain,
+    int tail_w = 0;       //   super-panels are tail_w wide (plain logpdf only; 0 = off)
+    int tail_s = 32;      // GAPLAC_TAIL_S: the last ~tail_s tile columns run serially on one stream
     gaplac_stats stats{};
     struct Slot {
         int kind;  // 0 bulk syrk, 1 gram, 2 diag, 4 trsm, 5 column update, 6 small bulk
@@ -347,9 +350,7 @@ int accumulate_slots(gaplac_ctx* ctx, const std::vector<gaplac_ctx::Slot>& slots
 // the previous columns of its own super-panel). Columns of SP p+1 receive SP p-1 in
 // R(p-1) and SP p in the lookahead col_update; within a step the streams touch disjoint
 // tile columns. Events ping-pong (p & 1).
-void factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, int nt, int p) {
-    const int W = ctx->spw;
-    const int c0 = W * p, c1 = std::min(W * p + W, nt);
+void factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, int nt, int c0, int c1) {
     for (int c = c0; c < c1; ++c) {
         double* Acol = ctx->A + (int64_t)c * NB * lda;
         if (c > c0)
@@ -395,31 +396,75 @@ void extra_rows_step(gaplac_ctx* ctx, hipStream_t sm, int64_t lda, int nt, int p
     }
 }
 
+// Super-panel boundaries: tile columns sp[p] .. sp[p+1]-1 form SP p. Width spw throughout,
+// except that a plain logpdf switches to tail_w once at most tail_m tile columns remain:
+// in the chain-bound tail a narrow super-panel keeps the lookahead update short (K = 128
+// tail_w instead of 128 spw) while the bulk updates have slack.
+// With a serial tail (tail_s > 0) the list stops at the first boundary with at most tail_s
+// tile columns after it; those columns are factored by serial_tail().
+static std::vector<int> superpanel_starts(const gaplac_ctx* ctx, int nt) {
+    std::vector<int> sp{0};
+    int c = 0;
+    while (c < nt) {
+        if (ctx->xr_mode == 0 && ctx->tail_s > 0 && c > 0 && nt - c <= ctx->tail_s) break;
+        const bool tail = ctx->xr_mode == 0 && ctx->tail_w > 0 && nt - c <= ctx->tail_m && c > 0;
+        c = std::min(c + (tail ? ctx->tail_w : ctx->spw), nt);
+        sp.push_back(c);
+    }
+    return sp;
+}
+
+// Serial tail: tile columns ts .. nt-1 factored right-looking on one stream,
+// after the bulk update that applied the last super-panel to them: per column the whole
+// remaining triangle gets the previous column (K = 128), then the diagonal block and the
+// TRSM. No events: in the chain-bound tail every event record or cross-stream wait costs
+// ~6-12 us of dispatch latency on the critical path, more than the small updates save by
+// overlapping.
+static void serial_tail(gaplac_ctx* ctx, hipStream_t sm, int64_t N, int64_t lda, int nt, int ts) {
+    for (int c = ts; c < nt; ++c) {
+        double* Acol = ctx->A + (int64_t)c * NB * lda;
+        if (c > ts) {
+            const int m = nt - c;
+            BulkArgs ba{ctx->A, lda, Panel{Acol - NB * lda, lda, 0}, ctx->tiles + ctx->tile_off[(size_t)m],
+                        m * (m + 1) / 2, NB, c, c, ColMap{1, 0, ctx->spw}};
+            launch_bulk(sm, ba, slot(ctx, 6, 0));
+        }
+        double* Dk = ctx->Dinv + (size_t)c * DINV_PER_BLOCK;
+        if ((int64_t)c * NB < N)
+            launch_potrf_diag(sm, Acol + (int64_t)c * NB, lda, N, (int64_t)c * NB, Dk, ctx->dres, slot(ctx, 2, 0));
+        launch_trsm(sm, Acol, lda, nt, c, Dk, slot(ctx, 4, 0));
+    }
+}
+
 int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     hipStream_t sm = ctx->s_main;
     hipStream_t sp = ctx->serial ? sm : ctx->s_panel;
     const int W = ctx->spw;
-    const int nsp = (nt + W - 1) / W;
+    const std::vector<int> spc = superpanel_starts(ctx, nt);
+    const int nsp = (int)spc.size() - 1;
     HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_gram, 0));  // first W tile columns built
-    factor_superpanel(ctx, sp, N, lda, nt, 0);
+    factor_superpanel(ctx, sp, N, lda, nt, spc[0], spc[1]);
     HIPQ(ctx, hipEventRecord(ctx->ev_P[0], sp));
     for (int p = 0; p < nsp; ++p) {
-        const int c0 = W * p;
-        const int kd = (std::min(c0 + W, nt) - c0) * NB;  // depth of super-panel p
+        const int c0 = spc[(size_t)p], c1 = spc[(size_t)p + 1];
+        const int kd = (c1 - c0) * NB;  // depth of super-panel p
         if (p + 1 < nsp) {
             if (p >= 1)
                 HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_R[(p - 1) & 1], 0));
             else
                 HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_gram2, 0));  // rest of the Gram built
-            const int ncols = std::min(c0 + 2 * W, nt) - (c0 + W);
-            launch_col_update(sp, ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nt, c0 + W,
-                              c0 + W, ncols, kd, slot(ctx, 5, 0));
-            HIPQ(ctx, hipEventRecord(ctx->ev_L[p & 1], sp));
-            factor_superpanel(ctx, sp, N, lda, nt, p + 1);
+            const int c2 = spc[(size_t)p + 2];
+            launch_col_update(sp, ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nt, c1, c1, c2 - c1, kd,
+                              slot(ctx, 5, 0));
+            // only GAPLAC_LA_FIRST waits on L(p); an unneeded record costs ~6 us of dispatch
+            // latency on the chain
+            if (ctx->la_first > 0) HIPQ(ctx, hipEventRecord(ctx->ev_L[p & 1], sp));
+            factor_superpanel(ctx, sp, N, lda, nt, c1, c2);
             HIPQ(ctx, hipEventRecord(ctx->ev_P[(p + 1) & 1], sp));
         }
         HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_P[p & 1], 0));
-        const int jb = c0 + 2 * W;
+        // tile columns after SP p+1; the last super-panel also updates a serial tail
+        const int jb = p + 2 <= nsp ? spc[(size_t)p + 2] : spc[(size_t)nsp];
         if (p + 1 < nsp && jb < nt && sp != sm && (nt - jb) * (nt - jb + 1) / 2 <= ctx->la_first)
             HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_L[p & 1], 0));
         if (jb < nt) {
@@ -456,6 +501,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             extra_rows_step(ctx, sx, lda, nt, p);
         }
     }
+    if (spc[(size_t)nsp] < nt) serial_tail(ctx, sm, N, lda, nt, spc[(size_t)nsp]);
     if (ctx->xr_mode && !ctx->serial) {
         HIPQ(ctx, hipEventRecord(ctx->ev_xdone, ctx->s_extra));
         HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_xdone, 0));
@@ -899,6 +945,9 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_SERIAL")) ctx->serial = s[0] == '1';
     if (const char* s = std::getenv("GAPLAC_LA_FIRST")) ctx->la_first = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_YIELD_M")) ctx->yield_m = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_TAIL_M")) ctx->tail_m = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_TAIL_W")) ctx->tail_w = std::max(0, std::min(8, std::atoi(s)));
+    if (const char* s = std::getenv("GAPLAC_TAIL_S")) ctx->tail_s = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     auto fail = [&](const char* what, hipError_t e) {
