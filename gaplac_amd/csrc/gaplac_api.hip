@@ -70,6 +70,8 @@ struct gaplac_ctx {
     int tail_m = 0;       // GAPLAC_TAIL_M / GAPLAC_TAIL_W: once at most tail_m tile columns remain,
     int tail_w = 0;       //   super-panels are tail_w wide (plain logpdf only; 0 = off)
     int tail_s = 32;      // GAPLAC_TAIL_S: the last ~tail_s tile columns run serially on one stream
+    int gram_queue = 2;   // GAPLAC_GRAM_QUEUE: second Gram launch as a work queue of this many
+                          //   workgroups per CU, leaving room for the panel chain (0 = plain grid)
     gaplac_stats stats{};
     struct Slot {
         int kind;  // 0 bulk syrk, 1 gram, 2 diag, 4 trsm, 5 column update, 6 small bulk
@@ -527,16 +529,6 @@ int ensure_tile_lists(gaplac_ctx* ctx, int nt) {
     return 0;
 }
 
-// Second Gram launch as a work queue with this many workgroups per CU, leaving room for
-// the panel chain (GAPLAC_GRAM_QUEUE; 0 = the plain grid, for A/B runs).
-static int gram_queue_mode() {
-    static const int k = [] {
-        const char* e = std::getenv("GAPLAC_GRAM_QUEUE");
-        return e ? std::max(0, std::min(4, std::atoi(e))) : 2;
-    }();
-    return k;
-}
-
 // Everything one evaluation puts on the streams (eager launch or graph capture): reset
 // the result record (and the profiling slots), Gram build, factorisation schedule,
 // reduction, result copy to the pinned host record. Inputs: ctx->dX (ld N), ctx->dv,
@@ -553,9 +545,9 @@ int enqueue_eval_body(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt)
     launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 1, ctx->spw,
                 slot(ctx, 1, bytes * frac));
     HIPQ(ctx, hipEventRecord(ctx->ev_gram, ctx->s_main));
-    if (gram_queue_mode())
+    if (ctx->gram_queue > 0)
         launch_gram_queue(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, ctx->spw,
-                          gram_queue_mode(), ctx->dres, slot(ctx, 1, bytes * (1.0 - frac)));
+                          ctx->gram_queue, ctx->dres, slot(ctx, 1, bytes * (1.0 - frac)));
     else
         launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 2, ctx->spw,
                     slot(ctx, 1, bytes * (1.0 - frac)));
@@ -948,6 +940,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_TAIL_M")) ctx->tail_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_TAIL_W")) ctx->tail_w = std::max(0, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAIL_S")) ctx->tail_s = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_GRAM_QUEUE")) ctx->gram_queue = std::max(0, std::min(4, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     auto fail = [&](const char* what, hipError_t e) {

@@ -545,6 +545,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
 // ---------------------------------------------------------------------------------
 // Diagonal kernel phase 2: wave 3 only inverts, waves 1-2 take the trailing tiles in
 // interleaved pairs (1), or all three waves share the trailing tiles (0).
+// Panels 4-7 of the diagonal kernel with one row per lane (1) or two (0).
+#ifndef GAPLAC_DPANEL1
+#define GAPLAC_DPANEL1 1
+#endif
 #ifndef GAPLAC_DIAG_SPLIT
 #define GAPLAC_DIAG_SPLIT 1
 #endif
@@ -628,36 +632,40 @@ __device__ __forceinline__ void dinv_diag(const double* Ab, double* __restrict__
     }
 }
 
-// Wave-level factorisation of panel s: rows 16s..127 x 16 columns, two rows per lane.
+// Wave-level factorisation of panel s: rows 16s..127 x 16 columns, RPL rows per lane (2 for
+// panels 0-3; 1 from panel 4 on, where at most 64 rows remain: the sweep is issue-bound in
+// one wave, ~50 instructions and ~440 cycles per column with two rows per lane, against a
+// ~120-cycle dependent chain -- tools/lat_chain_probe.hip).
 // Per column the critical chain is kept short: pivot (v_readlane) -> 1/sqrt (v_rsq_f64
 // + one third-order step) -> scale -> update of the NEXT column only (one v_readlane
 // broadcast) -> next pivot. Column c's updates of the later columns (c+2..15) are
 // deferred into iteration c+1, where they fill the latency of that pivot's 1/sqrt chain;
-// their L(c2, c) factors come from an LDS broadcast (lanes 0..7 publish the scaled
-// column, every lane reads it back at the end of iteration c; LDS is in order within a
-// wave). The sweep is branch-free (padding pivots and the info test are selects).
-__device__ __forceinline__ void dpanel(double* Ab, double* rdiag, double* colbuf, int s, int lane,
-                                       int64_t gcol0, int64_t N, EvalResult* res) {
+// their L(c2, c) factors come from an LDS broadcast (the lanes holding the panel's first 16
+// rows publish the scaled column, every lane reads it back at the end of iteration c; LDS
+// is in order within a wave). The sweep is branch-free (padding pivots and the info test
+// are selects).
+template <int RPL>
+__device__ __forceinline__ void dpanel_t(double* Ab, double* rdiag, double* colbuf, int s, int lane,
+                                         int64_t gcol0, int64_t N, EvalResult* res) {
     // opaque copy of the lane id: keeps the lane-dependent masks of the sweep from being
     // hoisted out of the panel loop (and spilled) by loop-invariant code motion
     asm volatile("" : "+v"(lane));
     const int R0 = 16 * s;
-    const int rel0 = 2 * lane, rel1 = rel0 + 1;
+    const int rel0 = RPL * lane;
     const int row0 = R0 + rel0;
     const bool live = row0 < NB;
-    double v0[16], v1[16];
+    double v[RPL][16];
     // lanes past the last row read (and never store) the panel's diagonal block
     double* blk = Ab + bidx(live ? (row0 >> 4) : s, s) * 256;
     const int rr = row0 & 15;
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        v0[c] = blk[c * 16 + rr];
-        v1[c] = blk[c * 16 + rr + 1];
-    }
+    for (int c = 0; c < 16; ++c)
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) v[r][c] = blk[c * 16 + rr + r];
     const int64_t npiv = N - (gcol0 + R0);  // columns >= npiv are padding (unit pivots)
     double myrd = 1.0;
     int bad = 16;
-    double piv = readlane_d(v0[0], 0);
+    double piv = readlane_d(v[0][0], 0);
     double lc[16];  // L(c2, c-1) for c2 >= c+1 (broadcast of the previous column)
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
@@ -668,32 +676,37 @@ __device__ __forceinline__ void dpanel(double* Ab, double* rdiag, double* colbuf
         const double p = pad ? 1.0 : piv;
         // v_rsq_f64 (~24 bits) refined by one third-order step: e = 1 - p y^2,
         // 1/sqrt(p) = y + y e (1/2 + 3/8 e), sqrt(p) = t + t e (1/2 + 3/8 e) with t = p y
-        // (<= 2 ulp, tools/rsq_probe.hip; 1/sqrt(p) at dependency level 4, where two
+        // (<= 1 ulp, tools/rsq_probe.hip; 1/sqrt(p) at dependency level 4, where two
         // Goldschmidt steps took 6)
         const double y = __builtin_amdgcn_rsq(p);
         const double t = p * y;
         // deferred updates of columns c+1..15 by column c-1
         if (c >= 1) {
 #pragma unroll
-            for (int c2 = c + 1; c2 < 16; ++c2) {
-                v0[c2] = fma(-v0[c - 1], lc[c2], v0[c2]);
-                v1[c2] = fma(-v1[c - 1], lc[c2], v1[c2]);
-            }
+            for (int c2 = c + 1; c2 < 16; ++c2)
+#pragma unroll
+                for (int r = 0; r < RPL; ++r) v[r][c2] = fma(-v[r][c - 1], lc[c2], v[r][c2]);
         }
         const double e = fma(-t, y, 1.0);
         const double cc = fma(e, 0.375, 0.5);
         const double rd = fma(y * e, cc, y);
         const double d = fma(t * e, cc, t);
         myrd = lane == c ? rd : myrd;
-        v0[c] = rel0 > c ? v0[c] * rd : (rel0 == c ? d : v0[c]);
-        v1[c] = rel1 > c ? v1[c] * rd : (rel1 == c ? d : v1[c]);
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) v[r][c] = rel0 + r > c ? v[r][c] * rd : (rel0 + r == c ? d : v[r][c]);
         if (c < 15) {
             double* cb = colbuf + 16 * (c & 1);
-            if (c < 14 && lane < 8) *reinterpret_cast<double2*>(&cb[2 * lane]) = make_double2(v0[c], v1[c]);
-            const double ln = readlane_d(((c + 1) & 1) ? v1[c] : v0[c], (c + 1) >> 1);
-            v0[c + 1] = fma(-v0[c], ln, v0[c + 1]);
-            v1[c + 1] = fma(-v1[c], ln, v1[c + 1]);
-            piv = readlane_d(((c + 1) & 1) ? v1[c + 1] : v0[c + 1], (c + 1) >> 1);
+            if (c < 14) {
+                if constexpr (RPL == 2) {
+                    if (lane < 8) *reinterpret_cast<double2*>(&cb[2 * lane]) = make_double2(v[0][c], v[1][c]);
+                } else {
+                    if (lane < 16) cb[lane] = v[0][c];
+                }
+            }
+            const double ln = readlane_d(v[(c + 1) % RPL][c], (c + 1) / RPL);
+#pragma unroll
+            for (int r = 0; r < RPL; ++r) v[r][c + 1] = fma(-v[r][c], ln, v[r][c + 1]);
+            piv = readlane_d(v[(c + 1) % RPL][c + 1], (c + 1) / RPL);
             if (c < 14) {
                 __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -710,10 +723,10 @@ __device__ __forceinline__ void dpanel(double* Ab, double* rdiag, double* colbuf
     if (lane < 16) rdiag[R0 + lane] = myrd;
     if (live) {
 #pragma unroll
-        for (int c = 0; c < 16; ++c) {
-            blk[c * 16 + rr] = (rel0 >= c) ? v0[c] : 0.0;  // zero the diagonal block's upper part
-            blk[c * 16 + rr + 1] = (rel1 >= c) ? v1[c] : 0.0;
-        }
+        for (int c = 0; c < 16; ++c)
+#pragma unroll
+            for (int r = 0; r < RPL; ++r)
+                blk[c * 16 + rr + r] = (rel0 + r >= c) ? v[r][c] : 0.0;  // zero the diagonal block's upper part
     }
 }
 
@@ -747,7 +760,12 @@ __device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ Ag, 
         __syncthreads();
         STAMP(1 + 2 * s);
         if (wave == 0) {
-            dpanel(Ab, rdiag, colbuf, s, lane, g0, N, res);
+#if GAPLAC_DPANEL1
+            if (s >= NDB / 2)
+                dpanel_t<1>(Ab, rdiag, colbuf, s, lane, g0, N, res);
+            else
+#endif
+                dpanel_t<2>(Ab, rdiag, colbuf, s, lane, g0, N, res);
         } else if (s >= 1) {
             const int ntr = (NDB - 1 - s) * (NDB - s) / 2;  // tiles (I,J), s+1 <= J <= I <= 7
             auto tile_of = [&](int task, int& I, int& J) {

@@ -1,0 +1,93 @@
+"""The factorisation schedule's alternatives against the oracle and against each other
+(DESIGN.md §3.1, §4): every knob below changes only the order and grouping of the same
+updates, so each must reproduce the oracle's logpdf, logdet and quad (1e-12 relative at
+these sizes) and agree with the default schedule.
+
+* GAPLAC_TAIL_S: the last tile columns factored right-looking on one stream (serial tail;
+  1000 makes it everything after the first super-panel, 0 turns it off);
+* GAPLAC_TAIL_M / GAPLAC_TAIL_W: narrow super-panels near the end;
+* GAPLAC_GRAM_QUEUE: the second Gram launch as a work queue (0 = plain grid);
+* GAPLAC_SPW: the super-panel width.
+The settings are read when a context is created (gaplac_ctx_create).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from gaplac_amd._native import CAT, NOISE, OU, SQEXP
+from gaplac_amd.backend import Context
+from oracle import restatement as R
+from tests.conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+SCHEDULES = {
+    "default": {},
+    "serial_everything": {"GAPLAC_TAIL_S": "1000"},
+    "no_serial_tail": {"GAPLAC_TAIL_S": "0"},
+    "narrow_tail_w1": {"GAPLAC_TAIL_S": "0", "GAPLAC_TAIL_M": "12", "GAPLAC_TAIL_W": "1"},
+    "narrow_tail_w2_then_serial": {"GAPLAC_TAIL_S": "4", "GAPLAC_TAIL_M": "14", "GAPLAC_TAIL_W": "2"},
+    "plain_gram_grid": {"GAPLAC_GRAM_QUEUE": "0"},
+    "gram_queue_1": {"GAPLAC_GRAM_QUEUE": "1"},
+    "spw3_serial8": {"GAPLAC_SPW": "3", "GAPLAC_TAIL_S": "8"},
+}
+SIZES = [1, 127, 129, 700, 2049, 3000]
+TERMS = [(SQEXP, 0, 1.5, 0), (OU, 0, 3.0, 1), (CAT, 1, 0.0, 2), (NOISE, -1, 1.0, 3)]
+
+
+def inputs(N):
+    rng = np.random.default_rng(N)
+    X = np.column_stack([rng.uniform(0, 10, N), rng.integers(0, max(1, N // 3), N).astype(float)])
+    return X, rng.standard_normal(N)
+
+
+def make_ctx(env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return Context(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def ctxs():
+    if not gpu_available():
+        pytest.skip("no GPU")
+    cs = {name: make_ctx(env) for name, env in SCHEDULES.items()}
+    yield cs
+    for c in cs.values():
+        c.close()
+
+
+@pytest.mark.parametrize("N", SIZES)
+def test_schedules_match_oracle_and_each_other(ctxs, N):
+    X, v = inputs(N)
+    rl, rd, rq = R.logpdf(X, TERMS, 0.1, v)
+    base = ctxs["default"].logpdf(X, TERMS, 0.1, v, full=True)
+    for name, c in ctxs.items():
+        lp, ld, q = c.logpdf(X, TERMS, 0.1, v, full=True)
+        assert abs(lp - rl) <= 1e-12 * abs(rl), (name, lp, rl)
+        assert abs(ld - rd) <= 1e-12 * abs(rl), (name, ld, rd)
+        assert abs(q - rq) <= 1e-12 * abs(rl), (name, q, rq)
+        assert abs(lp - base[0]) <= 1e-12 * abs(rl), (name, lp, base[0])
+
+
+def test_serial_tail_reports_posdef_failure(ctxs):
+    # a zero pivot inside the serial tail: Cat-only without noise (exactly singular),
+    # the same info from every schedule
+    N = 1500  # distinct categories for 1000 rows (identity), then repeated triples: the first
+    # zero pivot is at row 1002, tile column 7, inside the serial tail by default
+    cats = np.concatenate([np.arange(1000), 1000 + np.repeat(np.arange(500 // 2 + 1), 2)[:500]])
+    X = np.column_stack([np.zeros(N), cats.astype(float)])
+    infos = set()
+    for name, c in ctxs.items():
+        out, info = c.logpdf_batch(X, [[(CAT, 1, 0.0, 0)]], 0.0, np.ones(N))
+        assert info[0] > 0, name
+        infos.add(int(info[0]))
+    assert infos == {1002}
