@@ -28,7 +28,7 @@ struct gaplac_ctx {
     hipStream_t s_extra = nullptr;  // extra rows (gradient / posterior), beside the bulk updates
     hipEvent_t ev_xinit = nullptr, ev_xdone = nullptr;
     int diag_cus = 0;  // CUs masked out of s_main for the diagonal kernel (0: no mask)
-    hipEvent_t ev_P[2] = {}, ev_R[2] = {}, ev_L[2] = {}, ev_gram = nullptr, ev_gram2 = nullptr;
+    hipEvent_t ev_P[2] = {}, ev_R[2] = {}, ev_L[2] = {}, ev_D[2] = {}, ev_gram = nullptr, ev_gram2 = nullptr;
     // bulk updates of at most this many tiles wait for the step's lookahead column update
     // (GAPLAC_LA_FIRST): late in the factorisation the panel chain is the critical path
     int la_first = 0;
@@ -70,6 +70,8 @@ struct gaplac_ctx {
     int tail_m = 0;       // GAPLAC_TAIL_M / GAPLAC_TAIL_W: once at most tail_m tile columns remain,
     int tail_w = 0;       //   super-panels are tail_w wide (plain logpdf only; 0 = off)
     int tail_s = 32;      // GAPLAC_TAIL_S: the last ~tail_s tile columns run serially on one stream
+    int diag_first_m = 0; // GAPLAC_DIAG_FIRST_M: bulk updates of <= this many tile rows wait for the
+                          //   next super-panel's first diagonal block + TRSM
     int gram_queue = 2;   // GAPLAC_GRAM_QUEUE: second Gram launch as a work queue of this many
                           //   workgroups per CU, leaving room for the panel chain (0 = plain grid)
     gaplac_stats stats{};
@@ -352,7 +354,9 @@ int accumulate_slots(gaplac_ctx* ctx, const std::vector<gaplac_ctx::Slot>& slots
 // the previous columns of its own super-panel). Columns of SP p+1 receive SP p-1 in
 // R(p-1) and SP p in the lookahead col_update; within a step the streams touch disjoint
 // tile columns. Events ping-pong (p & 1).
-void factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, int nt, int c0, int c1) {
+// after_first: recorded once the first column's diagonal block and TRSM are enqueued.
+int factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, int nt, int c0, int c1,
+                      hipEvent_t after_first = nullptr) {
     for (int c = c0; c < c1; ++c) {
         double* Acol = ctx->A + (int64_t)c * NB * lda;
         if (c > c0)
@@ -362,7 +366,9 @@ void factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, 
         if ((int64_t)c * NB < N)
             launch_potrf_diag(sp, Acol + (int64_t)c * NB, lda, N, (int64_t)c * NB, Dk, ctx->dres, slot(ctx, 2, 0));
         launch_trsm(sp, Acol, lda, nt, c, Dk, slot(ctx, 4, 0));
+        if (c == c0 && after_first) HIPQ(ctx, hipEventRecord(after_first, sp));
     }
+    return 0;
 }
 
 // Extra rows, tile rows nt .. nt + xr_tiles - 1 of the column storage,
@@ -445,9 +451,11 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     const std::vector<int> spc = superpanel_starts(ctx, nt);
     const int nsp = (int)spc.size() - 1;
     HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_gram, 0));  // first W tile columns built
-    factor_superpanel(ctx, sp, N, lda, nt, spc[0], spc[1]);
+    int frc;
+    if ((frc = factor_superpanel(ctx, sp, N, lda, nt, spc[0], spc[1]))) return frc;
     HIPQ(ctx, hipEventRecord(ctx->ev_P[0], sp));
     for (int p = 0; p < nsp; ++p) {
+        bool diag_first = false;
         const int c0 = spc[(size_t)p], c1 = spc[(size_t)p + 1];
         const int kd = (c1 - c0) * NB;  // depth of super-panel p
         if (p + 1 < nsp) {
@@ -461,10 +469,18 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             // only GAPLAC_LA_FIRST waits on L(p); an unneeded record costs ~6 us of dispatch
             // latency on the chain
             if (ctx->la_first > 0) HIPQ(ctx, hipEventRecord(ctx->ev_L[p & 1], sp));
-            factor_superpanel(ctx, sp, N, lda, nt, c1, c2);
+            // In the chain-bound steps (small trailing matrix) the bulk update waits until the
+            // next super-panel's first diagonal block and TRSM have run: launched together,
+            // the bulk tiles take every CU's LDS first and the diagonal block (75 KB) waits for
+            // one to retire (107 instead of 33 us); the bulk has slack there.
+            const int mb = nt - (p + 2 <= nsp ? spc[(size_t)p + 2] : spc[(size_t)nsp]);
+            diag_first = sp != sm && mb > 0 && mb <= ctx->diag_first_m;
+            if ((frc = factor_superpanel(ctx, sp, N, lda, nt, c1, c2, diag_first ? ctx->ev_D[p & 1] : nullptr)))
+                return frc;
             HIPQ(ctx, hipEventRecord(ctx->ev_P[(p + 1) & 1], sp));
         }
         HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_P[p & 1], 0));
+        if (diag_first) HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_D[p & 1], 0));
         // tile columns after SP p+1; the last super-panel also updates a serial tail
         const int jb = p + 2 <= nsp ? spc[(size_t)p + 2] : spc[(size_t)nsp];
         if (p + 1 < nsp && jb < nt && sp != sm && (nt - jb) * (nt - jb + 1) / 2 <= ctx->la_first)
@@ -941,6 +957,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_TAIL_W")) ctx->tail_w = std::max(0, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAIL_S")) ctx->tail_s = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_GRAM_QUEUE")) ctx->gram_queue = std::max(0, std::min(4, std::atoi(s)));
+    if (const char* s = std::getenv("GAPLAC_DIAG_FIRST_M")) ctx->diag_first_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     auto fail = [&](const char* what, hipError_t e) {
@@ -983,6 +1000,8 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
         if ((e = hipEventCreateWithFlags(&ctx->ev_R[q], hipEventDisableTiming)) != hipSuccess)
             return fail("event", e);
         if ((e = hipEventCreateWithFlags(&ctx->ev_L[q], hipEventDisableTiming)) != hipSuccess)
+            return fail("event", e);
+        if ((e = hipEventCreateWithFlags(&ctx->ev_D[q], hipEventDisableTiming)) != hipSuccess)
             return fail("event", e);
     }
     if ((e = hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming)) != hipSuccess)
@@ -1032,6 +1051,7 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
         if (ctx->ev_P[q]) (void)hipEventDestroy(ctx->ev_P[q]);
         if (ctx->ev_R[q]) (void)hipEventDestroy(ctx->ev_R[q]);
         if (ctx->ev_L[q]) (void)hipEventDestroy(ctx->ev_L[q]);
+        if (ctx->ev_D[q]) (void)hipEventDestroy(ctx->ev_D[q]);
     }
     if (ctx->ev_gram) (void)hipEventDestroy(ctx->ev_gram);
     if (ctx->ev_gram2) (void)hipEventDestroy(ctx->ev_gram2);
