@@ -1100,6 +1100,57 @@ __global__ __launch_bounds__(256) void trsm_subst_kernel(
     kt_end(kt);
 }
 
+// Panel TRSM, light variant: the same substitution, one wave (16 rows) per workgroup and no
+// LDS: the L_kk and Dinv fragments come straight from L2 (every TRSM workgroup of the
+// column reads the same 128 KB). At <= 96 registers a workgroup fits beside two resident
+// bulk-update workgroups (2 x 208 registers, 2 x 72 KB LDS), so it starts at once instead
+// of taking the slot of a retiring bulk tile for its whole life.
+// One accumulator per block: an f64 MFMA costs 64 cycles dependent or not.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void trsm_lite_kernel(
+    double* __restrict__ Acol, int64_t lda, int k, int bi0, const double* __restrict__ Dinv,
+    KTime* __restrict__ kt) {
+    kt_begin(kt);
+    __builtin_amdgcn_s_setprio(2);  // critical path
+    const int lane = threadIdx.x;
+    const int fr = lane >> 4, fc = lane & 15;
+    const int bi = bi0 + (int)(blockIdx.x >> 3);
+    const int64_t k0 = (int64_t)k * NB;
+    const double* L = Acol + k0;  // L_kk, column-major, lda
+    double* B = Acol + (int64_t)bi * NB + 16 * (blockIdx.x & 7);
+    d4 Y[NDB];
+    // fragments of L(16b + fc, 16c + fr + 4kk), kk = 0..3, for the step after the current one
+    auto lfrag = [&](int b, int c, double (&f)[4]) {
+        const double* Lbc = L + (int64_t)(16 * c + fr) * lda + 16 * b + fc;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) f[kk] = Lbc[(int64_t)(4 * kk) * lda];
+    };
+#pragma unroll
+    for (int b = 0; b < NDB; ++b) {
+        d4 acc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = B[(int64_t)(16 * b + fr + 4 * q) * lda + fc];  // B_b^T
+        double fcur[4], fnext[4];
+        if (b > 0) lfrag(b, 0, fcur);
+#pragma unroll
+        for (int c = 0; c < b; ++c) {
+            if (c + 1 < b) lfrag(b, c + 1, fnext);  // one step ahead
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-fcur[kk], Y[c][kk], acc, 0, 0, 0);
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) fcur[kk] = fnext[kk];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const double* Di = Dinv + b * 256 + fr * 16 + fc;  // column-major [j = fc][m = 4kk + fr]
+        d4 y = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) y = __builtin_amdgcn_mfma_f64_16x16x4f64(Di[64 * kk], acc[kk], y, 0, 0, 0);
+        Y[b] = y;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) B[(int64_t)(16 * b + fr + 4 * q) * lda + fc] = y[q];
+    }
+    kt_end(kt);
+}
+
 // ---------------------------------------------------------------------------------
 // Bulk trailing update, one 128x128 tile per 256-thread workgroup:
 //   C(bi, bj) -= P_bi P_bj^T,   P = the kdepth panel columns (Panel operand),
@@ -2157,11 +2208,24 @@ void launch_potrf_diag(hipStream_t s, double* Ablk, int64_t lda, int64_t N, int6
     potrf_diag_kernel<<<dim3(1), dim3(256), 0, s>>>(Ablk, lda, N, g0, Dinv, res, kt);
 }
 
+// GAPLAC_TRSM_LITE=n: panel TRSMs with more than n tiles below the panel through
+// trsm_lite_kernel (one wave per 16 rows, no LDS); 0 = never.
+static int trsm_lite_mode() {
+    static const int m = [] {
+        const char* e = std::getenv("GAPLAC_TRSM_LITE");
+        return e ? std::atoi(e) : 0;
+    }();
+    return m;
+}
+
 void launch_trsm(hipStream_t s, double* Acol, int64_t lda, int nt, int k, const double* Dinv, KTime* kt) {
     const int n = nt - k - 1;
     if (n <= 0) return;
     if (!guard_launch("trsm_subst_kernel", Acol, 0, tiles_end(lda, nt - 1, 0))) return;
-    trsm_subst_kernel<<<dim3(2 * n), dim3(256), 0, s>>>(Acol, lda, k, k + 1, Dinv, kt);
+    if (trsm_lite_mode() > 0 && n > trsm_lite_mode())  // more than that many tiles below the panel
+        trsm_lite_kernel<<<dim3(8 * n), dim3(64), 0, s>>>(Acol, lda, k, k + 1, Dinv, kt);
+    else
+        trsm_subst_kernel<<<dim3(2 * n), dim3(256), 0, s>>>(Acol, lda, k, k + 1, Dinv, kt);
 }
 
 void launch_trsm_rows(hipStream_t s, double* Acol, int64_t lda, int k, int bi0, int nrows, const double* Dinv,
