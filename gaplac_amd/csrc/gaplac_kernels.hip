@@ -827,172 +827,6 @@ __device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ Ag, 
     STAMP(19);
 }
 
-// ---------------------------------------------------------------------------------
-// Diagonal block, blocked version (default): 16x16 leaves.
-//
-// Per 16-column panel s only the 16x16 diagonal sub-block is factored serially (wave 0,
-// one row per lane, f16_factor); the 16(7-s) rows below it are solved against it on the
-// other waves (one row per lane, VALU forward substitution, f16_trsm_row), and the
-// trailing sub-blocks get the panel on MFMA (dblk_update). Wave 0 updates the next
-// diagonal sub-block itself and factors it right away, while waves 1-3 update the rest.
-// Two barriers per panel. The serial part per column is only the 16-row pivot chain
-// (readlane pivot -> v_rcp_f64 + 2 Newton steps -> the next column's own update ->
-// readlane), against the whole 128-row panel sweep of the unblocked kernel above.
-// ---------------------------------------------------------------------------------
-
-// Factor the 16x16 diagonal sub-block blk (LDS, column-major) in place: L (upper part
-// zeroed), rdg[c] = 1/L(c,c). Wave-level: lane r (r = lane & 15) holds row r; lanes 16..63
-// mirror lanes 0..15 and never store. Schur updates use A(r,c) A(c2,c) / p (p the pivot),
-// so the chain to the next pivot needs 1/p only; 1/sqrt(p) (the scaled column) is off the
-// chain. Padding columns (>= npiv) get unit pivots; the first pivot <= 0 sets bad.
-__device__ __forceinline__ void f16_factor(double* blk, double* rdg, int lane, int64_t npiv, int& bad) {
-    asm volatile("" : "+v"(lane));  // keep the lane masks inside the loop (see dpanel)
-    const int r = lane & 15;
-    double a[16];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) a[c] = blk[c * 16 + r];
-    double myrd = 1.0;
-    double q = a[0];  // lane c: the updated A(c,c) when column c starts
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        const double piv = readlane_d(q, c);
-        const bool pad = c >= npiv;
-        // OpenBLAS potf2 tests ajj <= 0 only: a NaN pivot propagates (as in the reference)
-        bad = (!pad && piv <= 0.0 && bad == 16) ? c : bad;
-        const double p = pad ? 1.0 : piv;
-        double y = __builtin_amdgcn_rcp(p);  // 1/p: two Newton steps
-        double e = fma(-p, y, 1.0);
-        y = fma(y, e, y);
-        e = fma(-p, y, 1.0);
-        y = fma(y, e, y);
-        const double w = a[c] * y;  // A(r, c) / p
-        if (c < 15) {
-            q = fma(-a[c], w, a[c + 1]);  // lane c+1: next pivot from its own w
-#pragma unroll
-            for (int c2 = c + 1; c2 < 16; ++c2) a[c2] = fma(-a[c], readlane_d(w, c2), a[c2]);
-        }
-        const double z = __builtin_amdgcn_rsq(p);  // 1/sqrt(p), Goldschmidt-refined
-        double g = p * z, h = 0.5 * z;
-        double t = fma(-g, h, 0.5);
-        g = fma(g, t, g);
-        h = fma(h, t, h);
-        t = fma(-g, h, 0.5);
-        g = fma(g, t, g);
-        h = fma(h, t, h);
-        const double rs = h + h;
-        myrd = r == c ? rs : myrd;
-        a[c] = r > c ? a[c] * rs : (r == c ? g : 0.0);
-    }
-    if (lane < 16) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) blk[c * 16 + r] = a[c];
-        rdg[r] = myrd;
-    }
-}
-
-// One row of a sub-block below the diagonal: x <- x L^{-T} (forward substitution against
-// the factored diagonal sub-block Ls; rd = 1/diag). L values are wave-uniform LDS reads.
-__device__ __forceinline__ void f16_trsm_row(double* row, const double* Ls, const double* rd) {
-    double x[16];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) x[c] = row[c * 16];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        x[c] *= rd[c];
-#pragma unroll
-        for (int c2 = c + 1; c2 < 16; ++c2) x[c2] = fma(-x[c], Ls[c * 16 + c2], x[c2]);
-    }
-#pragma unroll
-    for (int c = 0; c < 16; ++c) row[c * 16] = x[c];
-}
-
-__device__ __forceinline__ void potrf_diag_blocked_body(double* __restrict__ Ag, int64_t lda, int64_t N, int64_t g0,
-                                                        double* __restrict__ Dinv, EvalResult* __restrict__ res) {
-    __shared__ double smem[NB + NPK * 256];
-    double* rdiag = smem;
-    double* Ab = smem + NB;
-    __builtin_amdgcn_s_setprio(3);
-    STAMP(99);
-    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-    {
-        const double* colp = Ag + (int64_t)(t >> 4) * lda + (t & 15);
-#pragma unroll
-        for (int J = 0; J < NDB; ++J)
-#pragma unroll
-            for (int I = J; I < NDB; ++I) Ab[bidx(I, J) * 256 + t] = colp[(int64_t)(16 * J) * lda + 16 * I];
-    }
-    STAMP(100);
-    __syncthreads();
-    STAMP(101);
-    int bad = 16, badpanel = -1;
-    if (wave == 0) {
-        f16_factor(Ab, rdiag, lane, N - g0, bad);
-        if (bad < 16) badpanel = 0;
-    }
-    STAMP(102);
-    __syncthreads();
-    for (int s = 0; s < NDB; ++s) {
-        // panel rows below the diagonal sub-block: waves 1..3, one row per lane;
-        // wave 0 inverts the diagonal sub-block for the TRSM kernel (output only)
-        STAMP(4 * s);
-        if (wave == 0) {
-            dinv_diag(Ab, Dinv, rdiag, s, lane);
-            STAMP(4 * s + 1);
-        } else {
-            const double* Ls = Ab + bidx(s, s) * 256;
-            for (int rr = t - 64; rr < 16 * (NDB - 1 - s); rr += 192) {
-                const int I = s + 1 + (rr >> 4);
-                f16_trsm_row(Ab + bidx(I, s) * 256 + (rr & 15), Ls, rdiag + 16 * s);
-            }
-            STAMPT(64, 40 + s);
-        }
-        __syncthreads();
-        STAMP(4 * s + 2);
-        // column s of L is final: store it (waves 1..3; a diagonal sub-block's lower part)
-        if (wave > 0) {
-            const int nel = (NDB - s) * 256;
-            for (int e = t - 64; e < nel; e += 192) {
-                const int I = s + (e >> 8), el = e & 255, c = el >> 4, r = el & 15;
-                if (I != s || r >= c) Ag[(int64_t)(16 * s + c) * lda + 16 * I + r] = Ab[bidx(I, s) * 256 + el];
-            }
-        }
-        if (s == NDB - 1) break;
-        if (wave == 0) {
-            dblk_update(Ab, s + 1, s + 1, s, lane);
-            STAMP(4 * s + 3);
-            int b2 = 16;
-            f16_factor(Ab + bidx(s + 1, s + 1) * 256, rdiag + 16 * (s + 1), lane, N - g0 - 16 * (s + 1), b2);
-            if (b2 < 16 && bad == 16) {
-                bad = b2;
-                badpanel = s + 1;
-            }
-        } else {
-            // trailing sub-blocks (I, J), s+1 <= J <= I <= 7, except (s+1, s+1)
-            const int ntr = (NDB - 1 - s) * (NDB - s) / 2;
-            for (int task = wave; task < ntr; task += 3) {
-                int J = s + 1, rem = task;
-                while (rem >= NDB - J) {
-                    rem -= NDB - J;
-                    ++J;
-                }
-                dblk_update(Ab, J + rem, J, s, lane);
-            }
-            STAMPT(64, 50 + s);
-        }
-        STAMP(60 + s);
-        __syncthreads();
-    }
-    STAMP(103);
-    if (wave == 0 && lane == 0 && badpanel >= 0)
-        atomicMin(&res->info, (unsigned long long)(g0 + 16 * badpanel + bad + 1));
-}
-
-// Diagonal kernel choice (compile time): 1 = the unblocked 128-row panel sweep (default,
-// 39 us alone); 0 = the blocked 16x16-leaf kernel (44 us alone, measured slower: its
-// serial leaf factor costs ~360 cycles per column, as much as the whole-panel sweep).
-#ifndef GAPLAC_DIAG_V1
-#define GAPLAC_DIAG_V1 1
-#endif
 
 // Ag: the diagonal block (global rows/cols g0 .. g0+127) in its storage, leading dim lda.
 __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ Ag, int64_t lda,
@@ -1002,10 +836,7 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ Ag
                                                          KTime* __restrict__ kt) {
     kt_begin(kt);
     if (GAPLAC_YIELD & 1) chain_enter();
-    if constexpr (GAPLAC_DIAG_V1)
-        potrf_diag_kernel_body(Ag, lda, N, g0, Dinv, res);
-    else
-        potrf_diag_blocked_body(Ag, lda, N, g0, Dinv, res);
+    potrf_diag_kernel_body(Ag, lda, N, g0, Dinv, res);
     if (GAPLAC_YIELD & 1) chain_leave();
     kt_end(kt);
 }
@@ -1027,7 +858,7 @@ constexpr int TRSM_LBLK = NDB * (NDB - 1) / 2;  // 28
 // Acol: storage of the panel's first column (global column k*NB), rows global.
 __device__ __forceinline__ void trsm_subst_kernel_body(double* __restrict__ Acol, int64_t lda, int k, int bi0,
                                                          const double* __restrict__ Dinv) {
-    __shared__ double Ls[(TRSM_LBLK + NDB) * 256 + NB];  // + NB: padded to CHAIN_LDS (see LR8)
+    __shared__ double Ls[(TRSM_LBLK + NDB) * 256];
     __builtin_amdgcn_s_setprio(2);  // critical path
     const int tid = threadIdx.x;
     const int bi = bi0 + (int)(blockIdx.x >> 1);
@@ -1333,147 +1164,6 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a) {
 __global__ __launch_bounds__(256, 2) void tile_syrk_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
     tile_syrk_body(a);
-    kt_end(kt);
-}
-
-// ---------------------------------------------------------------------------------
-// Bulk trailing update, 8-wave variant (default): one 128x128 tile per 512-thread
-// workgroup, waves as 2 (rows) x 4 (columns), each a 64x32 sub-tile = 4x2 f64 MFMA
-// accumulators (half the accumulator registers of the 4-wave kernel). Launched with
-// dynamic LDS padding so that ONE such workgroup occupies a CU (2 waves per SIMD): the
-// rest of the CU — 4 KiB short of half its LDS and more than half of every SIMD's
-// registers — stays free for the critical-path kernels (diagonal block, TRSM, column
-// updates), which then start at once instead of waiting for a round of bulk workgroups
-// to retire. Same staging scheme as tile_mma_neg.
-// ---------------------------------------------------------------------------------
-// LDS budget of a CU shared by one bulk workgroup and one critical-path workgroup
-// (measured with tools/coresid_probe.hip and tools/cores2_probe.hip on MI355X). LDS is
-// allocated contiguously per workgroup, and a pair summing to exactly 160 KiB does not
-// fit. The bulk kernel's staging rows are padded (row stride LR8) to 84 KiB, so two bulk
-// workgroups never share a CU, and every LDS-heavy chain kernel (diagonal block, TRSM)
-// takes exactly CHAIN_LDS = 73 KiB: in whichever order the two land on a CU, the hole one
-// leaves is what the other needs (a 72 KiB TRSM at offset 0 would otherwise leave a bulk
-// workgroup at 72..156 KiB and no 73 KiB hole for the next diagonal block until that bulk
-// workgroup retires).
-constexpr int LR8 = 168;  // 86,016 B of staging (the rows past NB are padding)
-constexpr int BULK8_LDS = 2 * 2 * KB * LR8 * 8;
-constexpr int CHAIN_LDS = 8 * (NB + NPK * 256);  // the blocked diagonal kernel's footprint
-static_assert(2 * BULK8_LDS > 163840 && BULK8_LDS + CHAIN_LDS < 163840, "one bulk + one chain workgroup per CU");
-static_assert(8 * ((TRSM_LBLK + NDB) * 256 + NB) == CHAIN_LDS, "TRSM kernel padded to CHAIN_LDS");
-
-__device__ __forceinline__ void tile_mma8_neg(const double* __restrict__ P, const double* __restrict__ Q,
-                                              int64_t ldp, int kdepth, bool active, d4 (&acc)[4][2]) {
-    __shared__ double sm[2][2][KB][LR8];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int wi = w & 1, wj = w >> 1;
-    const int fr = lane >> 4, fc = lane & 15;
-    // staging: thread -> (k rows krow, krow + 8, rows 2 lane, 2 lane + 1) of both operands
-    const int krow = w;  // 0..7
-    const double* Pr = P + (int64_t)krow * ldp + 2 * lane;
-    const double* Qr = Q + (int64_t)krow * ldp + 2 * lane;
-    const int64_t s8 = 8 * ldp;
-    double2 p0, p1, q0, q1;
-#define GAPLAC_GLOAD8(ch)                                                              \
-    do {                                                                               \
-        const int64_t o_ = (int64_t)(ch) * KB * ldp;                                   \
-        p0 = *reinterpret_cast<const double2*>(Pr + o_);                               \
-        q0 = *reinterpret_cast<const double2*>(Qr + o_);                               \
-        if constexpr (KB == 16) {                                                      \
-            p1 = *reinterpret_cast<const double2*>(Pr + o_ + s8);                      \
-            q1 = *reinterpret_cast<const double2*>(Qr + o_ + s8);                      \
-        }                                                                              \
-    } while (0)
-#define GAPLAC_LSTORE8(buf)                                                            \
-    do {                                                                               \
-        double* sp_ = &sm[buf][0][krow][2 * lane];                                     \
-        double* sq_ = &sm[buf][1][krow][2 * lane];                                     \
-        *reinterpret_cast<double2*>(sp_) = make_double2(-p0.x, -p0.y);                 \
-        *reinterpret_cast<double2*>(sq_) = q0;                                         \
-        if constexpr (KB == 16) {                                                      \
-            *reinterpret_cast<double2*>(sp_ + 8 * LR8) = make_double2(-p1.x, -p1.y);   \
-            *reinterpret_cast<double2*>(sq_ + 8 * LR8) = q1;                           \
-        }                                                                              \
-    } while (0)
-
-    GAPLAC_GLOAD8(0);
-    GAPLAC_LSTORE8(0);
-    __syncthreads();
-    const int NCH = kdepth / KB;
-    for (int ch = 0; ch < NCH; ++ch) {
-        const int buf = ch & 1;
-        const bool more = ch + 1 < NCH;
-        if (more) GAPLAC_GLOAD8(ch + 1);
-        if (active) {
-#pragma unroll
-            for (int ks = 0; ks < KB; ks += 4) {
-                double fa[2], fb[4];
-#pragma unroll
-                for (int m = 0; m < 2; ++m) fa[m] = sm[buf][1][ks + fr][32 * wj + 16 * m + fc];
-#pragma unroll
-                for (int m = 0; m < 4; ++m) fb[m] = sm[buf][0][ks + fr][64 * wi + 16 * m + fc];
-#pragma unroll
-                for (int mj = 0; mj < 2; ++mj)
-#pragma unroll
-                    for (int mi = 0; mi < 4; ++mi)
-                        acc[mi][mj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mj], fb[mi], acc[mi][mj], 0, 0, 0);
-            }
-        }
-        if (more) GAPLAC_LSTORE8(buf ^ 1);
-        __syncthreads();
-    }
-#undef GAPLAC_GLOAD8
-#undef GAPLAC_LSTORE8
-}
-
-__global__ __launch_bounds__(512, 1) void tile_syrk8_kernel(BulkArgs a, KTime* __restrict__ kt) {
-    kt_begin(kt);
-    // Tiles of XCD x (= blockIdx % 8) are the contiguous run [x chunk, (x+1) chunk) of the
-    // list. Persistent launches (gridDim < tiles) walk it with stride gridDim / 8.
-    const int chunk = (a.ntiles + 7) >> 3;
-    const int per_xcd = (int)gridDim.x >> 3;
-    const int x = (int)blockIdx.x & 7;
-    for (int k = (int)blockIdx.x >> 3; k < chunk; k += per_xcd) {
-    const int idx = x * chunk + k;
-    if (idx >= a.ntiles) break;
-    {
-        int bi, bj, lj;
-        tile_decode(a, idx, bi, bj, lj);
-        const int64_t r0 = (int64_t)bi * NB;
-        const int64_t ldc = a.ldc;
-        double* __restrict__ Ct = a.C + (int64_t)lj * NB * ldc + r0;
-        const double* __restrict__ P = a.pn.P + (r0 - a.pn.row0);
-        const double* __restrict__ Q = a.pn.P + ((int64_t)bj * NB - a.pn.row0);
-        const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-        const int wi = w & 1, wj = w >> 1;
-        // on a diagonal tile, waves with rows 0..63 and columns 64..127 lie above it
-        const bool active = !(bi == bj && wi == 0 && wj >= 2);
-        const int fr = lane >> 4, fc = lane & 15;
-        d4 acc[4][2];
-        if (active) {
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi) {
-                const double* Ci = Ct + 64 * wi + 16 * mi + fc;
-#pragma unroll
-                for (int mj = 0; mj < 2; ++mj)
-#pragma unroll
-                    for (int rg = 0; rg < 4; ++rg)
-                        acc[mi][mj][rg] = Ci[(int64_t)(32 * wj + 16 * mj + fr + 4 * rg) * ldc];
-            }
-        }
-        tile_mma8_neg(P, Q, a.pn.ld, a.kdepth, active, acc);
-        if (active) {
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi) {
-                double* Ci = Ct + 64 * wi + 16 * mi + fc;
-#pragma unroll
-                for (int mj = 0; mj < 2; ++mj)
-#pragma unroll
-                    for (int rg = 0; rg < 4; ++rg)
-                        Ci[(int64_t)(32 * wj + 16 * mj + fr + 4 * rg) * ldc] = acc[mi][mj][rg];
-            }
-        }
-    }
-    }
     kt_end(kt);
 }
 
@@ -2237,19 +1927,6 @@ void launch_trsm_rows(hipStream_t s, double* Acol, int64_t lda, int k, int bi0, 
 
 bool syrk_is_small(int ntiles) { return ntiles <= QUAD_BULK_MAX_TILES; }
 
-// Bulk kernel choice (GAPLAC_BULK8, read once): 0 = the 4-wave tile kernel, two workgroups
-// per CU (default); 1 = 8-wave tile kernel, one workgroup per CU beside one chain
-// workgroup; 2 = the same, persistent (one workgroup per CU walking its tiles). Measured
-// at N=16384: 31.5 / 32.5 / 35.2 ms per evaluation — the chain kernels co-reside under 1
-// and 2 but still run 2-4x slower beside MFMA-saturating bulk waves.
-static int bulk8_mode() {
-    static const int m = [] {
-        const char* s = std::getenv("GAPLAC_BULK8");
-        return s ? std::atoi(s) : 0;
-    }();
-    return m;
-}
-
 static int device_cus() {
     static const int n = [] {
         int dev = 0, cus = 0;
@@ -2277,9 +1954,6 @@ void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt) {
     int grid = ((a.ntiles + 7) >> 3) << 3;
     if (syrk_is_small(a.ntiles)) {
         quad_bulk_kernel<<<dim3((unsigned)(4 * grid)), dim3(256), 0, s>>>(a, kt);
-    } else if (bulk8_mode()) {
-        if (bulk8_mode() == 2) grid = std::min(grid, device_cus());
-        tile_syrk8_kernel<<<dim3((unsigned)grid), dim3(512), 0, s>>>(a, kt);
     } else
         tile_syrk_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
 }

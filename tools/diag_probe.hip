@@ -1,6 +1,7 @@
-// Diagnostic: the diagonal-block kernels on an idle GPU. Checks the blocked kernel
-// (default) against a CPU Cholesky of the same 128x128 block (L and the 16x16 inverses),
-// times it against the unblocked kernel (v1), and times the other chain kernels alone.
+// Diagnostic: the diagonal-block kernel on an idle GPU. Checks it against a CPU Cholesky of
+// the same 128x128 block (L and the 16x16 inverses), prints its per-wave stamps per panel
+// (the "v1" lines; the blocked 16x16-leaf variant that was "v2" was measured slower and
+// removed), and times the other chain kernels alone.
 #define GAPLAC_STAMPS 1
 #include "../gaplac_amd/csrc/gaplac_kernels.hip"
 #include <cmath>
@@ -11,9 +12,6 @@ using namespace gaplac;
 
 __global__ __launch_bounds__(256) void diag_v1(double* Ag, int64_t lda, int64_t N, int64_t g0, double* Dinv, EvalResult* res) {
   potrf_diag_kernel_body(Ag, lda, N, g0, Dinv, res);
-}
-__global__ __launch_bounds__(256) void diag_v2(double* Ag, int64_t lda, int64_t N, int64_t g0, double* Dinv, EvalResult* res) {
-  potrf_diag_blocked_body(Ag, lda, N, g0, Dinv, res);
 }
 
 int main() {
@@ -42,14 +40,13 @@ int main() {
   CK(hipMalloc(&res, sizeof(EvalResult)));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   std::vector<double> out(h.size()), dinv(DINV_PER_BLOCK);
-  for (int v = 1; v <= 2; ++v) {
+  for (int v = 1; v <= 1; ++v) {
     for (int rep = 0; rep < 4; ++rep) {
       CK(hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice));
       launch_init_result(0, res);
       CK(hipDeviceSynchronize());
       CK(hipEventRecord(e0));
       if (v == 1) diag_v1<<<1, 256>>>(A, Np, 1 << 30, 0, Dinv, res);
-      else diag_v2<<<1, 256>>>(A, Np, 1 << 30, 0, Dinv, res);
       CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
       CK(hipMemcpy(out.data(), A, out.size() * 8, hipMemcpyDeviceToHost));
@@ -78,32 +75,15 @@ int main() {
         }
         printf("  v1 last dinv+store %llu total %llu cycles\n", st[19] - st[17], st[19] - st[20]);
       }
-      if (v == 2 && rep == 3) {
-        unsigned long long st[128]; CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof st));
-        const unsigned long long b = st[99];
-        printf("  load %llu  barrier %llu  f16(0) %llu\n", st[100] - b, st[101] - st[100], st[102] - st[101]);
-        unsigned long long prev = st[102];
-        for (int s = 0; s < 8; ++s) {
-          printf("  s=%d: [w0] ->T %5llu dinv %5llu T-barrier %5llu", s, st[4 * s] - prev, st[4 * s + 1] - st[4 * s], st[4 * s + 2] - st[4 * s + 1]);
-          printf(" [w1] trsm %5llu", st[40 + s] - st[4 * s]);
-          if (s < 7) {
-            printf(" [w0] upd %5llu f16 %5llu [w1] store+upd %5llu U-barrier(w0 view) %5llu\n", st[4 * s + 3] - st[4 * s + 2],
-                   st[60 + s] - st[4 * s + 3], st[50 + s] - st[4 * s + 2], st[4 * s + 4] - st[60 + s]);
-            prev = st[4 * s + 4];
-          } else printf("\n");
-        }
-        printf("  end %llu total %llu cycles\n", st[103] - st[4 * 7 + 2], st[103] - b);
-      }
     }
   }
   // non-PD: zero the block's (37,37) pivot region -> info must be 38 in both
-  for (int v = 1; v <= 2; ++v) {
+  for (int v = 1; v <= 1; ++v) {
     std::vector<double> hb = h;
     for (int i = 0; i < Np; ++i) { hb[(size_t)37 * Np + i] = 0; hb[(size_t)i * Np + 37] = 0; }
     CK(hipMemcpy(A, hb.data(), hb.size() * 8, hipMemcpyHostToDevice));
     launch_init_result(0, res);
     if (v == 1) diag_v1<<<1, 256>>>(A, Np, 1 << 30, 0, Dinv, res);
-    else diag_v2<<<1, 256>>>(A, Np, 1 << 30, 0, Dinv, res);
     EvalResult hr; CK(hipMemcpy(&hr, res, sizeof hr, hipMemcpyDeviceToHost));
     printf("non-PD v%d: info %llu (expect 38)\n", v, (unsigned long long)hr.info);
   }
