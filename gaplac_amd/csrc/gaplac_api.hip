@@ -70,6 +70,7 @@ struct gaplac_ctx {
     int tail_m = 0;       // GAPLAC_TAIL_M / GAPLAC_TAIL_W: once at most tail_m tile columns remain,
     int tail_w = 0;       //   super-panels are tail_w wide (plain logpdf only; 0 = off)
     int tail_s = 32;      // GAPLAC_TAIL_S: the last ~tail_s tile columns run serially on one stream
+    int head_w = 0;       // GAPLAC_HEAD_W: width of the first super-panel (0 = spw)
     int diag_first_m = 0; // GAPLAC_DIAG_FIRST_M: bulk updates of <= this many tile rows wait for the
                           //   next super-panel's first diagonal block + TRSM
     int gram_queue = 2;   // GAPLAC_GRAM_QUEUE: second Gram launch as a work queue of this many
@@ -416,7 +417,8 @@ static std::vector<int> superpanel_starts(const gaplac_ctx* ctx, int nt) {
     while (c < nt) {
         if (ctx->xr_mode == 0 && ctx->tail_s > 0 && c > 0 && nt - c <= ctx->tail_s) break;
         const bool tail = ctx->xr_mode == 0 && ctx->tail_w > 0 && nt - c <= ctx->tail_m && c > 0;
-        c = std::min(c + (tail ? ctx->tail_w : ctx->spw), nt);
+        const bool head = ctx->xr_mode == 0 && c == 0 && ctx->head_w > 0;  // within Gram part 1
+        c = std::min(c + (head ? std::min(ctx->head_w, ctx->spw) : tail ? ctx->tail_w : ctx->spw), nt);
         sp.push_back(c);
     }
     return sp;
@@ -958,6 +960,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_TAIL_S")) ctx->tail_s = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_GRAM_QUEUE")) ctx->gram_queue = std::max(0, std::min(4, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_DIAG_FIRST_M")) ctx->diag_first_m = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_HEAD_W")) ctx->head_w = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     auto fail = [&](const char* what, hipError_t e) {
