@@ -343,10 +343,11 @@ int accumulate_slots(gaplac_ctx* ctx, const std::vector<gaplac_ctx::Slot>& slots
 // ~10 us fixed (C load, first staging, epilogue) + K at the MFMA ceiling, so larger K
 // amortises the fixed part (and cuts C-tile HBM traffic per flop by W).
 //
-// Two streams. s_panel (highest priority, all CUs) runs the critical path in order;
-// s_main (CU-masked when available: GAPLAC_DIAG_CUS CUs, default 1, excluded) runs the
-// bulk updates. In eager mode the excluded CU keeps a free slot for the diagonal kernel;
-// in graph mode (default) the kernels are slot-compatible anyway.
+// Two streams, eager launches (GAPLAC_GRAPH=1 captures and replays instead). s_panel
+// (highest priority, all CUs) runs the critical path in order; s_main (lowest priority;
+// optionally CU-masked, GAPLAC_DIAG_CUS, off by default) runs the Gram and the bulk
+// updates. Super-panel boundaries come from superpanel_starts() (width spw; the last
+// ~tail_s tile columns are factored by serial_tail() on s_main alone).
 //   s_panel: wait R(p-1) | col_update(columns of SP p+1, with SP p, K=128W)
 //            | for each column c of SP p+1: [col_update(c with c-1..first, K=128)] potrf(c) trsm(c)
 //            | rec P(p+1)
