@@ -71,6 +71,10 @@ struct gaplac_ctx {
     int tail_w = 0;       //   super-panels are tail_w wide (plain logpdf only; 0 = off)
     int tail_s = 32;      // GAPLAC_TAIL_S: the last ~tail_s tile columns run serially on one stream
     int head_w = 0;       // GAPLAC_HEAD_W: width of the first super-panel (0 = spw)
+    int persist_m = 0;    // GAPLAC_PERSIST_M: bulk updates of <= this many tile rows run on a capped
+    int persist_t = 1;    //   grid, GAPLAC_PERSIST_T tile / GAPLAC_PERSIST_Q quadrant workgroups per
+    int persist_q = 1;    //   CU, so the panel chain's workgroups always find room (0 = off)
+    int ncu = 256;        // compute units of the device
     int diag_first_m = 0; // GAPLAC_DIAG_FIRST_M: bulk updates of <= this many tile rows wait for the
                           //   next super-panel's first diagonal block + TRSM
     int gram_queue = 2;   // GAPLAC_GRAM_QUEUE: second Gram launch as a work queue of this many
@@ -495,6 +499,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
                         ColMap{1, 0, W}};
             ba.yield = (m <= ctx->yield_m && sp != sm) ? 1 : 0;
             const bool small = syrk_is_small(ba.ntiles);
+            if (m <= ctx->persist_m && sp != sm) ba.persist = (small ? ctx->persist_q : ctx->persist_t) * ctx->ncu;
             KTime* kt = small ? slot(ctx, 6, 0) : slot(ctx, 0, syrk_flops(m) * (kd / NB), syrk_bytes(m, kd));
             const bool ev = ctx->prof_mode == 2 && !small;
             size_t e0 = 0;
@@ -962,6 +967,9 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_GRAM_QUEUE")) ctx->gram_queue = std::max(0, std::min(4, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_DIAG_FIRST_M")) ctx->diag_first_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_HEAD_W")) ctx->head_w = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_PERSIST_M")) ctx->persist_m = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_PERSIST_T")) ctx->persist_t = std::max(1, std::min(2, std::atoi(s)));
+    if (const char* s = std::getenv("GAPLAC_PERSIST_Q")) ctx->persist_q = std::max(1, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     auto fail = [&](const char* what, hipError_t e) {
@@ -979,6 +987,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     int ncu = 0;
     if ((e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
         return fail("attribute", e);
+    if (ncu > 0) ctx->ncu = ncu;
     int least = 0, greatest = 0;
     if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess)
         return fail("priority range", e);

@@ -1119,8 +1119,7 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
 #undef GAPLAC_LSTORE
 }
 
-__device__ __forceinline__ void tile_syrk_body(const BulkArgs& a) {
-    const int b = (int)blockIdx.x;
+__device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
     const int chunk = (a.ntiles + 7) >> 3;
     const int idx = (b & 7) * chunk + (b >> 3);
     if (idx >= a.ntiles) return;
@@ -1161,9 +1160,13 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a) {
     }
 }
 
+// A capped grid (BulkArgs.persist, a multiple of 8) walks the virtual blocks with stride
+// gridDim.x, which keeps every block's XCD (b % 8) and leaves room on each CU for the
+// panel chain's workgroups.
 __global__ __launch_bounds__(256, 2) void tile_syrk_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
-    tile_syrk_body(a);
+    const int nb = ((a.ntiles + 7) >> 3) << 3;
+    for (int b = (int)blockIdx.x; b < nb; b += (int)gridDim.x) tile_syrk_body(a, b);
     kt_end(kt);
 }
 
@@ -1278,14 +1281,18 @@ __global__ __launch_bounds__(256) void col_update_kernel(double* __restrict__ C,
 // workgroups per tile (XCD-chunked like the tile kernel).
 __global__ __launch_bounds__(256) void quad_bulk_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
-    const int b = (int)blockIdx.x >> 2, q = (int)blockIdx.x & 3;
     const int chunk = (a.ntiles + 7) >> 3;
-    const int idx = (b & 7) * chunk + (b >> 3);
-    if (idx < a.ntiles) {
-        int bi, bj, lj;
-        tile_decode(a, idx, bi, bj, lj);
-        const int qi = q >> 1, qj = q & 1;
-        if (!(bi == bj && qj > qi)) quad_update(a.C, a.ldc, a.pn, bi, bj, lj, qi, qj, a.kdepth, a.yield != 0);
+    const int nvb = 4 * (chunk << 3);
+    // capped grid (a multiple of 32): the stride keeps (vb >> 2) % 8, i.e. the XCD
+    for (int vb = (int)blockIdx.x; vb < nvb; vb += (int)gridDim.x) {
+        const int b = vb >> 2, q = vb & 3;
+        const int idx = (b & 7) * chunk + (b >> 3);
+        if (idx < a.ntiles) {
+            int bi, bj, lj;
+            tile_decode(a, idx, bi, bj, lj);
+            const int qi = q >> 1, qj = q & 1;
+            if (!(bi == bj && qj > qi)) quad_update(a.C, a.ldc, a.pn, bi, bj, lj, qi, qj, a.kdepth, a.yield != 0);
+        }
     }
     kt_end(kt);
 }
@@ -1953,9 +1960,13 @@ void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt) {
     if (!guard_launch("bulk update", a.C, 0, tiles_end(a.ldc, a.bi0 + max_r, a.lj0 + max_c))) return;
     int grid = ((a.ntiles + 7) >> 3) << 3;
     if (syrk_is_small(a.ntiles)) {
-        quad_bulk_kernel<<<dim3((unsigned)(4 * grid)), dim3(256), 0, s>>>(a, kt);
-    } else
+        int qg = 4 * grid;
+        if (a.persist > 0) qg = std::min(qg, std::max(32, a.persist & ~31));
+        quad_bulk_kernel<<<dim3((unsigned)qg), dim3(256), 0, s>>>(a, kt);
+    } else {
+        if (a.persist > 0) grid = std::min(grid, std::max(8, a.persist & ~7));
         tile_syrk_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
+    }
 }
 
 void launch_col_update(hipStream_t s, double* C, int64_t ldc, const Panel& pn, int nt, int jb, int lj0,
