@@ -28,7 +28,7 @@ struct gaplac_ctx {
     hipStream_t s_extra = nullptr;  // extra rows (gradient / posterior), beside the bulk updates
     hipEvent_t ev_xinit = nullptr, ev_xdone = nullptr;
     int diag_cus = 0;  // CUs masked out of s_main for the diagonal kernel (0: no mask)
-    hipEvent_t ev_P[2] = {}, ev_R[2] = {}, ev_L[2] = {}, ev_D[2] = {}, ev_gram = nullptr, ev_gram2 = nullptr;
+    hipEvent_t ev_P[2] = {}, ev_R[2] = {}, ev_L[2] = {}, ev_D[2] = {}, ev_S[2] = {}, ev_gram = nullptr, ev_gram2 = nullptr;
     // bulk updates of at most this many tiles wait for the step's lookahead column update
     // (GAPLAC_LA_FIRST): late in the factorisation the panel chain is the critical path
     int la_first = 0;
@@ -71,6 +71,7 @@ struct gaplac_ctx {
     int tail_w = 0;       //   super-panels are tail_w wide (plain logpdf only; 0 = off)
     int tail_s = 32;      // GAPLAC_TAIL_S: the last ~tail_s tile columns run serially on one stream
     int head_w = 0;       // GAPLAC_HEAD_W: width of the first super-panel (0 = spw)
+    int la_split_m = 0;   // GAPLAC_LA_SPLIT_M: split lookahead when <= this many tile rows follow SP p+1
     int persist_m = 0;    // GAPLAC_PERSIST_M: bulk updates of <= this many tile rows run on a capped
     int persist_t = 1;    //   grid, GAPLAC_PERSIST_T tile / GAPLAC_PERSIST_Q quadrant workgroups per
     int persist_q = 1;    //   CU, so the panel chain's workgroups always find room (0 = off)
@@ -361,9 +362,12 @@ int accumulate_slots(gaplac_ctx* ctx, const std::vector<gaplac_ctx::Slot>& slots
 // R(p-1) and SP p in the lookahead col_update; within a step the streams touch disjoint
 // tile columns. Events ping-pong (p & 1).
 // after_first: recorded once the first column's diagonal block and TRSM are enqueued.
+// Columns cs .. ce-1 of the super-panel c0 .. c1-1 (default: all of them).
 int factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, int nt, int c0, int c1,
-                      hipEvent_t after_first = nullptr) {
-    for (int c = c0; c < c1; ++c) {
+                      hipEvent_t after_first = nullptr, int cs = -1, int ce = -1) {
+    if (cs < 0) cs = c0;
+    if (ce < 0) ce = c1;
+    for (int c = cs; c < ce; ++c) {
         double* Acol = ctx->A + (int64_t)c * NB * lda;
         if (c > c0)
             launch_col_update(sp, ctx->A, lda, Panel{Acol - NB * lda, lda, 0}, nt, c, c, c1 - c, NB,
@@ -471,8 +475,24 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             else
                 HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_gram2, 0));  // rest of the Gram built
             const int c2 = spc[(size_t)p + 2];
-            launch_col_update(sp, ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nt, c1, c1, c2 - c1, kd,
-                              slot(ctx, 5, 0));
+            // Split lookahead (GAPLAC_LA_SPLIT_M, chain-bound steps): the panel chain applies
+            // SP p to the first column of SP p+1 only and factors it, while s_main applies SP
+            // p to the other columns of SP p+1 ahead of its bulk update (event S(p)).
+            const int mb0 = nt - (p + 2 <= nsp ? spc[(size_t)p + 2] : spc[(size_t)nsp]);
+            const bool split = sp != sm && c2 - c1 > 1 && mb0 > 0 && mb0 <= ctx->la_split_m;
+            launch_col_update(sp, ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nt, c1, c1,
+                              split ? 1 : c2 - c1, kd, slot(ctx, 5, 0));
+            if (split) {
+                if ((frc = factor_superpanel(ctx, sp, N, lda, nt, c1, c2, nullptr, c1, c1 + 1))) return frc;
+                HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_P[p & 1], 0));
+                launch_col_update(sm, ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nt, c1 + 1,
+                                  c1 + 1, c2 - c1 - 1, kd, slot(ctx, 5, 0));
+                HIPQ(ctx, hipEventRecord(ctx->ev_S[p & 1], sm));
+                HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_S[p & 1], 0));
+                if ((frc = factor_superpanel(ctx, sp, N, lda, nt, c1, c2, nullptr, c1 + 1, c2))) return frc;
+                HIPQ(ctx, hipEventRecord(ctx->ev_P[(p + 1) & 1], sp));
+                goto bulk;
+            }
             // only GAPLAC_LA_FIRST waits on L(p); an unneeded record costs ~6 us of dispatch
             // latency on the chain
             if (ctx->la_first > 0) HIPQ(ctx, hipEventRecord(ctx->ev_L[p & 1], sp));
@@ -487,10 +507,12 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             HIPQ(ctx, hipEventRecord(ctx->ev_P[(p + 1) & 1], sp));
         }
         HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_P[p & 1], 0));
+    bulk:
         if (diag_first) HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_D[p & 1], 0));
         // tile columns after SP p+1; the last super-panel also updates a serial tail
         const int jb = p + 2 <= nsp ? spc[(size_t)p + 2] : spc[(size_t)nsp];
-        if (p + 1 < nsp && jb < nt && sp != sm && (nt - jb) * (nt - jb + 1) / 2 <= ctx->la_first)
+        if (p + 1 < nsp && jb < nt && sp != sm && ctx->la_split_m == 0 &&
+            (nt - jb) * (nt - jb + 1) / 2 <= ctx->la_first)
             HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_L[p & 1], 0));
         if (jb < nt) {
             const int m = nt - jb;
@@ -967,6 +989,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_GRAM_QUEUE")) ctx->gram_queue = std::max(0, std::min(4, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_DIAG_FIRST_M")) ctx->diag_first_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_HEAD_W")) ctx->head_w = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_LA_SPLIT_M")) ctx->la_split_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_PERSIST_M")) ctx->persist_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_PERSIST_T")) ctx->persist_t = std::max(1, std::min(2, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_PERSIST_Q")) ctx->persist_q = std::max(1, std::min(8, std::atoi(s)));
@@ -1015,6 +1038,8 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
         if ((e = hipEventCreateWithFlags(&ctx->ev_L[q], hipEventDisableTiming)) != hipSuccess)
             return fail("event", e);
         if ((e = hipEventCreateWithFlags(&ctx->ev_D[q], hipEventDisableTiming)) != hipSuccess)
+            return fail("event", e);
+        if ((e = hipEventCreateWithFlags(&ctx->ev_S[q], hipEventDisableTiming)) != hipSuccess)
             return fail("event", e);
     }
     if ((e = hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming)) != hipSuccess)
@@ -1065,6 +1090,7 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
         if (ctx->ev_R[q]) (void)hipEventDestroy(ctx->ev_R[q]);
         if (ctx->ev_L[q]) (void)hipEventDestroy(ctx->ev_L[q]);
         if (ctx->ev_D[q]) (void)hipEventDestroy(ctx->ev_D[q]);
+        if (ctx->ev_S[q]) (void)hipEventDestroy(ctx->ev_S[q]);
     }
     if (ctx->ev_gram) (void)hipEventDestroy(ctx->ev_gram);
     if (ctx->ev_gram2) (void)hipEventDestroy(ctx->ev_gram2);
