@@ -71,6 +71,7 @@ struct gaplac_ctx {
     int tail_w = 0;       //   super-panels are tail_w wide (plain logpdf only; 0 = off)
     int tail_s = 32;      // GAPLAC_TAIL_S: the last ~tail_s tile columns run serially on one stream
     int head_w = 0;       // GAPLAC_HEAD_W: width of the first super-panel (0 = spw)
+    int pair_m = 0;       // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
     int la_split_m = 0;   // GAPLAC_LA_SPLIT_M: split lookahead when <= this many tile rows follow SP p+1
     int persist_m = 0;    // GAPLAC_PERSIST_M: bulk updates of <= this many tile rows run on a capped
     int persist_t = 1;    //   grid, GAPLAC_PERSIST_T tile / GAPLAC_PERSIST_Q quadrant workgroups per
@@ -465,6 +466,35 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     int frc;
     if ((frc = factor_superpanel(ctx, sp, N, lda, nt, spc[0], spc[1]))) return frc;
     HIPQ(ctx, hipEventRecord(ctx->ev_P[0], sp));
+    // bulk trailing update of the triangle of tile columns >= j0 with the panel pn (K = kd)
+    auto bulk_tri = [&](int j0, const Panel& pn, int kdep) -> int {
+        if (j0 >= nt) return 0;
+        const int m = nt - j0;
+        BulkArgs ba{ctx->A, lda, pn, ctx->tiles + ctx->tile_off[(size_t)m], m * (m + 1) / 2, kdep, j0, j0,
+                    ColMap{1, 0, W}};
+        ba.yield = (m <= ctx->yield_m && sp != sm) ? 1 : 0;
+        const bool small = syrk_is_small(ba.ntiles);
+        if (m <= ctx->persist_m && sp != sm) ba.persist = (small ? ctx->persist_q : ctx->persist_t) * ctx->ncu;
+        KTime* kt = small ? slot(ctx, 6, 0) : slot(ctx, 0, syrk_flops(m) * (kdep / NB), syrk_bytes(m, kdep));
+        const bool ev = ctx->prof_mode == 2 && !small;
+        size_t e0 = 0;
+        if (ev) {
+            e0 = 2 * ctx->evpairs.size();
+            while (ctx->evpool.size() < e0 + 2) {
+                hipEvent_t e;
+                HIPQ(ctx, hipEventCreate(&e));
+                ctx->evpool.push_back(e);
+            }
+            HIPQ(ctx, hipEventRecord(ctx->evpool[e0], sm));
+        }
+        launch_bulk(sm, ba, kt);
+        if (ev) {
+            HIPQ(ctx, hipEventRecord(ctx->evpool[e0 + 1], sm));
+            ctx->evpairs.push_back({e0, syrk_flops(m) * (kdep / NB), syrk_bytes(m, kdep), 0});
+        }
+        return 0;
+    };
+    int pend = -1;  // first super-panel not yet applied beyond the band (paired updates)
     for (int p = 0; p < nsp; ++p) {
         bool diag_first = false;
         const int c0 = spc[(size_t)p], c1 = spc[(size_t)p + 1];
@@ -514,33 +544,24 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         if (p + 1 < nsp && jb < nt && sp != sm && ctx->la_split_m == 0 &&
             (nt - jb) * (nt - jb + 1) / 2 <= ctx->la_first)
             HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_L[p & 1], 0));
-        if (jb < nt) {
-            const int m = nt - jb;
-            BulkArgs ba{ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0},
-                        ctx->tiles + ctx->tile_off[(size_t)m], m * (m + 1) / 2, kd, jb, jb,
-                        ColMap{1, 0, W}};
-            ba.yield = (m <= ctx->yield_m && sp != sm) ? 1 : 0;
-            const bool small = syrk_is_small(ba.ntiles);
-            if (m <= ctx->persist_m && sp != sm) ba.persist = (small ? ctx->persist_q : ctx->persist_t) * ctx->ncu;
-            KTime* kt = small ? slot(ctx, 6, 0) : slot(ctx, 0, syrk_flops(m) * (kd / NB), syrk_bytes(m, kd));
-            const bool ev = ctx->prof_mode == 2 && !small;
-            size_t e0 = 0;
-            if (ev) {
-                e0 = 2 * ctx->evpairs.size();
-                while (ctx->evpool.size() < e0 + 2) {
-                    hipEvent_t e;
-                    HIPQ(ctx, hipEventCreate(&e));
-                    ctx->evpool.push_back(e);
-                }
-                HIPQ(ctx, hipEventRecord(ctx->evpool[e0], sm));
-            }
-            launch_bulk(sm, ba, kt);
-            if (ev) {
-                HIPQ(ctx, hipEventRecord(ctx->evpool[e0 + 1], sm));
-                ctx->evpairs.push_back({e0, syrk_flops(m) * (kd / NB), syrk_bytes(m, kd), 0});
-            }
+        // Paired bulk updates (GAPLAC_PAIR_M): at a deferring step only the next-needed band
+        // (SP p+2's columns) gets SP p, and the tile columns after it get SPs p and p+1 in
+        // one K = 2 x 128W update at step p+1 (band first, then R(p), then the rest).
+        const int je = p + 3 <= nsp ? spc[(size_t)p + 3] : spc[(size_t)nsp];
+        const int pc = pend >= 0 ? spc[(size_t)pend] : c0;  // first column of the pending SPs
+        const int kdp = (c1 - pc) * NB;
+        const Panel pnl{ctx->A + (int64_t)pc * NB * lda, lda, 0};
+        const bool defer = ctx->pair_m > 0 && pend < 0 && p + 1 < nsp && sp != sm && !ctx->xr_mode && je > jb &&
+                           nt - je >= ctx->pair_m;
+        if (pend >= 0 || defer) {
+            if (je > jb) launch_col_update(sm, ctx->A, lda, pnl, nt, jb, jb, je - jb, kdp, slot(ctx, 5, 0));
+            HIPQ(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
+            if (!defer && (frc = bulk_tri(je, pnl, kdp))) return frc;
+            pend = defer ? p : -1;
+        } else {
+            if ((frc = bulk_tri(jb, pnl, kd))) return frc;
+            HIPQ(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
         }
-        HIPQ(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
         if (ctx->xr_mode) {
             // extra rows on their own stream: they only need SP p final (P(p)) and touch
             // rows no other stream writes, so they fill the bulk stream's idle time
@@ -989,6 +1010,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_GRAM_QUEUE")) ctx->gram_queue = std::max(0, std::min(4, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_DIAG_FIRST_M")) ctx->diag_first_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_HEAD_W")) ctx->head_w = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_PAIR_M")) ctx->pair_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_LA_SPLIT_M")) ctx->la_split_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_PERSIST_M")) ctx->persist_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_PERSIST_T")) ctx->persist_t = std::max(1, std::min(2, std::atoi(s)));

@@ -10,6 +10,8 @@ these sizes) and agree with the default schedule.
 * GAPLAC_SPW: the super-panel width;
 * GAPLAC_LA_SPLIT_M: the lookahead of all but a super-panel's first column on the bulk
   stream (1000: every step);
+* GAPLAC_PAIR_M: paired bulk updates (every other step the columns beyond the next band
+  receive two super-panels at once; 1: whenever possible);
 * GAPLAC_PERSIST_M / _T / _Q: bulk updates on a capped grid whose workgroups loop over
   the tiles (1000 applies it to every step; N = 9000 runs the 128x128 tile kernel so).
 The settings are read when a context is created (gaplac_ctx_create).
@@ -39,6 +41,9 @@ SCHEDULES = {
     "persist_all_t2_q3": {"GAPLAC_PERSIST_M": "1000", "GAPLAC_PERSIST_T": "2", "GAPLAC_PERSIST_Q": "3"},
     "la_split_all": {"GAPLAC_LA_SPLIT_M": "1000", "GAPLAC_TAIL_S": "0"},
     "la_split_persist": {"GAPLAC_LA_SPLIT_M": "1000", "GAPLAC_PERSIST_M": "1000"},
+    "pair_all": {"GAPLAC_PAIR_M": "1"},
+    "pair_no_tail_split_persist": {"GAPLAC_PAIR_M": "1", "GAPLAC_TAIL_S": "0", "GAPLAC_LA_SPLIT_M": "1000",
+                                   "GAPLAC_PERSIST_M": "1000"},
 }
 SIZES = [1, 127, 129, 700, 2049, 3000, 9000]
 TERMS = [(SQEXP, 0, 1.5, 0), (OU, 0, 3.0, 1), (CAT, 1, 0.0, 2), (NOISE, -1, 1.0, 3)]
