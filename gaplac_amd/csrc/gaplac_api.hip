@@ -43,6 +43,9 @@ struct gaplac_ctx {
     size_t tiles_elems = 0;
     int tiles_nt = 0;
     std::vector<size_t> tile_off;
+    // band lists (paired updates): tile columns 0 .. spw-1 of an m-row trailing matrix, rows
+    // r >= c, rows outer; packed after the triangle lists, band_off[m] into tiles
+    std::vector<size_t> band_off;
     double* dX = nullptr;
     size_t dX_elems = 0;
     double* dv = nullptr;
@@ -554,7 +557,17 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         const bool defer = ctx->pair_m > 0 && pend < 0 && p + 1 < nsp && sp != sm && !ctx->xr_mode && je > jb &&
                            nt - je >= ctx->pair_m;
         if (pend >= 0 || defer) {
-            if (je > jb) launch_col_update(sm, ctx->A, lda, pnl, nt, jb, jb, je - jb, kdp, slot(ctx, 5, 0));
+            const int mbd = nt - jb;
+            if (je > jb && je - jb == W && ctx->band_off.size() > (size_t)mbd) {
+                // the band through the tile kernel (a list of its tiles; quadrants if small)
+                BulkArgs ba{ctx->A, lda, pnl, ctx->tiles + ctx->band_off[(size_t)mbd],
+                            W * mbd - W * (W - 1) / 2, kdp, jb, jb, ColMap{1, 0, W}};
+                ba.max_r = mbd - 1;
+                ba.max_c = W - 1;
+                launch_bulk(sm, ba, slot(ctx, 5, 0));
+            } else if (je > jb) {
+                launch_col_update(sm, ctx->A, lda, pnl, nt, jb, jb, je - jb, kdp, slot(ctx, 5, 0));
+            }
             HIPQ(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
             if (!defer && (frc = bulk_tri(je, pnl, kdp))) return frc;
             pend = defer ? p : -1;
@@ -585,9 +598,22 @@ int ensure_tile_lists(gaplac_ctx* ctx, int nt) {
     if (ctx->tiles_nt >= nt) return 0;
     std::vector<size_t> off((size_t)nt + 1, 0);
     for (int m = 1; m <= nt; ++m) off[(size_t)m] = off[(size_t)m - 1] + (size_t)(m - 1) * m / 2;
-    const size_t total = off[(size_t)nt] + (size_t)nt * (nt + 1) / 2;
+    const size_t tri_total = off[(size_t)nt] + (size_t)nt * (nt + 1) / 2;
+    const int w = ctx->spw;
+    size_t total = tri_total;
+    for (int m = 1; m <= nt; ++m) total += (size_t)std::min(w, m) * m - (size_t)std::min(w, m) * (std::min(w, m) - 1) / 2;
     std::vector<uint32_t> host(total);
     for (int m = 1; m <= nt; ++m) build_tile_list(m, host.data() + off[(size_t)m]);
+    {
+        size_t k = tri_total;
+        ctx->band_off.assign((size_t)nt + 1, tri_total);
+        for (int m = 1; m <= nt; ++m) {
+            ctx->band_off[(size_t)m] = k;
+            for (int r = 0; r < m; ++r)
+                for (int c = 0; c < w && c <= r; ++c) host[k++] = (uint32_t)r | ((uint32_t)c << 16);
+        }
+        if (k != total) return set_err(ctx, GAPLAC_E_ARG, "band list size mismatch");
+    }
     int rc;
     if ((rc = ensure(ctx, &ctx->tiles, &ctx->tiles_elems, total))) return rc;
     HIPCK(ctx, hipMemcpy(ctx->tiles, host.data(), total * sizeof(uint32_t), hipMemcpyHostToDevice));
