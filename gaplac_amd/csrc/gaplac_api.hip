@@ -74,6 +74,7 @@ struct gaplac_ctx {
     int tail_w = 0;       //   super-panels are tail_w wide (plain logpdf only; 0 = off)
     int tail_s = 32;      // GAPLAC_TAIL_S: the last ~tail_s tile columns run serially on one stream
     int head_w = 0;       // GAPLAC_HEAD_W: width of the first super-panel (0 = spw)
+    int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
     int pair_m = 0;       // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
     int la_split_m = 0;   // GAPLAC_LA_SPLIT_M: split lookahead when <= this many tile rows follow SP p+1
     int persist_m = 0;    // GAPLAC_PERSIST_M: bulk updates of <= this many tile rows run on a capped
@@ -564,6 +565,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
                             W * mbd - W * (W - 1) / 2, kdp, jb, jb, ColMap{1, 0, W}};
                 ba.max_r = mbd - 1;
                 ba.max_c = W - 1;
+                ba.whole = mbd >= ctx->band_tiles_m ? 1 : 0;
                 launch_bulk(sm, ba, slot(ctx, 5, 0));
             } else if (je > jb) {
                 launch_col_update(sm, ctx->A, lda, pnl, nt, jb, jb, je - jb, kdp, slot(ctx, 5, 0));
@@ -1036,6 +1038,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_GRAM_QUEUE")) ctx->gram_queue = std::max(0, std::min(4, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_DIAG_FIRST_M")) ctx->diag_first_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_HEAD_W")) ctx->head_w = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_BAND_TILES_M")) ctx->band_tiles_m = std::max(1, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_PAIR_M")) ctx->pair_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_LA_SPLIT_M")) ctx->la_split_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_PERSIST_M")) ctx->persist_m = std::max(0, std::atoi(s));

@@ -1959,7 +1959,7 @@ void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt) {
     }
     if (!guard_launch("bulk update", a.C, 0, tiles_end(a.ldc, a.bi0 + max_r, a.lj0 + max_c))) return;
     int grid = ((a.ntiles + 7) >> 3) << 3;
-    if (syrk_is_small(a.ntiles)) {
+    if (syrk_is_small(a.ntiles) && !a.whole) {
         int qg = 4 * grid;
         if (a.persist > 0) qg = std::min(qg, std::max(32, a.persist & ~31));
         quad_bulk_kernel<<<dim3((unsigned)qg), dim3(256), 0, s>>>(a, kt);
