@@ -74,6 +74,7 @@ struct gaplac_ctx {
     int tail_w = 0;       //   super-panels are tail_w wide (plain logpdf only; 0 = off)
     int tail_s = 32;      // GAPLAC_TAIL_S: the last ~tail_s tile columns run serially on one stream
     int head_w = 0;       // GAPLAC_HEAD_W: width of the first super-panel (0 = spw)
+    int spare = 0;        // GAPLAC_SPARE: see bulk_tri
     int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
     int pair_m = 0;       // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
     int la_split_m = 0;   // GAPLAC_LA_SPLIT_M: split lookahead when <= this many tile rows follow SP p+1
@@ -479,6 +480,9 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         ba.yield = (m <= ctx->yield_m && sp != sm) ? 1 : 0;
         const bool small = syrk_is_small(ba.ntiles);
         if (m <= ctx->persist_m && sp != sm) ba.persist = (small ? ctx->persist_q : ctx->persist_t) * ctx->ncu;
+        // GAPLAC_SPARE: large launches on a capped grid of 2 x CUs - spare looping workgroups,
+        // so `spare` CUs hold one bulk workgroup and always have room for a chain workgroup
+        if (ctx->spare > 0 && sp != sm && !small && ba.ntiles > 2 * ctx->ncu) ba.persist = 2 * ctx->ncu - ctx->spare;
         KTime* kt = small ? slot(ctx, 6, 0) : slot(ctx, 0, syrk_flops(m) * (kdep / NB), syrk_bytes(m, kdep));
         const bool ev = ctx->prof_mode == 2 && !small;
         size_t e0 = 0;
@@ -1038,6 +1042,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_GRAM_QUEUE")) ctx->gram_queue = std::max(0, std::min(4, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_DIAG_FIRST_M")) ctx->diag_first_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_HEAD_W")) ctx->head_w = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_SPARE")) ctx->spare = std::max(0, std::min(255, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BAND_TILES_M")) ctx->band_tiles_m = std::max(1, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_PAIR_M")) ctx->pair_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_LA_SPLIT_M")) ctx->la_split_m = std::max(0, std::atoi(s));
