@@ -75,6 +75,7 @@ struct gaplac_ctx {
     int tail_s = 32;      // GAPLAC_TAIL_S: the last ~tail_s tile columns run serially on one stream
     int head_w = 0;       // GAPLAC_HEAD_W: width of the first super-panel (0 = spw)
     int spare = 0;        // GAPLAC_SPARE: see bulk_tri
+    int pair_ext = 0;     // GAPLAC_PAIR_EXT: 1 = a deferring step also updates the band after next
     int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
     int pair_m = 0;       // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
     int la_split_m = 0;   // GAPLAC_LA_SPLIT_M: split lookahead when <= this many tile rows follow SP p+1
@@ -502,7 +503,8 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         }
         return 0;
     };
-    int pend = -1;  // first super-panel not yet applied beyond the band (paired updates)
+    int pend = -1;  // the super-panel not yet applied to the columns >= dcol (paired updates)
+    int dcol = nt;
     for (int p = 0; p < nsp; ++p) {
         bool diag_first = false;
         const int c0 = spc[(size_t)p], c1 = spc[(size_t)p + 1];
@@ -553,32 +555,48 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             (nt - jb) * (nt - jb + 1) / 2 <= ctx->la_first)
             HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_L[p & 1], 0));
         // Paired bulk updates (GAPLAC_PAIR_M): at a deferring step only the next-needed band
-        // (SP p+2's columns) gets SP p, and the tile columns after it get SPs p and p+1 in
-        // one K = 2 x 128W update at step p+1 (band first, then R(p), then the rest).
+        // (SP p+2's columns; with GAPLAC_PAIR_EXT also SP p+3's) gets SP p, and the tile
+        // columns after it get SPs p and p+1 in one K = 2 x 128W update at step p+1 (band
+        // first, then R(p), then the rest). Columns >= dcol lack SP pend.
         const int je = p + 3 <= nsp ? spc[(size_t)p + 3] : spc[(size_t)nsp];
-        const int pc = pend >= 0 ? spc[(size_t)pend] : c0;  // first column of the pending SPs
-        const int kdp = (c1 - pc) * NB;
-        const Panel pnl{ctx->A + (int64_t)pc * NB * lda, lda, 0};
-        const bool defer = ctx->pair_m > 0 && pend < 0 && p + 1 < nsp && sp != sm && !ctx->xr_mode && je > jb &&
-                           nt - je >= ctx->pair_m;
-        if (pend >= 0 || defer) {
-            const int mbd = nt - jb;
-            if (je > jb && je - jb == W && ctx->band_off.size() > (size_t)mbd) {
-                // the band through the tile kernel (a list of its tiles; quadrants if small)
-                BulkArgs ba{ctx->A, lda, pnl, ctx->tiles + ctx->band_off[(size_t)mbd],
-                            W * mbd - W * (W - 1) / 2, kdp, jb, jb, ColMap{1, 0, W}};
+        const bool defer = ctx->pair_m > 0 && pend < 0 && sp != sm && !ctx->xr_mode && je > jb &&
+                           p + 1 + ctx->pair_ext < nsp && p + 3 + ctx->pair_ext <= nsp &&
+                           nt - spc[(size_t)p + 3 + ctx->pair_ext] >= ctx->pair_m;
+        // a band [b0, b1) with the panel columns pc .. c1-1
+        auto band = [&](int b0, int b1, int pc) {
+            if (b1 <= b0) return;
+            const Panel pn{ctx->A + (int64_t)pc * NB * lda, lda, 0};
+            const int kb = (c1 - pc) * NB, mbd = nt - b0;
+            if (b1 - b0 == W && ctx->band_off.size() > (size_t)mbd) {
+                // through the tile kernel (a list of the band's tiles; quadrants if small)
+                BulkArgs ba{ctx->A, lda, pn, ctx->tiles + ctx->band_off[(size_t)mbd], W * mbd - W * (W - 1) / 2, kb,
+                            b0, b0, ColMap{1, 0, W}};
                 ba.max_r = mbd - 1;
                 ba.max_c = W - 1;
                 ba.whole = mbd >= ctx->band_tiles_m ? 1 : 0;
                 launch_bulk(sm, ba, slot(ctx, 5, 0));
-            } else if (je > jb) {
-                launch_col_update(sm, ctx->A, lda, pnl, nt, jb, jb, je - jb, kdp, slot(ctx, 5, 0));
+            } else {
+                launch_col_update(sm, ctx->A, lda, pn, nt, b0, b0, b1 - b0, kb, slot(ctx, 5, 0));
             }
+        };
+        if (defer) {
+            band(jb, je, c0);
             HIPQ(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
-            if (!defer && (frc = bulk_tri(je, pnl, kdp))) return frc;
-            pend = defer ? p : -1;
+            dcol = je;
+            if (ctx->pair_ext > 0) {
+                dcol = spc[(size_t)p + 4];
+                band(je, dcol, c0);
+            }
+            pend = p;
+        } else if (pend >= 0) {
+            band(jb, je, je <= dcol ? c0 : spc[(size_t)pend]);
+            HIPQ(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
+            if (je < dcol) band(je, dcol, c0);  // (not produced by the schedule above)
+            const Panel pnl{ctx->A + (int64_t)spc[(size_t)pend] * NB * lda, lda, 0};
+            if ((frc = bulk_tri(std::max(je, dcol), pnl, (c1 - spc[(size_t)pend]) * NB))) return frc;
+            pend = -1;
         } else {
-            if ((frc = bulk_tri(jb, pnl, kd))) return frc;
+            if ((frc = bulk_tri(jb, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, kd))) return frc;
             HIPQ(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
         }
         if (ctx->xr_mode) {
@@ -1042,6 +1060,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_GRAM_QUEUE")) ctx->gram_queue = std::max(0, std::min(4, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_DIAG_FIRST_M")) ctx->diag_first_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_HEAD_W")) ctx->head_w = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_PAIR_EXT")) ctx->pair_ext = std::max(0, std::min(1, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_SPARE")) ctx->spare = std::max(0, std::min(255, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BAND_TILES_M")) ctx->band_tiles_m = std::max(1, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_PAIR_M")) ctx->pair_m = std::max(0, std::atoi(s));
