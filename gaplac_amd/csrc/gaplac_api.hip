@@ -74,10 +74,10 @@ struct gaplac_ctx {
     int tail_w = 0;       //   super-panels are tail_w wide (plain logpdf only; 0 = off)
     int tail_s = 32;      // GAPLAC_TAIL_S: the last ~tail_s tile columns run serially on one stream
     int head_w = 0;       // GAPLAC_HEAD_W: width of the first super-panel (0 = spw)
-    int spare = 0;        // GAPLAC_SPARE: see bulk_tri
-    int pair_ext = 0;     // GAPLAC_PAIR_EXT: 1 = a deferring step also updates the band after next
+    int spare = 32;       // GAPLAC_SPARE: see bulk_tri
+    int pair_ext = 1;     // GAPLAC_PAIR_EXT: 1 = a deferring step also updates the band after next
     int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
-    int pair_m = 0;       // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
+    int pair_m = 40;      // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
     int la_split_m = 0;   // GAPLAC_LA_SPLIT_M: split lookahead when <= this many tile rows follow SP p+1
     int persist_m = 0;    // GAPLAC_PERSIST_M: bulk updates of <= this many tile rows run on a capped
     int persist_t = 1;    //   grid, GAPLAC_PERSIST_T tile / GAPLAC_PERSIST_Q quadrant workgroups per
@@ -483,7 +483,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         if (m <= ctx->persist_m && sp != sm) ba.persist = (small ? ctx->persist_q : ctx->persist_t) * ctx->ncu;
         // GAPLAC_SPARE: large launches on a capped grid of 2 x CUs - spare looping workgroups,
         // so `spare` CUs hold one bulk workgroup and always have room for a chain workgroup
-        if (ctx->spare > 0 && sp != sm && !small && ba.ntiles > 2 * ctx->ncu) ba.persist = 2 * ctx->ncu - ctx->spare;
+        if (ctx->spare > 0 && sp != sm && !ctx->xr_mode && !small && ba.ntiles > 2 * ctx->ncu) ba.persist = 2 * ctx->ncu - ctx->spare;
         KTime* kt = small ? slot(ctx, 6, 0) : slot(ctx, 0, syrk_flops(m) * (kdep / NB), syrk_bytes(m, kdep));
         const bool ev = ctx->prof_mode == 2 && !small;
         size_t e0 = 0;

@@ -44,7 +44,8 @@ SCHEDULES = {
     "pair_all": {"GAPLAC_PAIR_M": "1"},
     "pair_band_whole_tiles": {"GAPLAC_PAIR_M": "1", "GAPLAC_BAND_TILES_M": "1"},
     "pair_spare": {"GAPLAC_PAIR_M": "1", "GAPLAC_SPARE": "200"},
-    "pair_ext": {"GAPLAC_PAIR_M": "1", "GAPLAC_PAIR_EXT": "1"},
+    "no_pair_no_spare": {"GAPLAC_PAIR_M": "0", "GAPLAC_SPARE": "0"},
+    "pair_no_ext": {"GAPLAC_PAIR_M": "1", "GAPLAC_PAIR_EXT": "0"},
     "pair_ext_spw3_whole": {"GAPLAC_PAIR_M": "1", "GAPLAC_PAIR_EXT": "1", "GAPLAC_SPW": "3", "GAPLAC_BAND_TILES_M": "1"},
     "pair_no_tail_split_persist": {"GAPLAC_PAIR_M": "1", "GAPLAC_TAIL_S": "0", "GAPLAC_LA_SPLIT_M": "1000",
                                    "GAPLAC_PERSIST_M": "1000"},
