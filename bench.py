@@ -90,8 +90,8 @@ def cpu_baseline(N: int, budget_s: float = 25.0):
 
 # PMC traffic of the dominant kernel (tools/profile_round.sh: FETCH_SIZE / WRITE_SIZE
 # passes over the same command, corrected per MI355X_MICROARCH.md; per launch).
-TRAFFIC_FILE = os.path.join("profiles", "r02b_traffic_syrk.json")
-TRAFFIC_FILE_CINV = os.path.join("profiles", "r02b_traffic_cinv.json")
+TRAFFIC_FILE = os.path.join("profiles", "r02d_traffic_syrk.json")
+TRAFFIC_FILE_CINV = os.path.join("profiles", "r02d_traffic_cinv.json")
 
 
 def load_traffic(name=TRAFFIC_FILE):
@@ -253,7 +253,7 @@ def main():
         traffic, traffic_src = load_traffic()
         roofline = {
             "bound": "mfma",
-            "kernel": "tile_syrk_kernel (bulk trailing update, 128x128 tiles, K=512, fp64 MFMA 16x16x4)",
+            "kernel": "tile_syrk_kernel (bulk trailing update, 128x128 tiles, K=512 or 1024 (paired), fp64 MFMA 16x16x4)",
             "achieved": round(achieved, 3),
             "peak": PEAK_F64_TFLOPS,
             "unit": "TFLOP/s",

@@ -78,7 +78,7 @@ struct BulkArgs {
     int max_r = -1, max_c = -1;  // largest lo16 / hi16 list entry (-1: an m x m triangle list)
     int yield = 0;  // step aside on CUs where panel-chain waves run
     int persist = 0;  // > 0: grid capped at this many workgroups, each looping over tiles
-    int whole = 0;    // 1: 128x128 tile workgroups even for a small list (no quadrant split)
+    int whole = 0;    // 1: a band list as 128x128 tile workgroups (tile_band_kernel), never quadrants
 };
 
 // Host-side footprint guard. Before launching, every launcher computes the

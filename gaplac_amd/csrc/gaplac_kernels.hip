@@ -1170,6 +1170,16 @@ __global__ __launch_bounds__(256, 2) void tile_syrk_kernel(BulkArgs a, KTime* __
     kt_end(kt);
 }
 
+// The same kernel under its own name for the band updates of the paired schedule (a short
+// list of a super-panel's tiles ahead of the bulk update), so that kernel traces keep the
+// bulk launches (tile_syrk_kernel, the roofline kernel) apart.
+__global__ __launch_bounds__(256, 2) void tile_band_kernel(BulkArgs a, KTime* __restrict__ kt) {
+    kt_begin(kt);
+    const int nb = ((a.ntiles + 7) >> 3) << 3;
+    for (int b = (int)blockIdx.x; b < nb; b += (int)gridDim.x) tile_syrk_body(a, b);
+    kt_end(kt);
+}
+
 // ---------------------------------------------------------------------------------
 // Quadrant update: C_q -= P_q Q_q^T for one 64x64 quadrant (qi, qj) of tile (bi, bj)
 // (stored in local tile column lj), K = kdepth panel columns. 4 waves as 2x2 of 32x32
@@ -1965,7 +1975,10 @@ void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt) {
         quad_bulk_kernel<<<dim3((unsigned)qg), dim3(256), 0, s>>>(a, kt);
     } else {
         if (a.persist > 0) grid = std::min(grid, std::max(8, a.persist & ~7));
-        tile_syrk_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
+        if (a.whole)
+            tile_band_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
+        else
+            tile_syrk_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
     }
 }
 
