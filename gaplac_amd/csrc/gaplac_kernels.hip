@@ -1038,11 +1038,14 @@ __device__ __forceinline__ void tile_decode(const BulkArgs& a, int idx, int& bi,
 // tile j) are column-major with leading dimension ldp. Lane element (mi, mj, rg) is tile
 // entry (row 64 wi + 16 mi + (lane & 15), column 64 wj + 16 mj + (lane >> 4) + 4 rg).
 // Inactive waves (upper quadrant of a diagonal tile) only help with the staging.
+template <bool OPQ = false>
 __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const double* __restrict__ Q,
                                              int64_t ldp, int kdepth, bool active, d4 (&acc)[4][4],
                                              bool yield = false) {
     __shared__ double sm[2][2][KB][LR];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int tid = threadIdx.x;
+    if constexpr (OPQ) asm volatile("" : "+v"(tid));  // opaque in a tile loop: no lane-dependent hoisting
+    const int lane = tid & 63, w = tid >> 6;
     const int wi = w & 1, wj = w >> 1;
     const int fr = lane >> 4, fc = lane & 15;
     // staging: thread -> (k row krow + 4 it, rows 2 lane, 2 lane + 1) of both operands
@@ -1119,6 +1122,7 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
 #undef GAPLAC_LSTORE
 }
 
+template <bool OPQ = false>
 __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
     const int chunk = (a.ntiles + 7) >> 3;
     const int idx = (b & 7) * chunk + (b >> 3);
@@ -1130,7 +1134,9 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
     double* __restrict__ Ct = a.C + (int64_t)lj * NB * ldc + r0;
     const double* __restrict__ P = a.pn.P + (r0 - a.pn.row0);
     const double* __restrict__ Q = a.pn.P + ((int64_t)bj * NB - a.pn.row0);
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int tid = threadIdx.x;
+    if constexpr (OPQ) asm volatile("" : "+v"(tid));  // opaque in a tile loop: no lane-dependent hoisting
+    const int lane = tid & 63, w = tid >> 6;
     const int wi = w & 1, wj = w >> 1;
     const bool active = !(bi == bj && wj > wi);
     const int fr = lane >> 4, fc = lane & 15;
@@ -1147,7 +1153,7 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
                     acc[mi][mj][rg] = Ci[(int64_t)(64 * wj + 16 * mj + fr + 4 * rg) * ldc];
         }
     }
-    tile_mma_neg(P, Q, a.pn.ld, a.kdepth, active, acc, a.yield != 0);
+    tile_mma_neg<OPQ>(P, Q, a.pn.ld, a.kdepth, active, acc, a.yield != 0);
     if (!active) return;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
@@ -1163,10 +1169,19 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
 // A capped grid (BulkArgs.persist, a multiple of 8) walks the virtual blocks with stride
 // gridDim.x, which keeps every block's XCD (b % 8) and leaves room on each CU for the
 // panel chain's workgroups.
+// One tile per workgroup (208 VGPRs: two resident bulk workgroups leave exactly the 96
+// registers a quadrant chain kernel needs) or, LOOP, a capped grid looping over the tiles
+// (the loop keeps more addresses live: 226 VGPRs; used for the large launches of the
+// spare-CU schedule, where one bulk workgroup + a diagonal block, 226 + 272, still fit).
+template <bool LOOP>
 __global__ __launch_bounds__(256, 2) void tile_syrk_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
-    const int nb = ((a.ntiles + 7) >> 3) << 3;
-    for (int b = (int)blockIdx.x; b < nb; b += (int)gridDim.x) tile_syrk_body(a, b);
+    if constexpr (LOOP) {
+        const int nb = ((a.ntiles + 7) >> 3) << 3;
+        for (int b = (int)blockIdx.x; b < nb; b += (int)gridDim.x) tile_syrk_body<true>(a, b);
+    } else {
+        tile_syrk_body(a, (int)blockIdx.x);
+    }
     kt_end(kt);
 }
 
@@ -1175,8 +1190,7 @@ __global__ __launch_bounds__(256, 2) void tile_syrk_kernel(BulkArgs a, KTime* __
 // bulk launches (tile_syrk_kernel, the roofline kernel) apart.
 __global__ __launch_bounds__(256, 2) void tile_band_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
-    const int nb = ((a.ntiles + 7) >> 3) << 3;
-    for (int b = (int)blockIdx.x; b < nb; b += (int)gridDim.x) tile_syrk_body(a, b);
+    tile_syrk_body(a, (int)blockIdx.x);
     kt_end(kt);
 }
 
@@ -1202,7 +1216,9 @@ constexpr int QUAD_BULK_MAX_TILES = 512;
 
 __device__ __forceinline__ void quad_update(double* __restrict__ C, int64_t ldc, const Panel& pn, int bi,
                                             int bj, int lj, int qi, int qj, int kdepth, bool yield = false) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));  // opaque: nothing lane-dependent is hoisted out of a tile loop
+    const int wave = tid >> 6, lane = tid & 63;
     const int wi = wave & 1, wj = wave >> 1;
     const int fr = lane >> 4, fc = lane & 15;
     const int64_t ri = (int64_t)bi * NB + 64 * qi + 32 * wi;   // this wave's 32 rows
@@ -1974,11 +1990,12 @@ void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt) {
         if (a.persist > 0) qg = std::min(qg, std::max(32, a.persist & ~31));
         quad_bulk_kernel<<<dim3((unsigned)qg), dim3(256), 0, s>>>(a, kt);
     } else {
-        if (a.persist > 0) grid = std::min(grid, std::max(8, a.persist & ~7));
         if (a.whole)
             tile_band_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
+        else if (a.persist > 0 && a.persist < grid)
+            tile_syrk_kernel<true><<<dim3((unsigned)std::max(8, a.persist & ~7)), dim3(256), 0, s>>>(a, kt);
         else
-            tile_syrk_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
+            tile_syrk_kernel<false><<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
     }
 }
 
