@@ -75,6 +75,7 @@ struct gaplac_ctx {
     int tail_s = 32;      // GAPLAC_TAIL_S: the last ~tail_s tile columns run serially on one stream
     int head_w = 0;       // GAPLAC_HEAD_W: width of the first super-panel (0 = spw)
     int spare = 0;        // GAPLAC_SPARE: see bulk_tri
+    bool pair_xr = false; // GAPLAC_PAIR_XR: paired updates also with extra rows (gradient / posterior)
     int pair_ext = 1;     // GAPLAC_PAIR_EXT: 1 = a deferring step also updates the band after next
     int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
     int pair_m = 40;      // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
@@ -559,7 +560,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         // columns after it get SPs p and p+1 in one K = 2 x 128W update at step p+1 (band
         // first, then R(p), then the rest). Columns >= dcol lack SP pend.
         const int je = p + 3 <= nsp ? spc[(size_t)p + 3] : spc[(size_t)nsp];
-        const bool defer = ctx->pair_m > 0 && pend < 0 && sp != sm && !ctx->xr_mode && je > jb &&
+        const bool defer = ctx->pair_m > 0 && pend < 0 && sp != sm && (!ctx->xr_mode || ctx->pair_xr) && je > jb &&
                            p + 1 + ctx->pair_ext < nsp && p + 3 + ctx->pair_ext <= nsp &&
                            nt - spc[(size_t)p + 3 + ctx->pair_ext] >= ctx->pair_m;
         // a band [b0, b1) with the panel columns pc .. c1-1
@@ -1060,6 +1061,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_GRAM_QUEUE")) ctx->gram_queue = std::max(0, std::min(4, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_DIAG_FIRST_M")) ctx->diag_first_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_HEAD_W")) ctx->head_w = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_PAIR_XR")) ctx->pair_xr = s[0] == '1';
     if (const char* s = std::getenv("GAPLAC_PAIR_EXT")) ctx->pair_ext = std::max(0, std::min(1, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_SPARE")) ctx->spare = std::max(0, std::min(255, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BAND_TILES_M")) ctx->band_tiles_m = std::max(1, std::atoi(s));
