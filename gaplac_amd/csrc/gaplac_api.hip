@@ -76,6 +76,7 @@ struct gaplac_ctx {
     int head_w = 0;       // GAPLAC_HEAD_W: width of the first super-panel (0 = spw)
     int spare = 0;        // GAPLAC_SPARE: see bulk_tri
     bool pair_xr = false; // GAPLAC_PAIR_XR: paired updates also with extra rows (gradient / posterior)
+    bool fine_tail = true;  // GAPLAC_FINE_TAIL: serial-tail updates on 32x32 workgroups (fine_bulk_kernel)
     int pair_ext = 1;     // GAPLAC_PAIR_EXT: 1 = a deferring step also updates the band after next
     int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
     int pair_m = 40;      // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
@@ -454,6 +455,7 @@ static void serial_tail(gaplac_ctx* ctx, hipStream_t sm, int64_t N, int64_t lda,
             const int m = nt - c;
             BulkArgs ba{ctx->A, lda, Panel{Acol - NB * lda, lda, 0}, ctx->tiles + ctx->tile_off[(size_t)m],
                         m * (m + 1) / 2, NB, c, c, ColMap{1, 0, ctx->spw}};
+            ba.fine = ctx->fine_tail ? 1 : 0;
             launch_bulk(sm, ba, slot(ctx, 6, 0));
         }
         double* Dk = ctx->Dinv + (size_t)c * DINV_PER_BLOCK;
@@ -1061,6 +1063,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_GRAM_QUEUE")) ctx->gram_queue = std::max(0, std::min(4, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_DIAG_FIRST_M")) ctx->diag_first_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_HEAD_W")) ctx->head_w = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_FINE_TAIL")) ctx->fine_tail = s[0] != '0';
     if (const char* s = std::getenv("GAPLAC_PAIR_XR")) ctx->pair_xr = s[0] == '1';
     if (const char* s = std::getenv("GAPLAC_PAIR_EXT")) ctx->pair_ext = std::max(0, std::min(1, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_SPARE")) ctx->spare = std::max(0, std::min(255, std::atoi(s)));

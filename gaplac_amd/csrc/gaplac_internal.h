@@ -79,6 +79,7 @@ struct BulkArgs {
     int yield = 0;  // step aside on CUs where panel-chain waves run
     int persist = 0;  // > 0: grid capped at this many workgroups, each looping over tiles
     int whole = 0;    // 1: a band list as 128x128 tile workgroups (tile_band_kernel), never quadrants
+    int fine = 0;     // 1 (K = 128 only): sixteen 32x32 workgroups per tile (fine_bulk_kernel)
 };
 
 // Host-side footprint guard. Before launching, every launcher computes the

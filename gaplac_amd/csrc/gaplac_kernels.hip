@@ -1303,6 +1303,48 @@ __global__ __launch_bounds__(256) void col_update_kernel(double* __restrict__ C,
     kt_end(kt);
 }
 
+// Latency-bound K = 128 updates of the serial tail: sixteen 32x32
+// workgroups per 128x128 tile, each wave one 16x16 block with a single accumulator. Every
+// panel fragment (32 k-steps x 2 operands) is loaded before the first MFMA, then the 32
+// MFMAs run back to back: the same per-element summation order as quad_update, so the
+// results are bitwise those of the quadrant kernel, in a fraction of its latency.
+__global__ __launch_bounds__(256) void fine_bulk_kernel(BulkArgs a, KTime* __restrict__ kt) {
+    kt_begin(kt);
+    const int t = (int)blockIdx.x >> 4, sub = (int)blockIdx.x & 15;
+    if (t < a.ntiles) {
+        int bi, bj, lj;
+        tile_decode(a, t, bi, bj, lj);
+        const int si = sub >> 2, sj = sub & 3;
+        if (!(bi == bj && sj > si)) {
+            const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+            const int wi = wave & 1, wj = wave >> 1;
+            const int fr = lane >> 4, fc = lane & 15;
+            const int64_t ri = (int64_t)bi * NB + 32 * si + 16 * wi;  // this wave's 16 rows
+            const int64_t cj = (int64_t)bj * NB + 32 * sj + 16 * wj;  // its 16 columns (global)
+            const int64_t cl = (int64_t)lj * NB + 32 * sj + 16 * wj;  // ... in storage
+            const int64_t ldp = a.pn.ld, ldc = a.ldc;
+            const double* P = a.pn.P + (ri - a.pn.row0) + fc;
+            const double* Q = a.pn.P + (cj - a.pn.row0) + fc;
+            double fa[NB / 4], fb[NB / 4];
+#pragma unroll
+            for (int s = 0; s < NB / 4; ++s) {
+                const int64_t col = (int64_t)(4 * s + fr) * ldp;
+                fb[s] = P[col];
+                fa[s] = Q[col];
+            }
+            d4 acc;
+#pragma unroll
+            for (int rg = 0; rg < 4; ++rg) acc[rg] = a.C[(cl + fr + 4 * rg) * ldc + ri + fc];
+            __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first MFMA
+#pragma unroll
+            for (int s = 0; s < NB / 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[s], -fb[s], acc, 0, 0, 0);
+#pragma unroll
+            for (int rg = 0; rg < 4; ++rg) a.C[(cl + fr + 4 * rg) * ldc + ri + fc] = acc[rg];
+        }
+    }
+    kt_end(kt);
+}
+
 // Small bulk trailing updates: the same tile list as tile_syrk_kernel, four quadrant
 // workgroups per tile (XCD-chunked like the tile kernel).
 __global__ __launch_bounds__(256) void quad_bulk_kernel(BulkArgs a, KTime* __restrict__ kt) {
@@ -1985,7 +2027,9 @@ void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt) {
     }
     if (!guard_launch("bulk update", a.C, 0, tiles_end(a.ldc, a.bi0 + max_r, a.lj0 + max_c))) return;
     int grid = ((a.ntiles + 7) >> 3) << 3;
-    if (syrk_is_small(a.ntiles) && !a.whole) {
+    if (a.fine && a.kdepth == NB) {
+        fine_bulk_kernel<<<dim3((unsigned)(16 * a.ntiles)), dim3(256), 0, s>>>(a, kt);
+    } else if (syrk_is_small(a.ntiles) && !a.whole) {
         int qg = 4 * grid;
         if (a.persist > 0) qg = std::min(qg, std::max(32, a.persist & ~31));
         quad_bulk_kernel<<<dim3((unsigned)qg), dim3(256), 0, s>>>(a, kt);
