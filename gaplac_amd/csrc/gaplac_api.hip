@@ -76,7 +76,7 @@ struct gaplac_ctx {
     int head_w = 0;       // GAPLAC_HEAD_W: width of the first super-panel (0 = spw)
     int spare = 0;        // GAPLAC_SPARE: see bulk_tri
     bool pair_xr = false; // GAPLAC_PAIR_XR: paired updates also with extra rows (gradient / posterior)
-    bool fine_tail = true;  // GAPLAC_FINE_TAIL: serial-tail updates on 32x32 workgroups (fine_bulk_kernel)
+    bool fine_tail = false; // GAPLAC_FINE_TAIL: serial-tail updates on 32x32 workgroups (fine_bulk_kernel)
     int pair_ext = 1;     // GAPLAC_PAIR_EXT: 1 = a deferring step also updates the band after next
     int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
     int pair_m = 40;      // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band

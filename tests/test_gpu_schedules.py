@@ -12,8 +12,8 @@ these sizes) and agree with the default schedule.
   stream (1000: every step);
 * GAPLAC_PAIR_M: paired bulk updates (every other step the columns beyond the next band
   receive two super-panels at once; 1: whenever possible);
-* GAPLAC_FINE_TAIL=0: the serial tail's K = 128 updates on quadrant workgroups instead of
-  the 32x32 fine_bulk_kernel (same per-element summation order: bitwise equal);
+* GAPLAC_FINE_TAIL=1: the serial tail's K = 128 updates on the 32x32 fine_bulk_kernel instead of
+  quadrant workgroups (same per-element summation order: bitwise equal);
 * GAPLAC_PERSIST_M / _T / _Q: bulk updates on a capped grid whose workgroups loop over
   the tiles (1000 applies it to every step; N = 9000 runs the 128x128 tile kernel so).
 The settings are read when a context is created (gaplac_ctx_create).
@@ -47,7 +47,7 @@ SCHEDULES = {
     "pair_band_whole_tiles": {"GAPLAC_PAIR_M": "1", "GAPLAC_BAND_TILES_M": "1"},
     "pair_spare": {"GAPLAC_PAIR_M": "1", "GAPLAC_SPARE": "200"},
     "no_pair_no_spare": {"GAPLAC_PAIR_M": "0", "GAPLAC_SPARE": "0"},
-    "no_fine_tail": {"GAPLAC_FINE_TAIL": "0"},
+    "fine_tail": {"GAPLAC_FINE_TAIL": "1"},
     "pair_no_ext": {"GAPLAC_PAIR_M": "1", "GAPLAC_PAIR_EXT": "0"},
     "pair_ext_spw3_whole": {"GAPLAC_PAIR_M": "1", "GAPLAC_PAIR_EXT": "1", "GAPLAC_SPW": "3", "GAPLAC_BAND_TILES_M": "1"},
     "pair_no_tail_split_persist": {"GAPLAC_PAIR_M": "1", "GAPLAC_TAIL_S": "0", "GAPLAC_LA_SPLIT_M": "1000",
@@ -118,5 +118,5 @@ def test_serial_tail_reports_posdef_failure(ctxs):
 def test_fine_tail_bitwise_equal_to_quadrant_tail(ctxs, N):
     X, v = inputs(N)
     a = ctxs["default"].logpdf(X, TERMS, 0.1, v, full=True)
-    b = ctxs["no_fine_tail"].logpdf(X, TERMS, 0.1, v, full=True)
+    b = ctxs["fine_tail"].logpdf(X, TERMS, 0.1, v, full=True)
     assert a == b
