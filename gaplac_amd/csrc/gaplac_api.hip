@@ -46,6 +46,7 @@ struct gaplac_ctx {
     // band lists (paired updates): tile columns 0 .. spw-1 of an m-row trailing matrix, rows
     // r >= c, rows outer; packed after the triangle lists, band_off[m] into tiles
     std::vector<size_t> band_off;
+    std::vector<uint32_t> tiles_host;  // host copy of the packed lists
     double* dX = nullptr;
     size_t dX_elems = 0;
     double* dv = nullptr;
@@ -76,6 +77,7 @@ struct gaplac_ctx {
     int head_w = 0;       // GAPLAC_HEAD_W: width of the first super-panel (0 = spw)
     int spare = 0;        // GAPLAC_SPARE: see bulk_tri
     bool pair_xr = false; // GAPLAC_PAIR_XR: paired updates also with extra rows (gradient / posterior)
+    int quad_tail = 0;    // GAPLAC_QUAD_TAIL: see bulk_tri (percent of a round; 0 = off)
     bool fine_tail = false; // GAPLAC_FINE_TAIL: serial-tail updates on 32x32 workgroups (fine_bulk_kernel)
     int pair_ext = 1;     // GAPLAC_PAIR_EXT: 1 = a deferring step also updates the band after next
     int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
@@ -487,7 +489,25 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         // GAPLAC_SPARE: large launches on a capped grid of 2 x CUs - spare looping workgroups,
         // so `spare` CUs hold one bulk workgroup and always have room for a chain workgroup
         if (ctx->spare > 0 && sp != sm && !ctx->xr_mode && !small && ba.ntiles > 2 * ctx->ncu) ba.persist = 2 * ctx->ncu - ctx->spare;
-        KTime* kt = small ? slot(ctx, 6, 0) : slot(ctx, 0, syrk_flops(m) * (kdep / NB), syrk_bytes(m, kdep));
+        // GAPLAC_QUAD_TAIL=pct: when the last round of 2 x CUs tiles would be less than pct %
+        // full, those tiles run as quadrant workgroups (4 per tile) in a second launch
+        int full = ba.ntiles;
+        if (ctx->quad_tail > 0 && !small && ba.persist == 0 && !ctx->tiles_host.empty()) {
+            const int slots = 2 * ctx->ncu, rem = ba.ntiles % slots;
+            if (rem > 0 && rem * 100 < slots * ctx->quad_tail) full = ba.ntiles - rem;
+        }
+        double fl = syrk_flops(m) * (kdep / NB), by = syrk_bytes(m, kdep);
+        if (full < ba.ntiles) {  // exact flops of the list's first `full` tiles
+            const uint32_t* L = ctx->tiles_host.data() + ctx->tile_off[(size_t)m];
+            int d = 0;
+            for (int i = 0; i < full; ++i) d += (L[i] & 0xffffu) == (L[i] >> 16);
+            fl = ((double)(full - d) * 2.0 * NB * NB * NB + (double)d * NB * NB * (NB + 1)) * (kdep / NB);
+            by = by * full / ba.ntiles;
+            ba.max_r = ba.max_c = m - 1;
+        }
+        BulkArgs bt = ba;
+        bt.ntiles = full;
+        KTime* kt = small ? slot(ctx, 6, 0) : slot(ctx, 0, fl, by);
         const bool ev = ctx->prof_mode == 2 && !small;
         size_t e0 = 0;
         if (ev) {
@@ -499,10 +519,16 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             }
             HIPQ(ctx, hipEventRecord(ctx->evpool[e0], sm));
         }
-        launch_bulk(sm, ba, kt);
+        launch_bulk(sm, bt, kt);
         if (ev) {
             HIPQ(ctx, hipEventRecord(ctx->evpool[e0 + 1], sm));
-            ctx->evpairs.push_back({e0, syrk_flops(m) * (kdep / NB), syrk_bytes(m, kdep), 0});
+            ctx->evpairs.push_back({e0, fl, by, 0});
+        }
+        if (full < ba.ntiles) {
+            BulkArgs bq = ba;
+            bq.tiles = ba.tiles + full;
+            bq.ntiles = ba.ntiles - full;
+            launch_bulk(sm, bq, slot(ctx, 6, 0));
         }
         return 0;
     };
@@ -644,6 +670,7 @@ int ensure_tile_lists(gaplac_ctx* ctx, int nt) {
     int rc;
     if ((rc = ensure(ctx, &ctx->tiles, &ctx->tiles_elems, total))) return rc;
     HIPCK(ctx, hipMemcpy(ctx->tiles, host.data(), total * sizeof(uint32_t), hipMemcpyHostToDevice));
+    ctx->tiles_host = host;
     ctx->tile_off = off;
     ctx->tiles_nt = nt;
     return 0;
@@ -1063,6 +1090,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_GRAM_QUEUE")) ctx->gram_queue = std::max(0, std::min(4, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_DIAG_FIRST_M")) ctx->diag_first_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_HEAD_W")) ctx->head_w = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_QUAD_TAIL")) ctx->quad_tail = std::max(0, std::min(100, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_FINE_TAIL")) ctx->fine_tail = s[0] != '0';
     if (const char* s = std::getenv("GAPLAC_PAIR_XR")) ctx->pair_xr = s[0] == '1';
     if (const char* s = std::getenv("GAPLAC_PAIR_EXT")) ctx->pair_ext = std::max(0, std::min(1, std::atoi(s)));

@@ -14,6 +14,7 @@ these sizes) and agree with the default schedule.
   receive two super-panels at once; 1: whenever possible);
 * GAPLAC_FINE_TAIL=1: the serial tail's K = 128 updates on the 32x32 fine_bulk_kernel instead of
   quadrant workgroups (same per-element summation order: bitwise equal);
+* GAPLAC_QUAD_TAIL: a bulk launch's partial last round as quadrant workgroups;
 * GAPLAC_PERSIST_M / _T / _Q: bulk updates on a capped grid whose workgroups loop over
   the tiles (1000 applies it to every step; N = 9000 runs the 128x128 tile kernel so).
 The settings are read when a context is created (gaplac_ctx_create).
@@ -48,6 +49,7 @@ SCHEDULES = {
     "pair_spare": {"GAPLAC_PAIR_M": "1", "GAPLAC_SPARE": "200"},
     "no_pair_no_spare": {"GAPLAC_PAIR_M": "0", "GAPLAC_SPARE": "0"},
     "fine_tail": {"GAPLAC_FINE_TAIL": "1"},
+    "quad_tail_all": {"GAPLAC_QUAD_TAIL": "100"},
     "pair_no_ext": {"GAPLAC_PAIR_M": "1", "GAPLAC_PAIR_EXT": "0"},
     "pair_ext_spw3_whole": {"GAPLAC_PAIR_M": "1", "GAPLAC_PAIR_EXT": "1", "GAPLAC_SPW": "3", "GAPLAC_BAND_TILES_M": "1"},
     "pair_no_tail_split_persist": {"GAPLAC_PAIR_M": "1", "GAPLAC_TAIL_S": "0", "GAPLAC_LA_SPLIT_M": "1000",
