@@ -1545,6 +1545,16 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
     c.tile_off.assign((size_t)nt + 1, 0);
     for (int m = 1; m <= nt; ++m) c.tile_off[(size_t)m] = c.tile_off[(size_t)m - 1] + (size_t)(m - 1) * m / 2;
     c.tiles_nt = nt;
+    // band list offsets as ensure_tile_lists lays them out (the walk launches the same bands)
+    c.band_off.assign((size_t)nt + 1, 0);
+    {
+        size_t k = c.tile_off[(size_t)nt] + (size_t)nt * (nt + 1) / 2;
+        for (int m = 1; m <= nt; ++m) {
+            c.band_off[(size_t)m] = k;
+            const size_t w = (size_t)std::min(c.spw, m);
+            k += w * m - w * (w - 1) / 2;
+        }
+    }
     if (mode == 1) {
         std::vector<uint32_t> gl;
         build_grad_list((int)((N + NB - 1) / NB), gl);
