@@ -77,6 +77,7 @@ struct gaplac_ctx {
     int head_w = 0;       // GAPLAC_HEAD_W: width of the first super-panel (0 = spw)
     int spare = 0;        // GAPLAC_SPARE: see bulk_tri
     bool pair_xr = false; // GAPLAC_PAIR_XR: paired updates also with extra rows (gradient / posterior)
+    bool fused_tail = false;  // GAPLAC_FUSED_TAIL: serial tail's diagonal block + TRSM in one launch
     int quad_tail = 0;    // GAPLAC_QUAD_TAIL: see bulk_tri (percent of a round; 0 = off)
     bool fine_tail = false; // GAPLAC_FINE_TAIL: serial-tail updates on 32x32 workgroups (fine_bulk_kernel)
     int pair_ext = 1;     // GAPLAC_PAIR_EXT: 1 = a deferring step also updates the band after next
@@ -461,6 +462,10 @@ static void serial_tail(gaplac_ctx* ctx, hipStream_t sm, int64_t N, int64_t lda,
             launch_bulk(sm, ba, slot(ctx, 6, 0));
         }
         double* Dk = ctx->Dinv + (size_t)c * DINV_PER_BLOCK;
+        if (ctx->fused_tail) {
+            launch_diag_trsm(sm, Acol, lda, N, nt, c, Dk, ctx->dres, slot(ctx, 2, 0));
+            continue;
+        }
         if ((int64_t)c * NB < N)
             launch_potrf_diag(sm, Acol + (int64_t)c * NB, lda, N, (int64_t)c * NB, Dk, ctx->dres, slot(ctx, 2, 0));
         launch_trsm(sm, Acol, lda, nt, c, Dk, slot(ctx, 4, 0));
@@ -1090,6 +1095,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_GRAM_QUEUE")) ctx->gram_queue = std::max(0, std::min(4, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_DIAG_FIRST_M")) ctx->diag_first_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_HEAD_W")) ctx->head_w = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_FUSED_TAIL")) ctx->fused_tail = s[0] == '1';
     if (const char* s = std::getenv("GAPLAC_QUAD_TAIL")) ctx->quad_tail = std::max(0, std::min(100, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_FINE_TAIL")) ctx->fine_tail = s[0] != '0';
     if (const char* s = std::getenv("GAPLAC_PAIR_XR")) ctx->pair_xr = s[0] == '1';

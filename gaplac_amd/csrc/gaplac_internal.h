@@ -35,6 +35,7 @@ struct EvalResult {
     unsigned long long info;  // min over failing pivots of (j+1); ULLONG_MAX = none
     double part[2][REDUCE_BLOCKS];  // per-workgroup partial sums of the reduction
     unsigned gram_ticket;           // work queue of the second Gram launch (zeroed per eval)
+    unsigned diag_done;             // fused serial tail: last tile column whose L_kk is final, + 1
 };
 
 // Per-launch device timestamps (profiling): 100 MHz s_memrealtime ticks.
@@ -136,6 +137,9 @@ void launch_potrf_diag(hipStream_t s, double* Ablk, int64_t lda, int64_t N, int6
 // TRSM of the panel rows below diagonal block k: Acol is the storage of global column
 // k*NB; rows bi*NB.. for bi = k+1..nt-1 become A[bi,k] L_kk^{-T}.
 void launch_trsm(hipStream_t s, double* Acol, int64_t lda, int nt, int k, const double* Dinv, KTime* kt);
+// Diagonal block k and the TRSM of the tiles below it in one launch (serial tail only).
+void launch_diag_trsm(hipStream_t s, double* Acol, int64_t lda, int64_t N, int nt, int k, double* Dinv,
+                      EvalResult* res, KTime* kt);
 // Same substitution for an arbitrary run of row tiles bi0 .. bi0+nrows-1 of column k
 // (the gradient's identity rows below the matrix).
 void launch_trsm_rows(hipStream_t s, double* Acol, int64_t lda, int k, int bi0, int nrows, const double* Dinv,

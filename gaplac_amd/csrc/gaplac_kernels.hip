@@ -857,16 +857,16 @@ constexpr int TRSM_LBLK = NDB * (NDB - 1) / 2;  // 28
 
 // Acol: storage of the panel's first column (global column k*NB), rows global.
 __device__ __forceinline__ void trsm_subst_kernel_body(double* __restrict__ Acol, int64_t lda, int k, int bi0,
-                                                         const double* __restrict__ Dinv) {
+                                                         const double* __restrict__ Dinv, int vb) {
     __shared__ double Ls[(TRSM_LBLK + NDB) * 256];
     __builtin_amdgcn_s_setprio(2);  // critical path
     const int tid = threadIdx.x;
-    const int bi = bi0 + (int)(blockIdx.x >> 1);
+    const int bi = bi0 + (int)(vb >> 1);
     const int wave = tid >> 6, lane = tid & 63;
     const int fr = lane >> 4, fc = lane & 15;
     const int64_t k0 = (int64_t)k * NB;
     const double* L = Acol + k0;  // L_kk, column-major, lda
-    double* B = Acol + (int64_t)bi * NB + 64 * (blockIdx.x & 1) + 16 * wave;
+    double* B = Acol + (int64_t)bi * NB + 64 * (vb & 1) + 16 * wave;
     {
         // block (b, c), c < b, at p = b(b-1)/2 + c: Ls[p*256 + m*16 + j] = L(16b + j, 16c + m)
         const double* Lt = L + (int64_t)(tid >> 4) * lda + (tid & 15);
@@ -926,8 +926,42 @@ __global__ __launch_bounds__(256) void trsm_subst_kernel(
                                                          KTime* __restrict__ kt) {
     kt_begin(kt);
     if (GAPLAC_YIELD & 2) chain_enter();
-    trsm_subst_kernel_body(Acol, lda, k, bi0, Dinv);
+    trsm_subst_kernel_body(Acol, lda, k, bi0, Dinv, (int)blockIdx.x);
     if (GAPLAC_YIELD & 2) chain_leave();
+    kt_end(kt);
+}
+
+// Serial tail (GAPLAC_FUSED_TAIL): diagonal block k (workgroup 0) and the TRSM of the
+// tiles below it (workgroups 1 .. 2n) in one launch. Workgroup 0 is dispatched first and
+// waits on nothing; when L_kk and its 16x16 inverses are stored it publishes k + 1 in
+// EvalResult::diag_done (zeroed per evaluation) with release semantics, and the TRSM
+// workgroups, resident meanwhile, start the substitution as soon as they observe it. The
+// wait is bounded (100 ms of the 100 MHz clock), so a lost update cannot hang the GPU.
+// Only for the serial tail, where nothing else runs beside the chain: waiting workgroups
+// hold their CU slots. Same arithmetic as the two kernels: bitwise equal results.
+__global__ __launch_bounds__(256) void diag_trsm_kernel(double* __restrict__ Acol, int64_t lda, int64_t N, int k,
+                                                        double* __restrict__ Dinv, EvalResult* __restrict__ res,
+                                                        KTime* __restrict__ kt) {
+    kt_begin(kt);
+    const int64_t g0 = (int64_t)k * NB;
+    if (blockIdx.x == 0) {
+        if (g0 < N) potrf_diag_kernel_body(Acol + g0, lda, N, g0, Dinv, res);
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(&res->diag_done, (unsigned)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        if (threadIdx.x == 0) {
+            const unsigned long long t0 = wall_clock64();
+            while (__hip_atomic_load(&res->diag_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(k + 1)) {
+                __builtin_amdgcn_s_sleep(2);
+                if (wall_clock64() - t0 > 10000000ull) break;
+            }
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        trsm_subst_kernel_body(Acol, lda, k, k + 1, Dinv, (int)blockIdx.x - 1);
+    }
     kt_end(kt);
 }
 
@@ -1445,6 +1479,7 @@ __global__ void init_result_kernel(EvalResult* res) {
     res->quad = 0.0;
     res->info = ~0ull;
     res->gram_ticket = 0u;
+    res->diag_done = 0u;
 }
 
 // ---------------------------------------------------------------------------------
@@ -1991,6 +2026,13 @@ void launch_trsm(hipStream_t s, double* Acol, int64_t lda, int nt, int k, const 
         trsm_lite_kernel<<<dim3(8 * n), dim3(64), 0, s>>>(Acol, lda, k, k + 1, Dinv, kt);
     else
         trsm_subst_kernel<<<dim3(2 * n), dim3(256), 0, s>>>(Acol, lda, k, k + 1, Dinv, kt);
+}
+
+void launch_diag_trsm(hipStream_t s, double* Acol, int64_t lda, int64_t N, int nt, int k, double* Dinv,
+                      EvalResult* res, KTime* kt) {
+    const int n = nt - k - 1;
+    if (!guard_launch("diag_trsm_kernel", Acol, 0, tiles_end(lda, nt - 1, 0))) return;
+    diag_trsm_kernel<<<dim3(1 + 2 * std::max(n, 0)), dim3(256), 0, s>>>(Acol, lda, N, k, Dinv, res, kt);
 }
 
 void launch_trsm_rows(hipStream_t s, double* Acol, int64_t lda, int k, int bi0, int nrows, const double* Dinv,

@@ -15,6 +15,8 @@ these sizes) and agree with the default schedule.
 * GAPLAC_FINE_TAIL=1: the serial tail's K = 128 updates on the 32x32 fine_bulk_kernel instead of
   quadrant workgroups (same per-element summation order: bitwise equal);
 * GAPLAC_QUAD_TAIL: a bulk launch's partial last round as quadrant workgroups;
+* GAPLAC_FUSED_TAIL: the serial tail's diagonal block and TRSM in one launch (the TRSM
+  workgroups wait on a flag the diagonal workgroup publishes; bitwise equal);
 * GAPLAC_PERSIST_M / _T / _Q: bulk updates on a capped grid whose workgroups loop over
   the tiles (1000 applies it to every step; N = 9000 runs the 128x128 tile kernel so).
 The settings are read when a context is created (gaplac_ctx_create).
@@ -50,6 +52,8 @@ SCHEDULES = {
     "no_pair_no_spare": {"GAPLAC_PAIR_M": "0", "GAPLAC_SPARE": "0"},
     "fine_tail": {"GAPLAC_FINE_TAIL": "1"},
     "quad_tail_all": {"GAPLAC_QUAD_TAIL": "100"},
+    "fused_tail": {"GAPLAC_FUSED_TAIL": "1"},
+    "fused_everything_serial": {"GAPLAC_FUSED_TAIL": "1", "GAPLAC_TAIL_S": "1000"},
     "pair_no_ext": {"GAPLAC_PAIR_M": "1", "GAPLAC_PAIR_EXT": "0"},
     "pair_ext_spw3_whole": {"GAPLAC_PAIR_M": "1", "GAPLAC_PAIR_EXT": "1", "GAPLAC_SPW": "3", "GAPLAC_BAND_TILES_M": "1"},
     "pair_no_tail_split_persist": {"GAPLAC_PAIR_M": "1", "GAPLAC_TAIL_S": "0", "GAPLAC_LA_SPLIT_M": "1000",
@@ -122,3 +126,11 @@ def test_fine_tail_bitwise_equal_to_quadrant_tail(ctxs, N):
     a = ctxs["default"].logpdf(X, TERMS, 0.1, v, full=True)
     b = ctxs["fine_tail"].logpdf(X, TERMS, 0.1, v, full=True)
     assert a == b
+
+
+@pytest.mark.parametrize("N", [1, 129, 700, 3000, 9000])
+def test_fused_tail_bitwise_equal(ctxs, N):
+    X, v = inputs(N)
+    a = ctxs["default"].logpdf(X, TERMS, 0.1, v, full=True)
+    for name in ("fused_tail", "fused_everything_serial"):
+        assert ctxs[name].logpdf(X, TERMS, 0.1, v, full=True) == a, name
