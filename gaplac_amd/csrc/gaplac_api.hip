@@ -675,7 +675,7 @@ int ensure_tile_lists(gaplac_ctx* ctx, int nt) {
     int rc;
     if ((rc = ensure(ctx, &ctx->tiles, &ctx->tiles_elems, total))) return rc;
     HIPCK(ctx, hipMemcpy(ctx->tiles, host.data(), total * sizeof(uint32_t), hipMemcpyHostToDevice));
-    ctx->tiles_host = host;
+    if (ctx->quad_tail > 0) ctx->tiles_host = host;  // only GAPLAC_QUAD_TAIL reads it (~90 MB at N=65536)
     ctx->tile_off = off;
     ctx->tiles_nt = nt;
     return 0;
