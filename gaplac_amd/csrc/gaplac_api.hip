@@ -27,12 +27,7 @@ struct gaplac_ctx {
     hipStream_t s_main = nullptr, s_panel = nullptr;
     hipStream_t s_extra = nullptr;  // extra rows (gradient / posterior), beside the bulk updates
     hipEvent_t ev_xinit = nullptr, ev_xdone = nullptr;
-    int diag_cus = 0;  // CUs masked out of s_main for the diagonal kernel (0: no mask)
-    hipEvent_t ev_P[2] = {}, ev_R[2] = {}, ev_L[2] = {}, ev_D[2] = {}, ev_S[2] = {}, ev_gram = nullptr, ev_gram2 = nullptr;
-    // bulk updates of at most this many tiles wait for the step's lookahead column update
-    // (GAPLAC_LA_FIRST): late in the factorisation the panel chain is the critical path
-    int la_first = 0;
-    int yield_m = 0;  // bulk updates of trailing matrices of <= yield_m tile rows yield to the chain
+    hipEvent_t ev_P[2] = {}, ev_R[2] = {}, ev_gram = nullptr, ev_gram2 = nullptr;
     double* A = nullptr;
     size_t A_elems = 0;
     double* Dinv = nullptr;  // per diagonal block: 8 inverses of its 16x16 sub-blocks
@@ -46,7 +41,6 @@ struct gaplac_ctx {
     // band lists (paired updates): tile columns 0 .. spw-1 of an m-row trailing matrix, rows
     // r >= c, rows outer; packed after the triangle lists, band_off[m] into tiles
     std::vector<size_t> band_off;
-    std::vector<uint32_t> tiles_host;  // host copy of the packed lists
     double* dX = nullptr;
     size_t dX_elems = 0;
     double* dv = nullptr;
@@ -68,28 +62,16 @@ struct gaplac_ctx {
         int kind;  // 0 bulk tile_syrk launch, 8 cinv_tile launch
     };
     std::vector<EvPair> evpairs;
+    // Schedule switches, read once in gaplac_ctx_create; the defaults are
+    // the measured best at N = 16384.
     bool serial = false;  // GAPLAC_SERIAL=1: one stream, no overlap (per-kernel timing)
     bool dry = false;     // host-only walk of the schedule (gaplac_plan_check): no HIP calls
     int spw = 4;          // GAPLAC_SPW: super-panel width in 128-column tiles (bulk K = 128 spw)
-    int tail_m = 0;       // GAPLAC_TAIL_M / GAPLAC_TAIL_W: once at most tail_m tile columns remain,
-    int tail_w = 0;       //   super-panels are tail_w wide (plain logpdf only; 0 = off)
     int tail_s = 32;      // GAPLAC_TAIL_S: the last ~tail_s tile columns run serially on one stream
-    int head_w = 0;       // GAPLAC_HEAD_W: width of the first super-panel (0 = spw)
-    int spare = 0;        // GAPLAC_SPARE: see bulk_tri
-    bool pair_xr = false; // GAPLAC_PAIR_XR: paired updates also with extra rows (gradient / posterior)
-    bool fused_tail = false;  // GAPLAC_FUSED_TAIL: serial tail's diagonal block + TRSM in one launch
-    int quad_tail = 0;    // GAPLAC_QUAD_TAIL: see bulk_tri (percent of a round; 0 = off)
-    bool fine_tail = false; // GAPLAC_FINE_TAIL: serial-tail updates on 32x32 workgroups (fine_bulk_kernel)
     int pair_ext = 1;     // GAPLAC_PAIR_EXT: 1 = a deferring step also updates the band after next
     int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
     int pair_m = 40;      // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
-    int la_split_m = 0;   // GAPLAC_LA_SPLIT_M: split lookahead when <= this many tile rows follow SP p+1
-    int persist_m = 0;    // GAPLAC_PERSIST_M: bulk updates of <= this many tile rows run on a capped
-    int persist_t = 1;    //   grid, GAPLAC_PERSIST_T tile / GAPLAC_PERSIST_Q quadrant workgroups per
-    int persist_q = 1;    //   CU, so the panel chain's workgroups always find room (0 = off)
     int ncu = 256;        // compute units of the device
-    int diag_first_m = 0; // GAPLAC_DIAG_FIRST_M: bulk updates of <= this many tile rows wait for the
-                          //   next super-panel's first diagonal block + TRSM
     int gram_queue = 2;   // GAPLAC_GRAM_QUEUE: second Gram launch as a work queue of this many
                           //   workgroups per CU, leaving room for the panel chain (0 = plain grid)
     gaplac_stats stats{};
@@ -98,23 +80,11 @@ struct gaplac_ctx {
         double work;
         double bytes;  // kind 0: algorithmic HBM bytes
     };
-    std::vector<Slot> slots;     // slots of the launches being enqueued / of the profiled graph
+    std::vector<Slot> slots;     // slots of the launches being enqueued
     KTime* dkt = nullptr;        // device slot array
     KTime* hkt = nullptr;        // pinned copy
     size_t kt_cap = 0;
     bool recording = false;      // assign slots while enqueuing
-    // Captured schedule of one evaluation (hipGraph), replayed while N and the workspace
-    // pointers stay the same: removes the per-launch and cross-stream event-hop costs
-    // (2.9 us per dependent launch, ~12 us per event hop eager vs ~1.6 us in a graph).
-    // The profiled variant is the same schedule with KTime slots wired in.
-    bool use_graph = false;  // GAPLAC_GRAPH=1: capture/replay (loses stream priorities)
-    bool graph_prio = false;  // instantiate with per-node (capture-stream) priorities
-    hipGraph_t graph = nullptr, pgraph = nullptr;
-    hipGraphExec_t gexec = nullptr, pgexec = nullptr;
-    int64_t gN = -1, pgN = -1;
-    const void* gptrs[6] = {};
-    const void* pgptrs[6] = {};
-    std::vector<Slot> pslots;
     // Batched select: models in flight on independent lanes (child contexts with their
     // own workspace and streams; they read the parent's uploaded X and v).
     std::vector<gaplac_ctx*> lanes;
@@ -360,11 +330,10 @@ int accumulate_slots(gaplac_ctx* ctx, const std::vector<gaplac_ctx::Slot>& slots
 // ~10 us fixed (C load, first staging, epilogue) + K at the MFMA ceiling, so larger K
 // amortises the fixed part (and cuts C-tile HBM traffic per flop by W).
 //
-// Two streams, eager launches (GAPLAC_GRAPH=1 captures and replays instead). s_panel
-// (highest priority, all CUs) runs the critical path in order; s_main (lowest priority;
-// optionally CU-masked, GAPLAC_DIAG_CUS, off by default) runs the Gram and the bulk
-// updates. Super-panel boundaries come from superpanel_starts() (width spw; the last
-// ~tail_s tile columns are factored by serial_tail() on s_main alone).
+// Two streams, eager launches. s_panel (highest priority, all CUs) runs the critical path
+// in order; s_main (lowest priority) runs the Gram and the bulk updates. Super-panel
+// boundaries come from superpanel_starts() (width spw; the last ~tail_s tile columns are
+// factored by serial_tail() on s_main alone).
 //   s_panel: wait R(p-1) | col_update(columns of SP p+1, with SP p, K=128W)
 //            | for each column c of SP p+1: [col_update(c with c-1..first, K=128)] potrf(c) trsm(c)
 //            | rec P(p+1)
@@ -373,13 +342,8 @@ int accumulate_slots(gaplac_ctx* ctx, const std::vector<gaplac_ctx::Slot>& slots
 // the previous columns of its own super-panel). Columns of SP p+1 receive SP p-1 in
 // R(p-1) and SP p in the lookahead col_update; within a step the streams touch disjoint
 // tile columns. Events ping-pong (p & 1).
-// after_first: recorded once the first column's diagonal block and TRSM are enqueued.
-// Columns cs .. ce-1 of the super-panel c0 .. c1-1 (default: all of them).
-int factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, int nt, int c0, int c1,
-                      hipEvent_t after_first = nullptr, int cs = -1, int ce = -1) {
-    if (cs < 0) cs = c0;
-    if (ce < 0) ce = c1;
-    for (int c = cs; c < ce; ++c) {
+int factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, int nt, int c0, int c1) {
+    for (int c = c0; c < c1; ++c) {
         double* Acol = ctx->A + (int64_t)c * NB * lda;
         if (c > c0)
             launch_col_update(sp, ctx->A, lda, Panel{Acol - NB * lda, lda, 0}, nt, c, c, c1 - c, NB,
@@ -388,7 +352,6 @@ int factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, i
         if ((int64_t)c * NB < N)
             launch_potrf_diag(sp, Acol + (int64_t)c * NB, lda, N, (int64_t)c * NB, Dk, ctx->dres, slot(ctx, 2, 0));
         launch_trsm(sp, Acol, lda, nt, c, Dk, slot(ctx, 4, 0));
-        if (c == c0 && after_first) HIPQ(ctx, hipEventRecord(after_first, sp));
     }
     return 0;
 }
@@ -426,20 +389,15 @@ void extra_rows_step(gaplac_ctx* ctx, hipStream_t sm, int64_t lda, int nt, int p
     }
 }
 
-// Super-panel boundaries: tile columns sp[p] .. sp[p+1]-1 form SP p. Width spw throughout,
-// except that a plain logpdf switches to tail_w once at most tail_m tile columns remain:
-// in the chain-bound tail a narrow super-panel keeps the lookahead update short (K = 128
-// tail_w instead of 128 spw) while the bulk updates have slack.
-// With a serial tail (tail_s > 0) the list stops at the first boundary with at most tail_s
-// tile columns after it; those columns are factored by serial_tail().
+// Super-panel boundaries: tile columns sp[p] .. sp[p+1]-1 form SP p, width spw. With a
+// serial tail (tail_s > 0, plain logpdf) the list stops at the first boundary with at
+// most tail_s tile columns after it; those columns are factored by serial_tail().
 static std::vector<int> superpanel_starts(const gaplac_ctx* ctx, int nt) {
     std::vector<int> sp{0};
     int c = 0;
     while (c < nt) {
         if (ctx->xr_mode == 0 && ctx->tail_s > 0 && c > 0 && nt - c <= ctx->tail_s) break;
-        const bool tail = ctx->xr_mode == 0 && ctx->tail_w > 0 && nt - c <= ctx->tail_m && c > 0;
-        const bool head = ctx->xr_mode == 0 && c == 0 && ctx->head_w > 0;  // within Gram part 1
-        c = std::min(c + (head ? std::min(ctx->head_w, ctx->spw) : tail ? ctx->tail_w : ctx->spw), nt);
+        c = std::min(c + ctx->spw, nt);
         sp.push_back(c);
     }
     return sp;
@@ -458,14 +416,9 @@ static void serial_tail(gaplac_ctx* ctx, hipStream_t sm, int64_t N, int64_t lda,
             const int m = nt - c;
             BulkArgs ba{ctx->A, lda, Panel{Acol - NB * lda, lda, 0}, ctx->tiles + ctx->tile_off[(size_t)m],
                         m * (m + 1) / 2, NB, c, c, ColMap{1, 0, ctx->spw}};
-            ba.fine = ctx->fine_tail ? 1 : 0;
             launch_bulk(sm, ba, slot(ctx, 6, 0));
         }
         double* Dk = ctx->Dinv + (size_t)c * DINV_PER_BLOCK;
-        if (ctx->fused_tail) {
-            launch_diag_trsm(sm, Acol, lda, N, nt, c, Dk, ctx->dres, slot(ctx, 2, 0));
-            continue;
-        }
         if ((int64_t)c * NB < N)
             launch_potrf_diag(sm, Acol + (int64_t)c * NB, lda, N, (int64_t)c * NB, Dk, ctx->dres, slot(ctx, 2, 0));
         launch_trsm(sm, Acol, lda, nt, c, Dk, slot(ctx, 4, 0));
@@ -488,30 +441,8 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         const int m = nt - j0;
         BulkArgs ba{ctx->A, lda, pn, ctx->tiles + ctx->tile_off[(size_t)m], m * (m + 1) / 2, kdep, j0, j0,
                     ColMap{1, 0, W}};
-        ba.yield = (m <= ctx->yield_m && sp != sm) ? 1 : 0;
         const bool small = syrk_is_small(ba.ntiles);
-        if (m <= ctx->persist_m && sp != sm) ba.persist = (small ? ctx->persist_q : ctx->persist_t) * ctx->ncu;
-        // GAPLAC_SPARE: large launches on a capped grid of 2 x CUs - spare looping workgroups,
-        // so `spare` CUs hold one bulk workgroup and always have room for a chain workgroup
-        if (ctx->spare > 0 && sp != sm && !ctx->xr_mode && !small && ba.ntiles > 2 * ctx->ncu) ba.persist = 2 * ctx->ncu - ctx->spare;
-        // GAPLAC_QUAD_TAIL=pct: when the last round of 2 x CUs tiles would be less than pct %
-        // full, those tiles run as quadrant workgroups (4 per tile) in a second launch
-        int full = ba.ntiles;
-        if (ctx->quad_tail > 0 && !small && ba.persist == 0 && !ctx->tiles_host.empty()) {
-            const int slots = 2 * ctx->ncu, rem = ba.ntiles % slots;
-            if (rem > 0 && rem * 100 < slots * ctx->quad_tail) full = ba.ntiles - rem;
-        }
-        double fl = syrk_flops(m) * (kdep / NB), by = syrk_bytes(m, kdep);
-        if (full < ba.ntiles) {  // exact flops of the list's first `full` tiles
-            const uint32_t* L = ctx->tiles_host.data() + ctx->tile_off[(size_t)m];
-            int d = 0;
-            for (int i = 0; i < full; ++i) d += (L[i] & 0xffffu) == (L[i] >> 16);
-            fl = ((double)(full - d) * 2.0 * NB * NB * NB + (double)d * NB * NB * (NB + 1)) * (kdep / NB);
-            by = by * full / ba.ntiles;
-            ba.max_r = ba.max_c = m - 1;
-        }
-        BulkArgs bt = ba;
-        bt.ntiles = full;
+        const double fl = syrk_flops(m) * (kdep / NB), by = syrk_bytes(m, kdep);
         KTime* kt = small ? slot(ctx, 6, 0) : slot(ctx, 0, fl, by);
         const bool ev = ctx->prof_mode == 2 && !small;
         size_t e0 = 0;
@@ -524,23 +455,16 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             }
             HIPQ(ctx, hipEventRecord(ctx->evpool[e0], sm));
         }
-        launch_bulk(sm, bt, kt);
+        launch_bulk(sm, ba, kt);
         if (ev) {
             HIPQ(ctx, hipEventRecord(ctx->evpool[e0 + 1], sm));
             ctx->evpairs.push_back({e0, fl, by, 0});
-        }
-        if (full < ba.ntiles) {
-            BulkArgs bq = ba;
-            bq.tiles = ba.tiles + full;
-            bq.ntiles = ba.ntiles - full;
-            launch_bulk(sm, bq, slot(ctx, 6, 0));
         }
         return 0;
     };
     int pend = -1;  // the super-panel not yet applied to the columns >= dcol (paired updates)
     int dcol = nt;
     for (int p = 0; p < nsp; ++p) {
-        bool diag_first = false;
         const int c0 = spc[(size_t)p], c1 = spc[(size_t)p + 1];
         const int kd = (c1 - c0) * NB;  // depth of super-panel p
         if (p + 1 < nsp) {
@@ -549,51 +473,20 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             else
                 HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_gram2, 0));  // rest of the Gram built
             const int c2 = spc[(size_t)p + 2];
-            // Split lookahead (GAPLAC_LA_SPLIT_M, chain-bound steps): the panel chain applies
-            // SP p to the first column of SP p+1 only and factors it, while s_main applies SP
-            // p to the other columns of SP p+1 ahead of its bulk update (event S(p)).
-            const int mb0 = nt - (p + 2 <= nsp ? spc[(size_t)p + 2] : spc[(size_t)nsp]);
-            const bool split = sp != sm && c2 - c1 > 1 && mb0 > 0 && mb0 <= ctx->la_split_m;
-            launch_col_update(sp, ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nt, c1, c1,
-                              split ? 1 : c2 - c1, kd, slot(ctx, 5, 0));
-            if (split) {
-                if ((frc = factor_superpanel(ctx, sp, N, lda, nt, c1, c2, nullptr, c1, c1 + 1))) return frc;
-                HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_P[p & 1], 0));
-                launch_col_update(sm, ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nt, c1 + 1,
-                                  c1 + 1, c2 - c1 - 1, kd, slot(ctx, 5, 0));
-                HIPQ(ctx, hipEventRecord(ctx->ev_S[p & 1], sm));
-                HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_S[p & 1], 0));
-                if ((frc = factor_superpanel(ctx, sp, N, lda, nt, c1, c2, nullptr, c1 + 1, c2))) return frc;
-                HIPQ(ctx, hipEventRecord(ctx->ev_P[(p + 1) & 1], sp));
-                goto bulk;
-            }
-            // only GAPLAC_LA_FIRST waits on L(p); an unneeded record costs ~6 us of dispatch
-            // latency on the chain
-            if (ctx->la_first > 0) HIPQ(ctx, hipEventRecord(ctx->ev_L[p & 1], sp));
-            // In the chain-bound steps (small trailing matrix) the bulk update waits until the
-            // next super-panel's first diagonal block and TRSM have run: launched together,
-            // the bulk tiles take every CU's LDS first and the diagonal block (75 KB) waits for
-            // one to retire (107 instead of 33 us); the bulk has slack there.
-            const int mb = nt - (p + 2 <= nsp ? spc[(size_t)p + 2] : spc[(size_t)nsp]);
-            diag_first = sp != sm && mb > 0 && mb <= ctx->diag_first_m;
-            if ((frc = factor_superpanel(ctx, sp, N, lda, nt, c1, c2, diag_first ? ctx->ev_D[p & 1] : nullptr)))
-                return frc;
+            launch_col_update(sp, ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nt, c1, c1, c2 - c1,
+                              kd, slot(ctx, 5, 0));
+            if ((frc = factor_superpanel(ctx, sp, N, lda, nt, c1, c2))) return frc;
             HIPQ(ctx, hipEventRecord(ctx->ev_P[(p + 1) & 1], sp));
         }
         HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_P[p & 1], 0));
-    bulk:
-        if (diag_first) HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_D[p & 1], 0));
         // tile columns after SP p+1; the last super-panel also updates a serial tail
         const int jb = p + 2 <= nsp ? spc[(size_t)p + 2] : spc[(size_t)nsp];
-        if (p + 1 < nsp && jb < nt && sp != sm && ctx->la_split_m == 0 &&
-            (nt - jb) * (nt - jb + 1) / 2 <= ctx->la_first)
-            HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_L[p & 1], 0));
         // Paired bulk updates (GAPLAC_PAIR_M): at a deferring step only the next-needed band
         // (SP p+2's columns; with GAPLAC_PAIR_EXT also SP p+3's) gets SP p, and the tile
         // columns after it get SPs p and p+1 in one K = 2 x 128W update at step p+1 (band
         // first, then R(p), then the rest). Columns >= dcol lack SP pend.
         const int je = p + 3 <= nsp ? spc[(size_t)p + 3] : spc[(size_t)nsp];
-        const bool defer = ctx->pair_m > 0 && pend < 0 && sp != sm && (!ctx->xr_mode || ctx->pair_xr) && je > jb &&
+        const bool defer = ctx->pair_m > 0 && pend < 0 && sp != sm && !ctx->xr_mode && je > jb &&
                            p + 1 + ctx->pair_ext < nsp && p + 3 + ctx->pair_ext <= nsp &&
                            nt - spc[(size_t)p + 3 + ctx->pair_ext] >= ctx->pair_m;
         // a band [b0, b1) with the panel columns pc .. c1-1
@@ -675,7 +568,6 @@ int ensure_tile_lists(gaplac_ctx* ctx, int nt) {
     int rc;
     if ((rc = ensure(ctx, &ctx->tiles, &ctx->tiles_elems, total))) return rc;
     HIPCK(ctx, hipMemcpy(ctx->tiles, host.data(), total * sizeof(uint32_t), hipMemcpyHostToDevice));
-    if (ctx->quad_tail > 0) ctx->tiles_host = host;  // only GAPLAC_QUAD_TAIL reads it (~90 MB at N=65536)
     ctx->tile_off = off;
     ctx->tiles_nt = nt;
     return 0;
@@ -773,17 +665,6 @@ int enqueue_eval(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt) {
     return 0;
 }
 
-void drop_graph(gaplac_ctx* ctx, bool prof) {
-    hipGraphExec_t& gx = prof ? ctx->pgexec : ctx->gexec;
-    hipGraph_t& g = prof ? ctx->pgraph : ctx->graph;
-    if (gx) (void)hipGraphExecDestroy(gx);
-    if (g) (void)hipGraphDestroy(g);
-    gx = nullptr;
-    g = nullptr;
-    (prof ? ctx->pgN : ctx->gN) = -1;
-    if (prof) ctx->pslots.clear();
-}
-
 // Workspace for order N (grown on demand).
 int ensure_workspace(gaplac_ctx* ctx, int64_t N) {
     const int64_t Np = round_up(N + 1, NB);
@@ -869,43 +750,6 @@ int eval_device(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp, EvalR
     }
     *ctx->htp = tp;
     HIPCK(ctx, hipMemcpyAsync(ctx->dtp, ctx->htp, sizeof(TermPack), hipMemcpyHostToDevice, ctx->s_main));
-    if (ctx->use_graph && !ctx->serial && ctx->prof_mode != 2 && !ctx->xr_mode) {
-        hipGraph_t& G = prof ? ctx->pgraph : ctx->graph;
-        hipGraphExec_t& GX = prof ? ctx->pgexec : ctx->gexec;
-        int64_t& GN = prof ? ctx->pgN : ctx->gN;
-        const void** GP = prof ? ctx->pgptrs : ctx->gptrs;
-        const void* ptrs[6] = {ctx->A, ctx->Dinv, ctx->dX, ctx->dv, ctx->tiles, prof ? (const void*)ctx->dkt : nullptr};
-        if (!GX || GN != N || std::memcmp(ptrs, GP, sizeof ptrs) != 0) {
-            drop_graph(ctx, prof);
-            ctx->slots.clear();
-            ctx->recording = prof;
-            HIPCK(ctx, hipStreamBeginCapture(ctx->s_main, hipStreamCaptureModeThreadLocal));
-            rc = enqueue_eval(ctx, N, D, Np, nt);
-            ctx->recording = false;
-            hipGraph_t g = nullptr;
-            const hipError_t ce = hipStreamEndCapture(ctx->s_main, &g);
-            if (rc) {
-                if (g) (void)hipGraphDestroy(g);
-                return rc;
-            }
-            if (ce != hipSuccess)
-                return set_err(ctx, GAPLAC_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ce));
-            G = g;
-            if (ctx->graph_prio)
-                HIPCK(ctx, hipGraphInstantiateWithFlags(&GX, G, hipGraphInstantiateFlagUseNodePriority));
-            else
-                HIPCK(ctx, hipGraphInstantiate(&GX, G, nullptr, nullptr, 0));
-            GN = N;
-            std::memcpy(GP, ptrs, sizeof ptrs);
-            if (prof) ctx->pslots = ctx->slots;
-            ctx->slots.clear();
-        }
-        HIPCK(ctx, hipGraphLaunch(GX, ctx->s_main));
-        HIPCK(ctx, hipStreamSynchronize(ctx->s_main));
-        *out = *ctx->hres;
-        if (prof) return accumulate_slots(ctx, ctx->pslots);
-        return 0;
-    }
     ctx->slots.clear();
     ctx->recording = prof;
     rc = enqueue_eval(ctx, N, D, Np, nt);
@@ -1086,28 +930,14 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (device < 0 || device >= n) return GAPLAC_E_NODEVICE;
     gaplac_ctx* ctx = new gaplac_ctx();
     ctx->device = device;
+    // the schedule switches
     if (const char* s = std::getenv("GAPLAC_SERIAL")) ctx->serial = s[0] == '1';
-    if (const char* s = std::getenv("GAPLAC_LA_FIRST")) ctx->la_first = std::max(0, std::atoi(s));
-    if (const char* s = std::getenv("GAPLAC_YIELD_M")) ctx->yield_m = std::max(0, std::atoi(s));
-    if (const char* s = std::getenv("GAPLAC_TAIL_M")) ctx->tail_m = std::max(0, std::atoi(s));
-    if (const char* s = std::getenv("GAPLAC_TAIL_W")) ctx->tail_w = std::max(0, std::min(8, std::atoi(s)));
+    if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAIL_S")) ctx->tail_s = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_GRAM_QUEUE")) ctx->gram_queue = std::max(0, std::min(4, std::atoi(s)));
-    if (const char* s = std::getenv("GAPLAC_DIAG_FIRST_M")) ctx->diag_first_m = std::max(0, std::atoi(s));
-    if (const char* s = std::getenv("GAPLAC_HEAD_W")) ctx->head_w = std::max(0, std::atoi(s));
-    if (const char* s = std::getenv("GAPLAC_FUSED_TAIL")) ctx->fused_tail = s[0] == '1';
-    if (const char* s = std::getenv("GAPLAC_QUAD_TAIL")) ctx->quad_tail = std::max(0, std::min(100, std::atoi(s)));
-    if (const char* s = std::getenv("GAPLAC_FINE_TAIL")) ctx->fine_tail = s[0] != '0';
-    if (const char* s = std::getenv("GAPLAC_PAIR_XR")) ctx->pair_xr = s[0] == '1';
-    if (const char* s = std::getenv("GAPLAC_PAIR_EXT")) ctx->pair_ext = std::max(0, std::min(1, std::atoi(s)));
-    if (const char* s = std::getenv("GAPLAC_SPARE")) ctx->spare = std::max(0, std::min(255, std::atoi(s)));
-    if (const char* s = std::getenv("GAPLAC_BAND_TILES_M")) ctx->band_tiles_m = std::max(1, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_PAIR_M")) ctx->pair_m = std::max(0, std::atoi(s));
-    if (const char* s = std::getenv("GAPLAC_LA_SPLIT_M")) ctx->la_split_m = std::max(0, std::atoi(s));
-    if (const char* s = std::getenv("GAPLAC_PERSIST_M")) ctx->persist_m = std::max(0, std::atoi(s));
-    if (const char* s = std::getenv("GAPLAC_PERSIST_T")) ctx->persist_t = std::max(1, std::min(2, std::atoi(s)));
-    if (const char* s = std::getenv("GAPLAC_PERSIST_Q")) ctx->persist_q = std::max(1, std::min(8, std::atoi(s)));
-    if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
+    if (const char* s = std::getenv("GAPLAC_PAIR_EXT")) ctx->pair_ext = std::max(0, std::min(1, std::atoi(s)));
+    if (const char* s = std::getenv("GAPLAC_BAND_TILES_M")) ctx->band_tiles_m = std::max(1, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     auto fail = [&](const char* what, hipError_t e) {
         std::fprintf(stderr, "gaplac_ctx_create: %s: %s\n", what, hipGetErrorString(e));
@@ -1116,11 +946,9 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     };
     hipError_t e;
     if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
-    // s_panel: highest priority, all CUs; s_main: lowest priority. Optionally
-    // (GAPLAC_DIAG_CUS=n) s_main gets a CU mask that keeps n CUs free for the panel chain
-    // (a masked stream has no priority). Measured at N=16384: priorities alone, eager
-    // launches: 37.0 ms; mask of 1 CU: 38.2 ms; graph replay (priorities are not carried
-    // into graph nodes): 37.9 ms with the mask, 39.4 ms without.
+    // s_panel: highest priority; s_main: lowest priority. A CU mask for the
+    // chain and hipGraph replay were both measured slower (graph nodes lose the stream
+    // priorities) and are not kept.
     int ncu = 0;
     if ((e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
         return fail("attribute", e);
@@ -1130,30 +958,12 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
         return fail("priority range", e);
     if ((e = hipStreamCreateWithPriority(&ctx->s_panel, hipStreamNonBlocking, greatest)) != hipSuccess)
         return fail("stream", e);
-    int want = 0;
-    if (const char* s = std::getenv("GAPLAC_DIAG_CUS")) want = std::atoi(s);
-    if (want > 0 && ncu > 2 * want) {
-        const int words = (ncu + 31) / 32;
-        std::vector<uint32_t> rest((size_t)words, 0u);
-        for (int c = want; c < ncu; ++c) rest[(size_t)c / 32] |= 1u << (c % 32);
-        if (hipExtStreamCreateWithCUMask(&ctx->s_main, (uint32_t)words, rest.data()) == hipSuccess)
-            ctx->diag_cus = want;
-        else
-            ctx->s_main = nullptr;
-    }
-    if (!ctx->s_main &&
-        (e = hipStreamCreateWithPriority(&ctx->s_main, hipStreamNonBlocking, least)) != hipSuccess)
+    if ((e = hipStreamCreateWithPriority(&ctx->s_main, hipStreamNonBlocking, least)) != hipSuccess)
         return fail("stream", e);
     for (int q = 0; q < 2; ++q) {
         if ((e = hipEventCreateWithFlags(&ctx->ev_P[q], hipEventDisableTiming)) != hipSuccess)
             return fail("event", e);
         if ((e = hipEventCreateWithFlags(&ctx->ev_R[q], hipEventDisableTiming)) != hipSuccess)
-            return fail("event", e);
-        if ((e = hipEventCreateWithFlags(&ctx->ev_L[q], hipEventDisableTiming)) != hipSuccess)
-            return fail("event", e);
-        if ((e = hipEventCreateWithFlags(&ctx->ev_D[q], hipEventDisableTiming)) != hipSuccess)
-            return fail("event", e);
-        if ((e = hipEventCreateWithFlags(&ctx->ev_S[q], hipEventDisableTiming)) != hipSuccess)
             return fail("event", e);
     }
     if ((e = hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming)) != hipSuccess)
@@ -1181,8 +991,6 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
         return fail("hipMalloc", e);
     if ((e = hipHostMalloc(reinterpret_cast<void**>(&ctx->hgp), sizeof(GradTermPack), 0)) != hipSuccess)
         return fail("hipHostMalloc", e);
-    if (const char* s = std::getenv("GAPLAC_GRAPH")) ctx->use_graph = s[0] == '1';
-    if (const char* s = std::getenv("GAPLAC_GRAPH_PRIO")) ctx->graph_prio = s[0] != '0';
     *out = ctx;
     return 0;
 }
@@ -1202,9 +1010,6 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     for (int q = 0; q < 2; ++q) {
         if (ctx->ev_P[q]) (void)hipEventDestroy(ctx->ev_P[q]);
         if (ctx->ev_R[q]) (void)hipEventDestroy(ctx->ev_R[q]);
-        if (ctx->ev_L[q]) (void)hipEventDestroy(ctx->ev_L[q]);
-        if (ctx->ev_D[q]) (void)hipEventDestroy(ctx->ev_D[q]);
-        if (ctx->ev_S[q]) (void)hipEventDestroy(ctx->ev_S[q]);
     }
     if (ctx->ev_gram) (void)hipEventDestroy(ctx->ev_gram);
     if (ctx->ev_gram2) (void)hipEventDestroy(ctx->ev_gram2);
@@ -1215,8 +1020,6 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     if (ctx->tiles) (void)hipFree(ctx->tiles);
     if (ctx->dX) (void)hipFree(ctx->dX);
     if (ctx->dv) (void)hipFree(ctx->dv);
-    drop_graph(ctx, false);
-    drop_graph(ctx, true);
     for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
     if (ctx->dkt) (void)hipFree(ctx->dkt);
     if (ctx->hkt) (void)hipHostFree(ctx->hkt);

@@ -35,7 +35,6 @@ struct EvalResult {
     unsigned long long info;  // min over failing pivots of (j+1); ULLONG_MAX = none
     double part[2][REDUCE_BLOCKS];  // per-workgroup partial sums of the reduction
     unsigned gram_ticket;           // work queue of the second Gram launch (zeroed per eval)
-    unsigned diag_done;             // fused serial tail: last tile column whose L_kk is final, + 1
 };
 
 // Per-launch device timestamps (profiling): 100 MHz s_memrealtime ticks.
@@ -77,10 +76,7 @@ struct BulkArgs {
     ColMap cm;
     int rect_rows = 0;
     int max_r = -1, max_c = -1;  // largest lo16 / hi16 list entry (-1: an m x m triangle list)
-    int yield = 0;  // step aside on CUs where panel-chain waves run
-    int persist = 0;  // > 0: grid capped at this many workgroups, each looping over tiles
     int whole = 0;    // 1: a band list as 128x128 tile workgroups (tile_band_kernel), never quadrants
-    int fine = 0;     // 1 (K = 128 only): sixteen 32x32 workgroups per tile (fine_bulk_kernel)
 };
 
 // Host-side footprint guard. Before launching, every launcher computes the
@@ -137,9 +133,6 @@ void launch_potrf_diag(hipStream_t s, double* Ablk, int64_t lda, int64_t N, int6
 // TRSM of the panel rows below diagonal block k: Acol is the storage of global column
 // k*NB; rows bi*NB.. for bi = k+1..nt-1 become A[bi,k] L_kk^{-T}.
 void launch_trsm(hipStream_t s, double* Acol, int64_t lda, int nt, int k, const double* Dinv, KTime* kt);
-// Diagonal block k and the TRSM of the tiles below it in one launch (serial tail only).
-void launch_diag_trsm(hipStream_t s, double* Acol, int64_t lda, int64_t N, int nt, int k, double* Dinv,
-                      EvalResult* res, KTime* kt);
 // Same substitution for an arbitrary run of row tiles bi0 .. bi0+nrows-1 of column k
 // (the gradient's identity rows below the matrix).
 void launch_trsm_rows(hipStream_t s, double* Acol, int64_t lda, int k, int bi0, int nrows, const double* Dinv,

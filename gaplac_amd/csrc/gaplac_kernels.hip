@@ -55,51 +55,6 @@ __device__ __forceinline__ void kt_end(KTime* kt) {
     if (kt && (threadIdx.x & 63) == 0) atomicMax(&kt->end, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
-// ---------------------------------------------------------------------------------
-// CU-local priority for the critical path. Standalone the panel chain
-// (diagonal block, TRSM, column updates) costs ~3 ms of chip time per N=16384 evaluation,
-// but beside MFMA-saturating bulk waves on the same SIMDs it runs 2-4x slower and slows
-// the bulk update in turn. So chain waves announce themselves on their CU (a counter per
-// CU, indexed by XCC id and the SE/SH/CU bits of HW_ID; placement only, never correctness)
-// and the bulk waves of that CU step aside: they read the counter once per k-chunk (the
-// value is used one chunk later, so the load never stalls the MFMA stream) and, while a
-// chain wave is present, sleep in a bounded loop. Vector atomics only.
-// ---------------------------------------------------------------------------------
-__device__ int g_cu_busy[2048];
-
-__device__ __forceinline__ int cu_key() {
-    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // HW_REG_XCC_ID [3:0]
-    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);   // HW_REG_HW_ID
-    return (int)(((xcc & 7u) << 8) | ((hw >> 8) & 0xffu));  // CU_ID [11:8], SH_ID [12], SE_ID [15:13]
-}
-__device__ __forceinline__ void chain_enter() {
-    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(&g_cu_busy[cu_key()], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void chain_leave() {
-    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(&g_cu_busy[cu_key()], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int cu_busy_load(int key) {
-    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(&g_cu_busy[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-// Bulk side: sleep while a chain wave shares this CU (bounded: ~2k cycles per round).
-__device__ __noinline__ void yield_to_chain(int key) {
-    for (int it = 0; it < 8192; ++it) {
-        __builtin_amdgcn_s_sleep(32);
-        if (cu_busy_load(key) <= 0) break;
-    }
-}
-// Which critical-path kernels claim their CU (bit mask): 1 diagonal block, 2 TRSM,
-// 4 column updates inside a super-panel (K = 128), 8 lookahead column update (K = 128 W).
-// A claim is two relaxed atomics per wave and matters only to bulk launches that yield
-// (BulkArgs::yield, set by the host for trailing matrices of <= GAPLAC_YIELD_M tile rows).
-// Off by default: measured at N = 16384, yielding in every step is slower end to end (32.8
-// vs 30.7 ms: the bulk is the critical path while the trailing matrix is large), and
-// yielding only in the chain-bound steps (GAPLAC_YIELD_M = 40..100, claims 15) gains
-// nothing (30.6-31.9 vs 30.7 ms) -- DESIGN.md §3. Build with -DGAPLAC_YIELD=15 to try.
-#ifndef GAPLAC_YIELD
-#define GAPLAC_YIELD 0
-#endif
-
 // Row-major triangular tile index: t = bi*(bi+1)/2 + bj, 0 <= bj <= bi.
 __device__ __forceinline__ void tri_index(int64_t t, int& bi, int& bj) {
     int b = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
@@ -835,9 +790,7 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ Ag
                                                          EvalResult* __restrict__ res,
                                                          KTime* __restrict__ kt) {
     kt_begin(kt);
-    if (GAPLAC_YIELD & 1) chain_enter();
     potrf_diag_kernel_body(Ag, lda, N, g0, Dinv, res);
-    if (GAPLAC_YIELD & 1) chain_leave();
     kt_end(kt);
 }
 
@@ -925,94 +878,7 @@ __global__ __launch_bounds__(256) void trsm_subst_kernel(
                                                          int bi0, const double* __restrict__ Dinv,
                                                          KTime* __restrict__ kt) {
     kt_begin(kt);
-    if (GAPLAC_YIELD & 2) chain_enter();
     trsm_subst_kernel_body(Acol, lda, k, bi0, Dinv, (int)blockIdx.x);
-    if (GAPLAC_YIELD & 2) chain_leave();
-    kt_end(kt);
-}
-
-// Serial tail (GAPLAC_FUSED_TAIL): diagonal block k (workgroup 0) and the TRSM of the
-// tiles below it (workgroups 1 .. 2n) in one launch. Workgroup 0 is dispatched first and
-// waits on nothing; when L_kk and its 16x16 inverses are stored it publishes k + 1 in
-// EvalResult::diag_done (zeroed per evaluation) with release semantics, and the TRSM
-// workgroups, resident meanwhile, start the substitution as soon as they observe it. The
-// wait is bounded (100 ms of the 100 MHz clock), so a lost update cannot hang the GPU.
-// Only for the serial tail, where nothing else runs beside the chain: waiting workgroups
-// hold their CU slots. Same arithmetic as the two kernels: bitwise equal results.
-__global__ __launch_bounds__(256) void diag_trsm_kernel(double* __restrict__ Acol, int64_t lda, int64_t N, int k,
-                                                        double* __restrict__ Dinv, EvalResult* __restrict__ res,
-                                                        KTime* __restrict__ kt) {
-    kt_begin(kt);
-    const int64_t g0 = (int64_t)k * NB;
-    if (blockIdx.x == 0) {
-        if (g0 < N) potrf_diag_kernel_body(Acol + g0, lda, N, g0, Dinv, res);
-        __threadfence();
-        __syncthreads();
-        if (threadIdx.x == 0)
-            __hip_atomic_store(&res->diag_done, (unsigned)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        if (threadIdx.x == 0) {
-            const unsigned long long t0 = wall_clock64();
-            while (__hip_atomic_load(&res->diag_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(k + 1)) {
-                __builtin_amdgcn_s_sleep(2);
-                if (wall_clock64() - t0 > 10000000ull) break;
-            }
-        }
-        __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        trsm_subst_kernel_body(Acol, lda, k, k + 1, Dinv, (int)blockIdx.x - 1);
-    }
-    kt_end(kt);
-}
-
-// Panel TRSM, light variant: the same substitution, one wave (16 rows) per workgroup and no
-// LDS: the L_kk and Dinv fragments come straight from L2 (every TRSM workgroup of the
-// column reads the same 128 KB). At <= 96 registers a workgroup fits beside two resident
-// bulk-update workgroups (2 x 208 registers, 2 x 72 KB LDS), so it starts at once instead
-// of taking the slot of a retiring bulk tile for its whole life.
-// One accumulator per block: an f64 MFMA costs 64 cycles dependent or not.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void trsm_lite_kernel(
-    double* __restrict__ Acol, int64_t lda, int k, int bi0, const double* __restrict__ Dinv,
-    KTime* __restrict__ kt) {
-    kt_begin(kt);
-    __builtin_amdgcn_s_setprio(2);  // critical path
-    const int lane = threadIdx.x;
-    const int fr = lane >> 4, fc = lane & 15;
-    const int bi = bi0 + (int)(blockIdx.x >> 3);
-    const int64_t k0 = (int64_t)k * NB;
-    const double* L = Acol + k0;  // L_kk, column-major, lda
-    double* B = Acol + (int64_t)bi * NB + 16 * (blockIdx.x & 7);
-    d4 Y[NDB];
-    // fragments of L(16b + fc, 16c + fr + 4kk), kk = 0..3, for the step after the current one
-    auto lfrag = [&](int b, int c, double (&f)[4]) {
-        const double* Lbc = L + (int64_t)(16 * c + fr) * lda + 16 * b + fc;
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) f[kk] = Lbc[(int64_t)(4 * kk) * lda];
-    };
-#pragma unroll
-    for (int b = 0; b < NDB; ++b) {
-        d4 acc;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = B[(int64_t)(16 * b + fr + 4 * q) * lda + fc];  // B_b^T
-        double fcur[4], fnext[4];
-        if (b > 0) lfrag(b, 0, fcur);
-#pragma unroll
-        for (int c = 0; c < b; ++c) {
-            if (c + 1 < b) lfrag(b, c + 1, fnext);  // one step ahead
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-fcur[kk], Y[c][kk], acc, 0, 0, 0);
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) fcur[kk] = fnext[kk];
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        const double* Di = Dinv + b * 256 + fr * 16 + fc;  // column-major [j = fc][m = 4kk + fr]
-        d4 y = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) y = __builtin_amdgcn_mfma_f64_16x16x4f64(Di[64 * kk], acc[kk], y, 0, 0, 0);
-        Y[b] = y;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) B[(int64_t)(16 * b + fr + 4 * q) * lda + fc] = y[q];
-    }
     kt_end(kt);
 }
 
@@ -1072,13 +938,10 @@ __device__ __forceinline__ void tile_decode(const BulkArgs& a, int idx, int& bi,
 // tile j) are column-major with leading dimension ldp. Lane element (mi, mj, rg) is tile
 // entry (row 64 wi + 16 mi + (lane & 15), column 64 wj + 16 mj + (lane >> 4) + 4 rg).
 // Inactive waves (upper quadrant of a diagonal tile) only help with the staging.
-template <bool OPQ = false>
 __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const double* __restrict__ Q,
-                                             int64_t ldp, int kdepth, bool active, d4 (&acc)[4][4],
-                                             bool yield = false) {
+                                             int64_t ldp, int kdepth, bool active, d4 (&acc)[4][4]) {
     __shared__ double sm[2][2][KB][LR];
-    int tid = threadIdx.x;
-    if constexpr (OPQ) asm volatile("" : "+v"(tid));  // opaque in a tile loop: no lane-dependent hoisting
+    const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
     const int wi = w & 1, wj = w >> 1;
     const int fr = lane >> 4, fc = lane & 15;
@@ -1122,15 +985,9 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
     GAPLAC_LSTORE(0);
     __syncthreads();
     const int NCH = kdepth / KB;
-    const int key = yield ? cu_key() : 0;
-    int busy = 0;  // this CU's chain-wave count, read one chunk earlier
     for (int ch = 0; ch < NCH; ++ch) {
         const int buf = ch & 1;
         const bool more = ch + 1 < NCH;
-        if (yield) {
-            if (busy > 0) yield_to_chain(key);
-            busy = cu_busy_load(key);
-        }
         if (more) GAPLAC_GLOAD(ch + 1);
         if (active) {
 #pragma unroll
@@ -1156,7 +1013,6 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
 #undef GAPLAC_LSTORE
 }
 
-template <bool OPQ = false>
 __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
     const int chunk = (a.ntiles + 7) >> 3;
     const int idx = (b & 7) * chunk + (b >> 3);
@@ -1168,8 +1024,7 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
     double* __restrict__ Ct = a.C + (int64_t)lj * NB * ldc + r0;
     const double* __restrict__ P = a.pn.P + (r0 - a.pn.row0);
     const double* __restrict__ Q = a.pn.P + ((int64_t)bj * NB - a.pn.row0);
-    int tid = threadIdx.x;
-    if constexpr (OPQ) asm volatile("" : "+v"(tid));  // opaque in a tile loop: no lane-dependent hoisting
+    const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
     const int wi = w & 1, wj = w >> 1;
     const bool active = !(bi == bj && wj > wi);
@@ -1187,7 +1042,7 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
                     acc[mi][mj][rg] = Ci[(int64_t)(64 * wj + 16 * mj + fr + 4 * rg) * ldc];
         }
     }
-    tile_mma_neg<OPQ>(P, Q, a.pn.ld, a.kdepth, active, acc, a.yield != 0);
+    tile_mma_neg(P, Q, a.pn.ld, a.kdepth, active, acc);
     if (!active) return;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
@@ -1200,22 +1055,11 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
     }
 }
 
-// A capped grid (BulkArgs.persist, a multiple of 8) walks the virtual blocks with stride
-// gridDim.x, which keeps every block's XCD (b % 8) and leaves room on each CU for the
-// panel chain's workgroups.
-// One tile per workgroup (208 VGPRs: two resident bulk workgroups leave exactly the 96
-// registers a quadrant chain kernel needs) or, LOOP, a capped grid looping over the tiles
-// (the loop keeps more addresses live: 226 VGPRs; used for the large launches of the
-// spare-CU schedule, where one bulk workgroup + a diagonal block, 226 + 272, still fit).
-template <bool LOOP>
+// One tile per workgroup, 208 VGPRs: two resident bulk workgroups leave exactly the 96
+// registers a quadrant chain kernel needs.
 __global__ __launch_bounds__(256, 2) void tile_syrk_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
-    if constexpr (LOOP) {
-        const int nb = ((a.ntiles + 7) >> 3) << 3;
-        for (int b = (int)blockIdx.x; b < nb; b += (int)gridDim.x) tile_syrk_body<true>(a, b);
-    } else {
-        tile_syrk_body(a, (int)blockIdx.x);
-    }
+    tile_syrk_body(a, (int)blockIdx.x);
     kt_end(kt);
 }
 
@@ -1249,9 +1093,8 @@ constexpr int QG = GAPLAC_QG;
 constexpr int QUAD_BULK_MAX_TILES = 512;
 
 __device__ __forceinline__ void quad_update(double* __restrict__ C, int64_t ldc, const Panel& pn, int bi,
-                                            int bj, int lj, int qi, int qj, int kdepth, bool yield = false) {
-    int tid = threadIdx.x;
-    asm volatile("" : "+v"(tid));  // opaque: nothing lane-dependent is hoisted out of a tile loop
+                                            int bj, int lj, int qi, int qj, int kdepth) {
+    const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int wi = wave & 1, wj = wave >> 1;
     const int fr = lane >> 4, fc = lane & 15;
@@ -1291,14 +1134,8 @@ __device__ __forceinline__ void quad_update(double* __restrict__ C, int64_t ldc,
         }
     };
     const int ng = kdepth / (4 * QG);  // 4 per 128 panel columns
-    const int key = yield ? cu_key() : 0;
-    int busy = 0;  // as in tile_mma_neg: read one group pair earlier, used now
     load(0, 0);
     for (int g = 0; g < ng; g += 2) {
-        if (yield) {
-            if (busy > 0) yield_to_chain(key);
-            busy = cu_busy_load(key);
-        }
         if (g + 1 < ng) load(1, g + 1);
         compute(0);
         if (g + 1 < ng) {
@@ -1322,8 +1159,6 @@ __global__ __launch_bounds__(256) void col_update_kernel(double* __restrict__ C,
                                                          int jb0, int lj0, int m0, int kdepth,
                                                          KTime* __restrict__ kt) {
     kt_begin(kt);
-    const bool claim = (GAPLAC_YIELD & (kdepth <= NB ? 4 : 8)) != 0;
-    if (claim) chain_enter();
     __builtin_amdgcn_s_setprio(2);
     const int q = (int)blockIdx.x & 3;
     int t = (int)blockIdx.x >> 2, c = 0;
@@ -1333,49 +1168,6 @@ __global__ __launch_bounds__(256) void col_update_kernel(double* __restrict__ C,
     }
     const int jb = jb0 + c, bi = jb + t, qi = q >> 1, qj = q & 1;
     if (!(bi == jb && qj > qi)) quad_update(C, ldc, pn, bi, jb, lj0 + c, qi, qj, kdepth);
-    if (claim) chain_leave();
-    kt_end(kt);
-}
-
-// Latency-bound K = 128 updates of the serial tail: sixteen 32x32
-// workgroups per 128x128 tile, each wave one 16x16 block with a single accumulator. Every
-// panel fragment (32 k-steps x 2 operands) is loaded before the first MFMA, then the 32
-// MFMAs run back to back: the same per-element summation order as quad_update, so the
-// results are bitwise those of the quadrant kernel, in a fraction of its latency.
-__global__ __launch_bounds__(256) void fine_bulk_kernel(BulkArgs a, KTime* __restrict__ kt) {
-    kt_begin(kt);
-    const int t = (int)blockIdx.x >> 4, sub = (int)blockIdx.x & 15;
-    if (t < a.ntiles) {
-        int bi, bj, lj;
-        tile_decode(a, t, bi, bj, lj);
-        const int si = sub >> 2, sj = sub & 3;
-        if (!(bi == bj && sj > si)) {
-            const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-            const int wi = wave & 1, wj = wave >> 1;
-            const int fr = lane >> 4, fc = lane & 15;
-            const int64_t ri = (int64_t)bi * NB + 32 * si + 16 * wi;  // this wave's 16 rows
-            const int64_t cj = (int64_t)bj * NB + 32 * sj + 16 * wj;  // its 16 columns (global)
-            const int64_t cl = (int64_t)lj * NB + 32 * sj + 16 * wj;  // ... in storage
-            const int64_t ldp = a.pn.ld, ldc = a.ldc;
-            const double* P = a.pn.P + (ri - a.pn.row0) + fc;
-            const double* Q = a.pn.P + (cj - a.pn.row0) + fc;
-            double fa[NB / 4], fb[NB / 4];
-#pragma unroll
-            for (int s = 0; s < NB / 4; ++s) {
-                const int64_t col = (int64_t)(4 * s + fr) * ldp;
-                fb[s] = P[col];
-                fa[s] = Q[col];
-            }
-            d4 acc;
-#pragma unroll
-            for (int rg = 0; rg < 4; ++rg) acc[rg] = a.C[(cl + fr + 4 * rg) * ldc + ri + fc];
-            __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first MFMA
-#pragma unroll
-            for (int s = 0; s < NB / 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[s], -fb[s], acc, 0, 0, 0);
-#pragma unroll
-            for (int rg = 0; rg < 4; ++rg) a.C[(cl + fr + 4 * rg) * ldc + ri + fc] = acc[rg];
-        }
-    }
     kt_end(kt);
 }
 
@@ -1384,17 +1176,13 @@ __global__ __launch_bounds__(256) void fine_bulk_kernel(BulkArgs a, KTime* __res
 __global__ __launch_bounds__(256) void quad_bulk_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
     const int chunk = (a.ntiles + 7) >> 3;
-    const int nvb = 4 * (chunk << 3);
-    // capped grid (a multiple of 32): the stride keeps (vb >> 2) % 8, i.e. the XCD
-    for (int vb = (int)blockIdx.x; vb < nvb; vb += (int)gridDim.x) {
-        const int b = vb >> 2, q = vb & 3;
-        const int idx = (b & 7) * chunk + (b >> 3);
-        if (idx < a.ntiles) {
-            int bi, bj, lj;
-            tile_decode(a, idx, bi, bj, lj);
-            const int qi = q >> 1, qj = q & 1;
-            if (!(bi == bj && qj > qi)) quad_update(a.C, a.ldc, a.pn, bi, bj, lj, qi, qj, a.kdepth, a.yield != 0);
-        }
+    const int b = (int)blockIdx.x >> 2, q = (int)blockIdx.x & 3;
+    const int idx = (b & 7) * chunk + (b >> 3);
+    if (idx < a.ntiles) {
+        int bi, bj, lj;
+        tile_decode(a, idx, bi, bj, lj);
+        const int qi = q >> 1, qj = q & 1;
+        if (!(bi == bj && qj > qi)) quad_update(a.C, a.ldc, a.pn, bi, bj, lj, qi, qj, a.kdepth);
     }
     kt_end(kt);
 }
@@ -1479,7 +1267,6 @@ __global__ void init_result_kernel(EvalResult* res) {
     res->quad = 0.0;
     res->info = ~0ull;
     res->gram_ticket = 0u;
-    res->diag_done = 0u;
 }
 
 // ---------------------------------------------------------------------------------
@@ -2008,31 +1795,11 @@ void launch_potrf_diag(hipStream_t s, double* Ablk, int64_t lda, int64_t N, int6
     potrf_diag_kernel<<<dim3(1), dim3(256), 0, s>>>(Ablk, lda, N, g0, Dinv, res, kt);
 }
 
-// GAPLAC_TRSM_LITE=n: panel TRSMs with more than n tiles below the panel through
-// trsm_lite_kernel (one wave per 16 rows, no LDS); 0 = never.
-static int trsm_lite_mode() {
-    static const int m = [] {
-        const char* e = std::getenv("GAPLAC_TRSM_LITE");
-        return e ? std::atoi(e) : 0;
-    }();
-    return m;
-}
-
 void launch_trsm(hipStream_t s, double* Acol, int64_t lda, int nt, int k, const double* Dinv, KTime* kt) {
     const int n = nt - k - 1;
     if (n <= 0) return;
     if (!guard_launch("trsm_subst_kernel", Acol, 0, tiles_end(lda, nt - 1, 0))) return;
-    if (trsm_lite_mode() > 0 && n > trsm_lite_mode())  // more than that many tiles below the panel
-        trsm_lite_kernel<<<dim3(8 * n), dim3(64), 0, s>>>(Acol, lda, k, k + 1, Dinv, kt);
-    else
-        trsm_subst_kernel<<<dim3(2 * n), dim3(256), 0, s>>>(Acol, lda, k, k + 1, Dinv, kt);
-}
-
-void launch_diag_trsm(hipStream_t s, double* Acol, int64_t lda, int64_t N, int nt, int k, double* Dinv,
-                      EvalResult* res, KTime* kt) {
-    const int n = nt - k - 1;
-    if (!guard_launch("diag_trsm_kernel", Acol, 0, tiles_end(lda, nt - 1, 0))) return;
-    diag_trsm_kernel<<<dim3(1 + 2 * std::max(n, 0)), dim3(256), 0, s>>>(Acol, lda, N, k, Dinv, res, kt);
+    trsm_subst_kernel<<<dim3(2 * n), dim3(256), 0, s>>>(Acol, lda, k, k + 1, Dinv, kt);
 }
 
 void launch_trsm_rows(hipStream_t s, double* Acol, int64_t lda, int k, int bi0, int nrows, const double* Dinv,
@@ -2068,21 +1835,13 @@ void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt) {
         max_r = max_c = tri_row(a.ntiles - 1);  // an m x m triangle list: entries < m
     }
     if (!guard_launch("bulk update", a.C, 0, tiles_end(a.ldc, a.bi0 + max_r, a.lj0 + max_c))) return;
-    int grid = ((a.ntiles + 7) >> 3) << 3;
-    if (a.fine && a.kdepth == NB) {
-        fine_bulk_kernel<<<dim3((unsigned)(16 * a.ntiles)), dim3(256), 0, s>>>(a, kt);
-    } else if (syrk_is_small(a.ntiles) && !a.whole) {
-        int qg = 4 * grid;
-        if (a.persist > 0) qg = std::min(qg, std::max(32, a.persist & ~31));
-        quad_bulk_kernel<<<dim3((unsigned)qg), dim3(256), 0, s>>>(a, kt);
-    } else {
-        if (a.whole)
-            tile_band_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
-        else if (a.persist > 0 && a.persist < grid)
-            tile_syrk_kernel<true><<<dim3((unsigned)std::max(8, a.persist & ~7)), dim3(256), 0, s>>>(a, kt);
-        else
-            tile_syrk_kernel<false><<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
-    }
+    const int grid = ((a.ntiles + 7) >> 3) << 3;
+    if (syrk_is_small(a.ntiles) && !a.whole)
+        quad_bulk_kernel<<<dim3((unsigned)(4 * grid)), dim3(256), 0, s>>>(a, kt);
+    else if (a.whole)
+        tile_band_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
+    else
+        tile_syrk_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
 }
 
 void launch_col_update(hipStream_t s, double* C, int64_t ldc, const Panel& pn, int nt, int jb, int lj0,

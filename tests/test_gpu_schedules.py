@@ -1,24 +1,16 @@
 """The factorisation schedule's alternatives against the oracle and against each other
-(DESIGN.md §3.1, §4): every knob below changes only the order and grouping of the same
+(DESIGN.md §3.1, §4): every switch below changes only the order and grouping of the same
 updates, so each must reproduce the oracle's logpdf, logdet and quad (1e-12 relative at
 these sizes) and agree with the default schedule.
 
 * GAPLAC_TAIL_S: the last tile columns factored right-looking on one stream (serial tail;
   1000 makes it everything after the first super-panel, 0 turns it off);
-* GAPLAC_TAIL_M / GAPLAC_TAIL_W: narrow super-panels near the end;
 * GAPLAC_GRAM_QUEUE: the second Gram launch as a work queue (0 = plain grid);
 * GAPLAC_SPW: the super-panel width;
-* GAPLAC_LA_SPLIT_M: the lookahead of all but a super-panel's first column on the bulk
-  stream (1000: every step);
-* GAPLAC_PAIR_M: paired bulk updates (every other step the columns beyond the next band
-  receive two super-panels at once; 1: whenever possible);
-* GAPLAC_FINE_TAIL=1: the serial tail's K = 128 updates on the 32x32 fine_bulk_kernel instead of
-  quadrant workgroups (same per-element summation order: bitwise equal);
-* GAPLAC_QUAD_TAIL: a bulk launch's partial last round as quadrant workgroups;
-* GAPLAC_FUSED_TAIL: the serial tail's diagonal block and TRSM in one launch (the TRSM
-  workgroups wait on a flag the diagonal workgroup publishes; bitwise equal);
-* GAPLAC_PERSIST_M / _T / _Q: bulk updates on a capped grid whose workgroups loop over
-  the tiles (1000 applies it to every step; N = 9000 runs the 128x128 tile kernel so).
+* GAPLAC_PAIR_M / GAPLAC_PAIR_EXT / GAPLAC_BAND_TILES_M: paired bulk updates (every other
+  step the columns beyond the next band receive two super-panels at once; 1: whenever
+  possible), with or without the second band, bands as whole tiles or quadrants;
+* GAPLAC_SERIAL: everything on one stream.
 The settings are read when a context is created (gaplac_ctx_create).
 """
 import os
@@ -37,27 +29,17 @@ SCHEDULES = {
     "default": {},
     "serial_everything": {"GAPLAC_TAIL_S": "1000"},
     "no_serial_tail": {"GAPLAC_TAIL_S": "0"},
-    "narrow_tail_w1": {"GAPLAC_TAIL_S": "0", "GAPLAC_TAIL_M": "12", "GAPLAC_TAIL_W": "1"},
-    "narrow_tail_w2_then_serial": {"GAPLAC_TAIL_S": "4", "GAPLAC_TAIL_M": "14", "GAPLAC_TAIL_W": "2"},
     "plain_gram_grid": {"GAPLAC_GRAM_QUEUE": "0"},
     "gram_queue_1": {"GAPLAC_GRAM_QUEUE": "1"},
     "spw3_serial8": {"GAPLAC_SPW": "3", "GAPLAC_TAIL_S": "8"},
-    "persist_all": {"GAPLAC_PERSIST_M": "1000"},
-    "persist_all_t2_q3": {"GAPLAC_PERSIST_M": "1000", "GAPLAC_PERSIST_T": "2", "GAPLAC_PERSIST_Q": "3"},
-    "la_split_all": {"GAPLAC_LA_SPLIT_M": "1000", "GAPLAC_TAIL_S": "0"},
-    "la_split_persist": {"GAPLAC_LA_SPLIT_M": "1000", "GAPLAC_PERSIST_M": "1000"},
+    "spw1_no_tail": {"GAPLAC_SPW": "1", "GAPLAC_TAIL_S": "0"},
     "pair_all": {"GAPLAC_PAIR_M": "1"},
     "pair_band_whole_tiles": {"GAPLAC_PAIR_M": "1", "GAPLAC_BAND_TILES_M": "1"},
-    "pair_spare": {"GAPLAC_PAIR_M": "1", "GAPLAC_SPARE": "200"},
-    "no_pair_no_spare": {"GAPLAC_PAIR_M": "0", "GAPLAC_SPARE": "0"},
-    "fine_tail": {"GAPLAC_FINE_TAIL": "1"},
-    "quad_tail_all": {"GAPLAC_QUAD_TAIL": "100"},
-    "fused_tail": {"GAPLAC_FUSED_TAIL": "1"},
-    "fused_everything_serial": {"GAPLAC_FUSED_TAIL": "1", "GAPLAC_TAIL_S": "1000"},
+    "no_pair": {"GAPLAC_PAIR_M": "0"},
     "pair_no_ext": {"GAPLAC_PAIR_M": "1", "GAPLAC_PAIR_EXT": "0"},
     "pair_ext_spw3_whole": {"GAPLAC_PAIR_M": "1", "GAPLAC_PAIR_EXT": "1", "GAPLAC_SPW": "3", "GAPLAC_BAND_TILES_M": "1"},
-    "pair_no_tail_split_persist": {"GAPLAC_PAIR_M": "1", "GAPLAC_TAIL_S": "0", "GAPLAC_LA_SPLIT_M": "1000",
-                                   "GAPLAC_PERSIST_M": "1000"},
+    "pair_no_tail": {"GAPLAC_PAIR_M": "1", "GAPLAC_TAIL_S": "0"},
+    "serial_stream": {"GAPLAC_SERIAL": "1"},
 }
 SIZES = [1, 127, 129, 700, 2049, 3000, 9000]
 TERMS = [(SQEXP, 0, 1.5, 0), (OU, 0, 3.0, 1), (CAT, 1, 0.0, 2), (NOISE, -1, 1.0, 3)]
@@ -118,19 +100,3 @@ def test_serial_tail_reports_posdef_failure(ctxs):
         assert info[0] > 0, name
         infos.add(int(info[0]))
     assert infos == {1002}
-
-
-@pytest.mark.parametrize("N", [700, 3000, 9000])
-def test_fine_tail_bitwise_equal_to_quadrant_tail(ctxs, N):
-    X, v = inputs(N)
-    a = ctxs["default"].logpdf(X, TERMS, 0.1, v, full=True)
-    b = ctxs["fine_tail"].logpdf(X, TERMS, 0.1, v, full=True)
-    assert a == b
-
-
-@pytest.mark.parametrize("N", [1, 129, 700, 3000, 9000])
-def test_fused_tail_bitwise_equal(ctxs, N):
-    X, v = inputs(N)
-    a = ctxs["default"].logpdf(X, TERMS, 0.1, v, full=True)
-    for name in ("fused_tail", "fused_everything_serial"):
-        assert ctxs[name].logpdf(X, TERMS, 0.1, v, full=True) == a, name
