@@ -215,6 +215,7 @@ def main():
     # evaluation's panel chain with the other's bulk updates.
     two = None
     n4096 = None
+    n65536 = None
     if full_run and rank == 0:
         models = [terms_for(LENGTHSCALES[i % len(LENGTHSCALES)]) for i in range(8)]
         ctx.logpdf_batch(X, models[:2], CF.NOISE_VAR, v)
@@ -223,6 +224,7 @@ def main():
             ctx.logpdf_batch(X, models, CF.NOISE_VAR, v)
         two = 16 / (time.perf_counter() - tb)
         n4096 = measure_config1(ctx, torch)
+        n65536 = measure_config3_single(local_rank, torch)
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -280,6 +282,7 @@ def main():
         "last_logpdf": lp,
         "two_chains_evals_per_s": two,
         "n4096": n4096,
+        "n65536": n65536,
         "dist": dist_line,
     }
     if gram_alone:
@@ -332,6 +335,11 @@ def main():
         "cpu_baseline": cpu,
         "extra": extra,
     }
+    if dist_line is not None:
+        # a failed configs[3] line must not hide behind a good replicas headline
+        out["dist_ok"] = "error" not in dist_line
+        if not out["dist_ok"]:
+            print(f"bench: configs[3] distributed line FAILED: {dist_line['error']}", file=sys.stderr, flush=True)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -362,6 +370,40 @@ def measure_config1(ctx, torch, steps: int = 8):
     tf = flops / dt / 1e12
     return {"workload": f"BASELINE configs[1]: SqExp(:x; l in {list(CF.LENGTHSCALES_1)}), N={N}, noise 0.1",
             "evals_per_s": 1.0 / dt, "ms_per_eval": dt * 1e3, "achieved_tflops": round(tf, 3),
+            "roofline": {"bound": "mfma", "kernel": "whole evaluation (F = N^3/3 + N^2)", "achieved": round(tf, 3),
+                         "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / PEAK_F64_TFLOPS, 4)}}
+
+
+def measure_config3_single(local_rank: int, torch, steps: int = 2):
+    """BASELINE configs[3]'s workload (SqExp(:x; l=1.5), N=65536, seed 3) as ONE evaluation
+    on ONE GPU: the north_star's 64k point and the 1-GPU base of the configs[3]
+    strong-scaling curve. Its own context (34 GB workspace), freed afterwards."""
+    from gaplac_amd.backend import Context
+    x, v = CF.config3_inputs()
+    N = x.shape[0]
+    dx = torch.from_numpy(x).to("cuda")
+    dvv = torch.from_numpy(v).to("cuda")
+    c = Context(local_rank)
+    try:
+        def one():
+            return c.logpdf_device(N, 1, dx.data_ptr(), N, CF.CONFIG3_TERMS, CF.NOISE_VAR, dvv.data_ptr())
+
+        one()  # warmup: workspace, tile lists
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        lp = None
+        for _ in range(steps):
+            lp = one()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+    finally:
+        c.close()
+        del dx, dvv
+        torch.cuda.empty_cache()
+    flops = N ** 3 / 3.0 + N ** 2
+    tf = flops / dt / 1e12
+    return {"workload": f"BASELINE configs[3] workload on 1 GPU: SqExp(:x; l=1.5), N={N}, noise 0.1",
+            "evals_per_s": 1.0 / dt, "ms_per_eval": dt * 1e3, "steps": steps, "last_logpdf": lp,
             "roofline": {"bound": "mfma", "kernel": "whole evaluation (F = N^3/3 + N^2)", "achieved": round(tf, 3),
                          "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / PEAK_F64_TFLOPS, 4)}}
 

@@ -6,14 +6,36 @@ reached from CLI/src/mcmc.jl:35 (`fx ~ FiniteGP(GP(k), RowVecs(X), 0.1)`) and
 CLI/src/select.jl:43-50 (`logpdf(FiniteGP(gp, x, 0.1, obsdim=1), y)`). This module
 mirrors that surface: GP(kernel), FiniteGP(gp, X, noise), logpdf(fx, v) — and routes the
 evaluation through libgaplac_hip.so. There is no CPU fallback.
+
+The switch: the Julia glue gates its overloads on a flag that
+__init__ sets from GAPLAC_HIP at every package load; here the same variable is read at
+EVERY call (hip_enabled). Off, the Julia host falls through to AbstractGPs' own method;
+this twin has no such method (no CPU path in the product), so it raises BackendDisabled.
+Default on here, since nothing else could answer.
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 
 from . import backend
 from . import formula as F
 from . import kernels as K
+
+
+class BackendDisabled(RuntimeError):
+    """GAPLAC_HIP=0: the HIP backend is switched off (the Julia host would use AbstractGPs)."""
+
+
+def hip_enabled() -> bool:
+    """GAPLAC_HIP, read now (not at import): "0" turns the backend off."""
+    return os.environ.get("GAPLAC_HIP", "1") != "0"
+
+
+def _gate():
+    if not hip_enabled():
+        raise BackendDisabled("GAPLAC_HIP=0: HIP backend disabled; the Julia host falls back to AbstractGPs")
 
 
 class GP:
@@ -50,6 +72,7 @@ class FiniteGP:
 def logpdf(fx: FiniteGP, y, ctx: backend.Context | None = None, full: bool = False):
     """-(N log 2pi + logdet(C) + ||U^-T y||^2) / 2 on the GPU; raises
     backend.PosDefException(info) when C is not positive definite (cholesky check=true)."""
+    _gate()
     ctx = ctx or backend.default_context()
     y = np.asarray(y, dtype=np.float64)
     if y.shape[0] != len(fx):
@@ -61,6 +84,7 @@ def logpdf_and_gradient(fx: FiniteGP, y, ctx: backend.Context | None = None):
     """(logpdf, dlogpdf/dy, dlogpdf/dparam per lowered term, dlogpdf/dnoise) on the GPU:
     what ForwardDiff computes through AbstractGPs.logpdf in the reference's mcmc
     (CLI/src/mcmc.jl:31-41), as one analytic evaluation (gaplac_logpdf_grad)."""
+    _gate()
     ctx = ctx or backend.default_context()
     y = np.asarray(y, dtype=np.float64)
     if y.shape[0] != len(fx):
@@ -90,6 +114,7 @@ class PosteriorGP:
     def mean_and_var(self, x):
         """AbstractGPs.mean_and_var(f::PosteriorGP, x): posterior mean and marginal variance
         (latent: no observation noise) at the rows of x."""
+        _gate()
         ctx = self.ctx or backend.default_context()
         return ctx.posterior_mean_var(self.prior.x, self.prior.terms, self.prior.noise, self.y, self._xs(x))
 
@@ -114,6 +139,7 @@ def rand(fx: FiniteGP, z=None, rng=None, ctx: backend.Context | None = None):
     """rand(rng, fx) = cholesky(C).U' * randn(rng, N) for the zero-mean FiniteGP
     (CLI/src/sample.jl:25). The standard-normal draws stay on the host: pass z, or an rng
     (numpy Generator) to draw it."""
+    _gate()
     ctx = ctx or backend.default_context()
     if z is None:
         rng = rng if rng is not None else np.random.default_rng()
@@ -145,6 +171,7 @@ def select_formulae(f1: str, f2: str, table, noise: float = 0.1, ctx: backend.Co
     """CLI/src/select.jl:21-54 (`select --formulae`): logpdf of two formulas on the same
     data and the printed "Log2 Bayes" value, which is lp1 - lp2. Both models
     run through one batched call."""
+    _gate()
     ctx = ctx or backend.default_context()
     specs = [F.gp_spec(f1), F.gp_spec(f2)]
     if F.response(specs[0]) != F.response(specs[1]):

@@ -51,16 +51,22 @@ class GradMemo:
 
     def __init__(self):
         self.key = None
+        self.X = None
         self.v = None
         self.val = None
         self.calls = 0
 
     def __call__(self, ctx, X, terms, noise: float, v):
+        # keyed on the VALUES of X and v (copies kept and compared), never on a buffer
+        # address: an X modified in place, or a new X in a reused buffer, misses the memo
+        X = np.ascontiguousarray(X, dtype=np.float64)
         v = np.ascontiguousarray(v, dtype=np.float64)
-        key = (X.ctypes.data, X.shape, tuple(map(tuple, terms)), float(noise), hash(v.tobytes()))
-        if key != self.key or self.v is None or not np.array_equal(v, self.v):
+        key = (X.shape, tuple(map(tuple, terms)), float(noise))
+        hit = (key == self.key and self.v is not None and np.array_equal(v, self.v)
+               and np.array_equal(X, self.X))
+        if not hit:
             self.val = ctx.logpdf_grad(X, terms, noise, v)
-            self.key, self.v = key, v.copy()
+            self.key, self.X, self.v = key, X.copy(), v.copy()
             self.calls += 1
         return self.val
 

@@ -13,14 +13,17 @@ NUTS(0.65) does with it, in the unconstrained space Turing samples in:
   * the no-U-turn sampler with multinomial sampling over the trajectory (AdvancedHMC's
     NUTS{MultinomialTS, GeneralisedNoUTurn}; the classic end-point U-turn test here), max
     tree depth 10, divergence at an energy error above 1000;
-  * step size: the find-a-good-step-size heuristic from ε = 1, then Nesterov dual averaging
+  * step size: AdvancedHMC's find_good_stepsize (a doubling / halving crossing search
+    around acceptance 1/2 from ε = 0.1, then bisection into [1/4, 3/4]), then Nesterov dual averaging
     towards acceptance δ = 0.65 (γ = 0.05, t0 = 10, κ = 0.75) over n_adapts =
     min(samples ÷ 10, 1000) warm-up iterations (Turing's default), which are discarded.
     The metric stays the identity (Turing also adapts a diagonal metric in windows; that
     only changes efficiency, not the target distribution).
 
-Output columns follow MCMCChains' table: iteration, chain, ℓ, fx[1..N], lp (the log joint
-in the constrained space, Turing's :lp, which `select --chains` reads), n_steps, is_accept,
+Output columns follow MCMCChains' table: iteration, chain, ℓ, fx[1..N], lp (Turing's :lp,
+which `select --chains` reads: in Turing 0.21 / DynamicPPL 0.19 the HMC step stores the
+sampler's log density, i.e. the log joint in the LINKED space including the logit
+log-Jacobian, so lp == log_density), n_steps, is_accept,
 acceptance_rate, log_density, hamiltonian_energy, hamiltonian_energy_error,
 tree_depth, numerical_error, step_size, nom_step_size.
 """
@@ -149,25 +152,42 @@ def nuts_transition(f, cur: _State, eps: float, rng) -> Tuple[_State, Dict[str, 
     return _State(prop.theta, None, prop.logp, prop.grad, prop.lp), stats
 
 
-def find_good_stepsize(f, cur: _State, rng, eps: float = 1.0) -> float:
-    """Double / halve ε from 1 until the one-step acceptance crosses 1/2 (AdvancedHMC's
-    find_good_stepsize)."""
+def find_good_stepsize(f, cur: _State, rng, eps: float = 0.1, max_iters: int = 100) -> float:
+    """AdvancedHMC 0.3's find_good_stepsize (what Turing's NUTS(0.65) calls when its initial
+    ε is 0): from ε = 0.1, double (acceptance of one leapfrog step above 1/2) or halve it
+    until the acceptance crosses 1/2, then bisect between the two neighbours until the
+    acceptance lies in [1/4, 3/4]. Restated from the published algorithm (the package is
+    not vendored in the reference); the constants are AdvancedHMC's defaults."""
+    a_min, a_cross, a_max = 0.25, 0.5, 0.75
     r = rng.standard_normal(cur.theta.shape[0])
     s0 = _State(cur.theta, r, cur.logp, cur.grad, cur.lp)
     H0 = _energy(s0)
 
-    def logacc(e):
+    def dH(e):  # H - H' (exp of it is the MH acceptance ratio)
         s1 = _leapfrog(f, s0, e)
         return -(_energy(s1) - H0) if math.isfinite(s1.logp) else -math.inf
 
-    a = 1 if logacc(eps) > math.log(0.5) else -1
-    for _ in range(100):
-        e2 = eps * (2.0 ** a)
-        la = logacc(e2)
-        if (a == 1 and not la > math.log(0.5)) or (a == -1 and la > math.log(0.5)):
-            return e2 if a == -1 else eps
-        eps = e2
-    return eps
+    direction = 1 if dH(eps) > math.log(a_cross) else -1
+    eps2 = eps
+    for _ in range(max_iters):
+        eps2 = 2.0 * eps if direction == 1 else 0.5 * eps
+        d = dH(eps2)
+        if (direction == 1 and not d > math.log(a_cross)) or (direction == -1 and not d < math.log(a_cross)):
+            break
+        eps = eps2
+    lo, hi = (eps, eps2) if eps < eps2 else (eps2, eps)  # lo: high acceptance, hi: low
+    for _ in range(max_iters):
+        mid = 0.5 * (lo + hi)
+        d = dH(mid)
+        a = math.exp(min(d, 0.0)) if math.isfinite(d) else 0.0  # min(1, exp(dH))
+        if a > a_max or d > 0.0:
+            lo = mid
+        elif a < a_min:
+            hi = mid
+        else:
+            lo = mid
+            break
+    return lo
 
 
 class DualAveraging:
@@ -231,7 +251,7 @@ def sample(model, samples: int, seed: int = 0, delta: float = 0.65, n_adapts: Op
         cols["ℓ"].append(f.ell(cur.theta))
         for i in range(N):
             cols[f"fx[{i + 1}]"].append(float(cur.theta[1 + i]))
-        cols["lp"].append(cur.lp)
+        cols["lp"].append(cur.logp)  # Turing's :lp = the linked-space log density
         for k in ("n_steps", "is_accept", "acceptance_rate", "log_density", "hamiltonian_energy",
                   "hamiltonian_energy_error", "tree_depth", "numerical_error"):
             cols[k].append(st[k])

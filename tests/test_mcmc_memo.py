@@ -83,3 +83,17 @@ def test_ell_equal_one_drops_the_tied_terms_like_forwarddiff():
     terms = m.terms(1.0)
     _, _, rdp, _ = R.logpdf_grad(m.X, terms, 0.1, fx)
     assert dell == rdp[2]  # only the Linear(:x) intercept depends on ℓ at ℓ == 1
+
+
+def test_memo_keys_on_values_not_buffer_address():
+    # keyed on X.ctypes.data, an X modified in place returned a stale gradient
+    m, ctx, fx, tab = _model(N=60)
+    terms = m.terms(2.0)
+    X = m.X.copy()
+    a = m.memo(ctx, X, terms, 0.1, fx)
+    X[:, 0] *= 1.5  # same buffer, new values (a shift would leave a stationary kernel unchanged)
+    b = m.memo(ctx, X, terms, 0.1, fx)
+    assert ctx.calls == 2
+    assert not np.array_equal(a[1], b[1])
+    c = m.memo(ctx, X.copy(), terms, 0.1, fx)  # new buffer, same values: a hit
+    assert ctx.calls == 2 and c is b

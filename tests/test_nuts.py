@@ -70,3 +70,32 @@ def test_mcmc_model_chain_through_oracle_density(tmp_path):
     assert head[:3] == ["iteration", "chain", "ℓ"] and "lp" in head
     bayes, lp1, lp2 = select_chains(str(out), str(out))
     assert bayes == 0.0 and math.isfinite(lp1)
+
+
+def test_lp_column_is_the_linked_space_log_density():
+    # Turing 0.21 / DynamicPPL 0.19: the HMC step sets the VarInfo's logp to the sampler's
+    # log density, which in linked space includes the logit log-Jacobian, so :lp equals
+    # log_density on every draw (the column omitted the Jacobian)
+    chain = nuts.sample(_Gauss(2), 50, seed=1, n_adapts=10)
+    assert chain["lp"] == chain["log_density"]
+    f = nuts.Unconstrained(_Gauss(2))
+    for ell, a, b in zip(chain["ℓ"], chain["fx[1]"], chain["fx[2]"]):
+        theta = f.to_theta(ell, [a, b])
+        logp, _, lp_constrained = f(theta)
+        s = ell / 20.0
+        assert abs(logp - (lp_constrained + math.log(20.0 * s * (1.0 - s)))) <= 1e-9 * max(1.0, abs(logp))
+
+
+def test_find_good_stepsize_bisects_into_the_acceptance_band():
+    f = nuts.Unconstrained(_Gauss(3))
+    rng = np.random.default_rng(5)
+    theta = rng.uniform(-2, 2, 4)
+    logp, grad, lp = f(theta)
+    cur = nuts._State(theta, None, logp, grad, lp)
+    eps = nuts.find_good_stepsize(f, cur, np.random.default_rng(7))
+    # the final step size's one-step acceptance, from the same momentum draw
+    r = np.random.default_rng(7).standard_normal(4)
+    s0 = nuts._State(theta, r, logp, grad, lp)
+    s1 = nuts._leapfrog(f, s0, eps)
+    acc = min(1.0, math.exp(-(nuts._energy(s1) - nuts._energy(s0))))
+    assert 0.25 <= acc <= 1.0 and eps > 0.0
