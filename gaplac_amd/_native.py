@@ -84,6 +84,8 @@ class Stats(ctypes.Structure):
         ("cinv_launches", c_int64),
         ("cinv_ms", c_double),
         ("contract_ms", c_double),
+        ("tail_launches", c_int64),
+        ("tail_ms", c_double),
     ]
 
 

@@ -68,12 +68,21 @@ struct gaplac_ctx {
     bool dry = false;     // host-only walk of the schedule (gaplac_plan_check): no HIP calls
     int spw = 4;          // GAPLAC_SPW: super-panel width in 128-column tiles (bulk K = 128 spw)
     int tail_s = 32;      // GAPLAC_TAIL_S: the last ~tail_s tile columns run serially on one stream
+                          //   (default 48 with the persistent tail, 32 without)
     int pair_ext = 1;     // GAPLAC_PAIR_EXT: 1 = a deferring step also updates the band after next
     int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
     int pair_m = 40;      // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
     int ncu = 256;        // compute units of the device
     int gram_queue = 2;   // GAPLAC_GRAM_QUEUE: second Gram launch as a work queue of this many
                           //   workgroups per CU, leaving room for the panel chain (0 = plain grid)
+    bool tailk = true;    // GAPLAC_TAILK: the serial tail as one persistent dataflow launch (tail_kernel)
+    TailCtl* tctl = nullptr;     // its completion counters (zeroed per launch)
+    uint32_t* ttasks = nullptr;  // its task list for ttasks_T tile columns
+    size_t ttasks_elems = 0;
+    int ttasks_T = -1, ttasks_n = 0;
+    std::string ttrace_path;     // GAPLAC_TAIL_TRACE: append per-task times of every tail launch here
+    unsigned long long* ttrace = nullptr;
+    size_t ttrace_elems = 0;
     gaplac_stats stats{};
     struct Slot {
         int kind;  // 0 bulk syrk, 1 gram, 2 diag, 4 trsm, 5 column update, 6 small bulk
@@ -301,6 +310,10 @@ int accumulate_slots(gaplac_ctx* ctx, const std::vector<gaplac_ctx::Slot>& slots
             case 9:
                 ctx->stats.contract_ms += ms;
                 break;
+            case 10:
+                ctx->stats.tail_ms += ms;
+                ctx->stats.tail_launches += 1;
+                break;
             case 1:
                 ctx->stats.gram_ms += ms;
                 ctx->stats.gram_bytes += slots[i].work;
@@ -394,6 +407,9 @@ void extra_rows_step(gaplac_ctx* ctx, hipStream_t sm, int64_t lda, int nt, int p
 // most tail_s tile columns after it; those columns are factored by serial_tail().
 static std::vector<int> superpanel_starts(const gaplac_ctx* ctx, int nt) {
     std::vector<int> sp{0};
+    // a matrix the persistent tail covers whole (plain logpdf, at most TAIL_TMAX tile
+    // columns, within tail_s): no super-panel at all, every column in the tail kernel
+    if (ctx->xr_mode == 0 && ctx->tailk && nt <= TAIL_TMAX && nt <= ctx->tail_s) return sp;
     int c = 0;
     while (c < nt) {
         if (ctx->xr_mode == 0 && ctx->tail_s > 0 && c > 0 && nt - c <= ctx->tail_s) break;
@@ -431,10 +447,12 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     const int W = ctx->spw;
     const std::vector<int> spc = superpanel_starts(ctx, nt);
     const int nsp = (int)spc.size() - 1;
-    HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_gram, 0));  // first W tile columns built
     int frc;
-    if ((frc = factor_superpanel(ctx, sp, N, lda, nt, spc[0], spc[1]))) return frc;
-    HIPQ(ctx, hipEventRecord(ctx->ev_P[0], sp));
+    if (nsp > 0) {
+        HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_gram, 0));  // first W tile columns built
+        if ((frc = factor_superpanel(ctx, sp, N, lda, nt, spc[0], spc[1]))) return frc;
+        HIPQ(ctx, hipEventRecord(ctx->ev_P[0], sp));
+    }
     // bulk trailing update of the triangle of tile columns >= j0 with the panel pn (K = kd)
     auto bulk_tri = [&](int j0, const Panel& pn, int kdep) -> int {
         if (j0 >= nt) return 0;
@@ -534,7 +552,34 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             extra_rows_step(ctx, sx, lda, nt, p);
         }
     }
-    if (spc[(size_t)nsp] < nt) serial_tail(ctx, sm, N, lda, nt, spc[(size_t)nsp]);
+    if (spc[(size_t)nsp] < nt) {
+        const int ts = spc[(size_t)nsp], T = nt - ts;
+        if (ctx->tailk && T <= TAIL_TMAX) {
+            // the tail as one persistent dataflow launch
+            if (ctx->ttasks_T != T && !ctx->dry) {
+                std::vector<uint32_t> host;
+                build_tail_tasks(T, host);
+                int rc;
+                if ((rc = ensure(ctx, &ctx->ttasks, &ctx->ttasks_elems, host.size()))) return rc;
+                HIPCK(ctx, hipMemcpy(ctx->ttasks, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+                ctx->ttasks_T = T;
+                ctx->ttasks_n = (int)host.size();
+            }
+            if (!ctx->tctl && !ctx->dry)
+                HIPCK(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->tctl), sizeof(TailCtl)));
+            HIPQ(ctx, hipMemsetAsync(ctx->tctl, 0, sizeof(TailCtl), sm));
+            const int nts = ctx->dry ? (int)(T * (T + 1) * (T + 2) / 6 + 3 * T * T) : ctx->ttasks_n;
+            if (!ctx->ttrace_path.empty() && !ctx->dry) {
+                int rc;
+                if ((rc = ensure(ctx, &ctx->ttrace, &ctx->ttrace_elems, 3 * (size_t)nts))) return rc;
+            }
+            TailArgs ta{ctx->A, lda, N, ts, T, ctx->Dinv, ctx->dres, ctx->tctl, ctx->ttasks, nts,
+                        ctx->ttrace_path.empty() ? nullptr : ctx->ttrace};
+            launch_tail(sm, ta, std::min(ctx->ncu, nts), slot(ctx, 10, 0));
+        } else {
+            serial_tail(ctx, sm, N, lda, nt, ts);
+        }
+    }
     if (ctx->xr_mode && !ctx->serial) {
         HIPQ(ctx, hipEventRecord(ctx->ev_xdone, ctx->s_extra));
         HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_xdone, 0));
@@ -728,6 +773,7 @@ int eval_enqueue(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp) {
 int eval_wait(gaplac_ctx* ctx, EvalResult* out) {
     HIPCK(ctx, hipStreamSynchronize(ctx->s_main));
     *out = *ctx->hres;
+    if (out->err) return set_err(ctx, GAPLAC_E_HIP, "in-kernel wait expired (code %u)", out->err);
     return 0;
 }
 
@@ -757,6 +803,19 @@ int eval_device(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp, EvalR
     if (rc) return rc;
     HIPCK(ctx, hipStreamSynchronize(ctx->s_main));
     *out = *ctx->hres;
+    if (out->err) return set_err(ctx, GAPLAC_E_HIP, "in-kernel wait expired (code %u)", out->err);
+    if (!ctx->ttrace_path.empty() && ctx->ttrace && ctx->ttasks_n > 0) {  // diagnostics: task timeline
+        std::vector<unsigned long long> tr(3 * (size_t)ctx->ttasks_n);
+        std::vector<uint32_t> tk((size_t)ctx->ttasks_n);
+        HIPCK(ctx, hipMemcpy(tr.data(), ctx->ttrace, tr.size() * 8, hipMemcpyDeviceToHost));
+        HIPCK(ctx, hipMemcpy(tk.data(), ctx->ttasks, tk.size() * 4, hipMemcpyDeviceToHost));
+        if (FILE* f = std::fopen(ctx->ttrace_path.c_str(), "a")) {
+            std::fprintf(f, "# N=%lld T=%d tasks=%d\n", (long long)N, ctx->ttasks_T, ctx->ttasks_n);
+            for (size_t i = 0; i < tk.size(); ++i)
+                std::fprintf(f, "%zu %u %llu %llu %llu\n", i, tk[i], tr[3 * i], tr[3 * i + 1], tr[3 * i + 2]);
+            std::fclose(f);
+        }
+    }
     if (prof) {
         rc = accumulate_slots(ctx, ctx->slots);
         ctx->slots.clear();
@@ -939,6 +998,10 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_PAIR_EXT")) ctx->pair_ext = std::max(0, std::min(1, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BAND_TILES_M")) ctx->band_tiles_m = std::max(1, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
+    if (const char* s = std::getenv("GAPLAC_TAILK")) ctx->tailk = s[0] != '0';
+    if (ctx->tailk) ctx->tail_s = 48;  // the persistent tail (A/B at N = 16384: 48 < 32 < 64 columns)
+    if (const char* s = std::getenv("GAPLAC_TAIL_S")) ctx->tail_s = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_TAIL_TRACE")) ctx->ttrace_path = s;  // diagnostics
     auto fail = [&](const char* what, hipError_t e) {
         std::fprintf(stderr, "gaplac_ctx_create: %s: %s\n", what, hipGetErrorString(e));
         gaplac_ctx_destroy(ctx);
@@ -1034,6 +1097,9 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     if (ctx->dgp) (void)hipFree(ctx->dgp);
     if (ctx->hgp) (void)hipHostFree(ctx->hgp);
     if (ctx->glist) (void)hipFree(ctx->glist);
+    if (ctx->tctl) (void)hipFree(ctx->tctl);
+    if (ctx->ttasks) (void)hipFree(ctx->ttasks);
+    if (ctx->ttrace) (void)hipFree(ctx->ttrace);
     if (ctx->dres) (void)hipFree(ctx->dres);
     if (ctx->dtp) (void)hipFree(ctx->dtp);
     if (ctx->htp) (void)hipHostFree(ctx->htp);

@@ -466,6 +466,7 @@ int gaplac_dist_finish(gaplac_dist* d, double* out_logdet, double* out_quad, int
     DCK(d, hipStreamSynchronize(d->s_panel));
     DCK(d, hipStreamSynchronize(d->s_comm));
     const EvalResult r = *d->hres;
+    if (r.err) return derr(d, GAPLAC_E_HIP, "in-kernel wait expired (code %u)", r.err);
     if (out_logdet) *out_logdet = r.logdet;
     if (out_quad) *out_quad = r.quad;
     if (out_info) *out_info = r.info == ~0ull ? 0 : (int64_t)r.info;

@@ -33,6 +33,8 @@ struct EvalResult {
     double logdet;
     double quad;
     unsigned long long info;  // min over failing pivots of (j+1); ULLONG_MAX = none
+    unsigned err;             // nonzero: a bounded in-kernel wait expired (the host returns GAPLAC_E_HIP)
+    unsigned err_pad;
     double part[2][REDUCE_BLOCKS];  // per-workgroup partial sums of the reduction
     unsigned gram_ticket;           // work queue of the second Gram launch (zeroed per eval)
 };
@@ -78,6 +80,30 @@ struct BulkArgs {
     int max_r = -1, max_c = -1;  // largest lo16 / hi16 list entry (-1: an m x m triangle list)
     int whole = 0;    // 1: a band list as 128x128 tile workgroups (tile_band_kernel), never quadrants
 };
+
+// Persistent tail (gaplac_kernels.hip tail_kernel): completion counters of
+// the tile tasks of the last T <= TAIL_TMAX tile columns, zeroed before every launch.
+constexpr int TAIL_TMAX = 64;
+struct TailCtl {
+    unsigned head;  // dequeue counter
+    unsigned err;   // an expired wait
+    unsigned ddone[TAIL_TMAX];                // D(k) finished
+    unsigned sdone[TAIL_TMAX * TAIL_TMAX];    // S(i,k) finished ([i][k], relative tile indices)
+    unsigned units[TAIL_TMAX * TAIL_TMAX];    // tile (i,j): update units applied (4 per column, 3 on the diagonal)
+};
+struct TailArgs {
+    double* A;
+    int64_t lda, N;
+    int ts, T;  // tile columns ts .. ts+T-1
+    double* Dinv;
+    EvalResult* res;
+    TailCtl* ctl;
+    const uint32_t* tasks;
+    int ntasks;
+    unsigned long long* trace;  // diagnostics (GAPLAC_TAIL_TRACE): per task dequeue / start / end times, or nullptr
+};
+void build_tail_tasks(int T, std::vector<uint32_t>& out);
+void launch_tail(hipStream_t s, const TailArgs& a, int grid, KTime* kt);
 
 // Host-side footprint guard. Before launching, every launcher computes the
 // element range [p + lo, p + hi) its grid will touch in the column storage it is given

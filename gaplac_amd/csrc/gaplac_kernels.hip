@@ -783,14 +783,430 @@ __device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ Ag, 
 }
 
 
+// ---------------------------------------------------------------------------------
+// Global accesses through a buffer resource over a wave-uniform base with a cache policy:
+// AUX = 0 plain, AUX = GM_SC1 (16) device-coherent "sc1" loads / write-through stores.
+// The persistent tail kernel (tail_kernel) hands tiles between workgroups on different
+// XCDs with sc1 stores + a flag and sc1 loads (MI355X_MICROARCH.md, "Valid forms",
+// table row 1); the stand-alone kernels use AUX = 0. Offsets are in doubles, < 2^28.
+// ---------------------------------------------------------------------------------
+constexpr int GM_SC1 = 16;
+// threadIdx.x through an opaque copy: in the persistent kernel nothing derived from it is
+// hoisted out of the task loop (LICM would keep every body's addresses live: spills)
+__device__ __forceinline__ int otid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+typedef unsigned gm_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned gm_u32x4 __attribute__((ext_vector_type(4)));
+template <int AUX>
+struct Gm {
+    __amdgpu_buffer_rsrc_t r;
+    __device__ __forceinline__ explicit Gm(const void* base) {
+        const uint64_t b = (uint64_t)base;
+        const uint64_t u = ((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) << 32) |
+                           (uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)b);
+        r = __builtin_amdgcn_make_buffer_rsrc((void*)u, 0, 0x7fffffff, 0x00020000);
+    }
+    __device__ __forceinline__ double ld(uint32_t i) const {
+        const gm_u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, i * 8u, 0, AUX);
+        double d;
+        __builtin_memcpy(&d, &v, 8);
+        return d;
+    }
+    __device__ __forceinline__ double2 ld2(uint32_t i) const {
+        const gm_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, i * 8u, 0, AUX);
+        double2 d;
+        __builtin_memcpy(&d, &v, 16);
+        return d;
+    }
+    __device__ __forceinline__ void st(uint32_t i, double d) const {
+        gm_u32x2 v;
+        __builtin_memcpy(&v, &d, 8);
+        __builtin_amdgcn_raw_buffer_store_b64(v, r, i * 8u, 0, AUX);
+    }
+    __device__ __forceinline__ void st2(uint32_t i, double2 d) const {
+        gm_u32x4 v;
+        __builtin_memcpy(&v, &d, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, i * 8u, 0, AUX);
+    }
+};
+
+// ---------------------------------------------------------------------------------
+// Diagonal block, round 3 (potrf_diag2_body): the same blocked right-looking structure
+// with 16-column panels, but the panel sweep is split over two waves and scheduled around
+// its dependency chain (measured on gfx950, one wave alone: dependent v_fma_f64 10 cycles,
+// v_rsq_f64 17, v_readlane of a double ~18 latency / ~16 issue, independent fp64 VALU
+// ~4.9 cycles issue; tools/lat_chain_probe.hip, tools/issue_probe.hip).
+//
+// Wave 0 ("A") holds rows 16s .. 16s+63 of panel s, one row per lane, and runs the pivot
+// chain. Per column c the chain is
+//   pivot -> rsq -> t = p y -> e = 1 - t y -> c = 1/2 + 3/8 e -> rd = y + y e c
+//         -> l = v rd -> readlane(l, c+1) -> v[c+1] -= l * ln -> readlane(v[c+1], c+1)
+// and everything else is taken off it: column c+1 receives columns c-2 and c-1 at the top
+// of iteration c (in the shadow of the rsq), columns c+2..15 receive column c-2 ("2-deep
+// deferral"; its L values come from an LDS broadcast written two iterations earlier, so
+// the LDS latency is never waited for), and those independent FMAs are placed between the
+// chain's dependent instructions by scheduling barriers.
+// Wave 1 ("B", panels 0-3) holds rows 16s+64 .. 127 and consumes each column as wave A
+// publishes it (L values of the 16 diagonal rows + rd, flagged per column in LDS).
+// Waves 2-3 (and wave 1 from panel 4 on) apply panel s-1 to the trailing block columns
+// and invert the finished 16x16 diagonal sub-blocks (Dinv) where the sweep leaves slack.
+// Results agree with the round-2 kernel to rounding (different but fixed summation order);
+// pivots of padding columns are 1, a pivot <= 0 records info (OpenBLAS potf2's test).
+// ---------------------------------------------------------------------------------
+// LDS: the small buffers first (their addresses fit the 16-bit DS offset), then the block.
+constexpr int DIAG2_COLBUF = 16 * 64;  // colbuf[c * 64 + lane]: column c's record (diag2_sweep_a)
+constexpr int DIAG2_SMEM = DIAG2_COLBUF + NB + NPK * 256;  // colbuf, rdiag, Ab (doubles)
+
+#define SB() __builtin_amdgcn_sched_barrier(0)
+#define PIN(x) asm volatile("" : "+v"(x))
+
+// Wave A's sweep of panel s (rows 16s + lane). Per column the published 16-lane record
+// colbuf[c * 64 + 0..15] holds L(16s + r, 16s + c) for r > c and rd_c = 1/L_cc in slot c;
+// slot c doubles as the record's flag (reset to -1 before the panel; rd is never -1): the
+// record is one ds_write_b64 whose lanes 0-15 form one LDS lane group, written in one cycle.
+__device__ __forceinline__ void diag2_sweep_a(double* Ab, double* colbuf, int s, int lane, int64_t gcol0, int64_t N,
+                                              EvalResult* res) {
+    asm volatile("" : "+v"(lane));
+    const int R0 = 16 * s;
+    const int row = R0 + lane;
+    const bool live = row < NB;
+    double* blk = Ab + bidx(live ? (row >> 4) : s, s) * 256;
+    const int rr = row & 15;
+    double v[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v[c] = blk[c * 16 + rr];
+    const int64_t npiv64 = N - (gcol0 + R0);  // columns >= npiv are padding (unit pivots)
+    const int npiv = (int)(npiv64 < 0 ? 0 : (npiv64 > 16 ? 16 : npiv64));
+    const unsigned padmask = (0xffffu << npiv) & 0xffffu;
+    double lcA[16], lcB[16];  // L(R0 + c2, c - 2) / L(R0 + c2, c - 1), uniform
+#pragma unroll
+    for (int c = 0; c < 16; ++c) lcA[c] = lcB[c] = 0.0;
+    double k375 = 0.375;  // kept in a VGPR (not an inline constant)
+    PIN(k375);
+    double ln2 = 0.0;  // L(R0 + c + 1, c - 1), uniform
+    double mypiv = 1.0;
+    double piv = readlane_d(v[0], 0);
+    SB();
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        // fillers: column c-2 into columns c+2 .. 15, pinned where they are placed
+        auto fill = [&](int k) {
+            const int c2 = c + 2 + k;
+            if (c >= 2 && c2 < 16) {
+                v[c2] = fma(-v[c - 2], lcA[c2], v[c2]);
+                PIN(v[c2]);
+            }
+        };
+        const bool pad = (padmask >> c) & 1u;
+        const double p = pad ? 1.0 : piv;
+        // G1: rsq; column c+1 gets columns c-2 and c-1; LDS reads of column c-1's L values
+        const double y = __builtin_amdgcn_rsq(p);
+        mypiv = lane == c ? v[c] : mypiv;  // the non-PD test runs after the sweep
+        if (c >= 1) {
+#pragma unroll
+            for (int c2 = c + 2; c2 < 16; ++c2) lcB[c2] = colbuf[(c - 1) * 64 + c2];
+        }
+        if (c >= 2 && c + 1 < 16) v[c + 1] = fma(-v[c - 2], lcA[c + 1], v[c + 1]);
+        if (c >= 1 && c + 1 < 16) {
+            v[c + 1] = fma(-v[c - 1], ln2, v[c + 1]);
+            PIN(v[c + 1]);
+        }
+        fill(0);
+        SB();
+        const double t = p * y;  // G2
+        fill(1);
+        fill(2);
+        SB();
+        const double e = fma(-t, y, 1.0);  // G3
+        fill(3);
+        fill(4);
+        SB();
+        const double cc = fma(e, k375, 0.5);  // G4
+        const double ye = y * e;
+        fill(5);
+        SB();
+        const double rd = fma(ye, cc, y);  // G5: 1/sqrt(p), <= 1 ulp
+        fill(6);
+        fill(7);
+        SB();
+        // G6: scale column c. The diagonal lane's own value is its pivot, so it becomes
+        // p * rd = sqrt(p) (padding columns: fixed to 1 at the write-back); lanes above the
+        // diagonal get junk * rd, never read, zeroed at the write-back.
+        v[c] = v[c] * rd;
+        fill(8);
+        SB();
+        // G7: the two readlanes of the chain, then the column's record
+        double ln = 0.0, ln2n = 0.0;
+        if (c + 1 < 16) ln = readlane_d(v[c], c + 1);
+        if (c + 2 < 16) ln2n = readlane_d(v[c], c + 2);
+        colbuf[c * 64 + lane] = lane == c ? rd : v[c];
+        fill(9);
+        fill(10);
+        SB();
+        if (c + 1 < 16) v[c + 1] = fma(-v[c], ln, v[c + 1]);  // G8
+        fill(11);
+        SB();
+        if (c + 1 < 16) piv = readlane_d(v[c + 1], c + 1);  // G9
+        fill(12);
+        ln2 = ln2n;
+#pragma unroll
+        for (int c2 = 0; c2 < 16; ++c2) lcA[c2] = lcB[c2];
+        SB();
+    }
+    // OpenBLAS potf2 (the reference's dpotrf, 0.3.20) tests ajj <= 0 only: a NaN pivot is
+    // not reported and propagates to a NaN logpdf, as in the reference
+    const unsigned long long badm = __ballot(lane < 16 && !((padmask >> lane) & 1u) && mypiv <= 0.0);
+    if (badm && lane == 0) atomicMin(&res->info, (unsigned long long)(gcol0 + R0 + __builtin_ctzll(badm) + 1));
+    if (live) {
+        const bool padlane = lane < 16 && ((padmask >> lane) & 1u);
+#pragma unroll
+        for (int c = 0; c < 16; ++c)  // zero the diagonal block's upper part, unit padding pivots
+            blk[c * 16 + rr] = lane > c ? v[c] : (lane == c ? (padlane ? 1.0 : v[c]) : 0.0);
+    }
+}
+
+// Wave B's rows of panel s (rows 16s + 64 + lane, s < 4): consumes wave A's records. The
+// flag of column c+1 is read while column c is computed; its L values after the flag.
+__device__ __forceinline__ void diag2_sweep_b(double* Ab, double* colbuf, int s, int lane, EvalResult* res) {
+    asm volatile("" : "+v"(lane));
+    const int row = 16 * s + 64 + lane;
+    const bool live = row < NB;
+    double* blk = Ab + bidx(live ? (row >> 4) : NDB - 1, s) * 256;
+    const int rr = row & 15;
+    double v[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v[c] = blk[c * 16 + rr];
+    bool timeout = false;
+    double fl = __hip_atomic_load(&colbuf[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        // bounded wait for wave A (same workgroup: it never waits for this wave)
+        for (int it = 0; fl == -1.0 && it < (1 << 20); ++it) {
+            __builtin_amdgcn_s_sleep(1);
+            fl = __hip_atomic_load(&colbuf[c * 64 + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (fl == -1.0) {
+            timeout = true;
+            fl = __builtin_nan("");
+        }
+        const double rd = fl;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the record's values after its flag
+        double lc[16];
+#pragma unroll
+        for (int c2 = c + 1; c2 < 16; ++c2) lc[c2] = colbuf[c * 64 + c2];
+        if (c + 1 < 16) fl = __hip_atomic_load(&colbuf[(c + 1) * 64 + c + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const double l = v[c] * rd;
+        v[c] = l;
+#pragma unroll
+        for (int c2 = c + 1; c2 < 16; ++c2) v[c2] = fma(-l, lc[c2], v[c2]);
+    }
+    if (timeout && lane == 0) atomicOr(&res->err, 1u);
+    if (live) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) blk[c * 16 + rr] = v[c];
+    }
+}
+
+// Dinv_s = L_ss^{-1} (column-major 16x16 into global): lane j < 16 solves L x = e_j
+// right-looking (x[m] final, then every later row updated with it).
+template <int AUX>
+__device__ __forceinline__ void diag2_dinv(const double* Ab, double* __restrict__ Dinv, const double* rdiag, int s,
+                                           int lane, double* Dl = nullptr) {
+    const double* Ls = Ab + bidx(s, s) * 256;  // L(r, m) = Ls[m * 16 + r]
+    asm volatile("" : "+v"(lane));
+    const int j = lane & 15;
+    double x[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x[r] = r == j ? 1.0 : 0.0;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        x[m] *= rdiag[16 * s + m];
+#pragma unroll
+        for (int r = m + 1; r < 16; ++r) x[r] = fma(-Ls[m * 16 + r], x[m], x[r]);
+    }
+    const Gm<AUX> g(Dinv);
+    if (lane < 16) {
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) g.st2((uint32_t)(s * 256 + j * 16 + r), make_double2(x[r], x[r + 1]));
+        if (Dl) {  // LDS copy for a TRSM in the same workgroup (tail_kernel)
+#pragma unroll
+            for (int r = 0; r < 16; r += 2)
+                *reinterpret_cast<double2*>(&Dl[s * 256 + j * 16 + r]) = make_double2(x[r], x[r + 1]);
+        }
+    }
+}
+
+// Trailing blocks (I, J), s+1 <= J <= I <= 7, with panel s-1: tasks t = first, first+step, ...
+__device__ __forceinline__ void diag2_trailing(double* Ab, int s, int first, int step, int lane) {
+    const int ntr = (NDB - 1 - s) * (NDB - s) / 2;
+    auto tile_of = [&](int task, int& I, int& J) {
+        int rem = task;
+        J = s + 1;
+        while (rem >= NDB - J) {
+            rem -= NDB - J;
+            ++J;
+        }
+        I = J + rem;
+    };
+    int task = first;
+    for (; task + step < ntr; task += 2 * step) {
+        int I1, J1, I2, J2;
+        tile_of(task, I1, J1);
+        tile_of(task + step, I2, J2);
+        dblk_update2(Ab, I1, J1, I2, J2, s - 1, lane);
+    }
+    if (task < ntr) {
+        int I, J;
+        tile_of(task, I, J);
+        dblk_update(Ab, I, J, s - 1, lane);
+    }
+}
+
+// Block m of the 28 below-and-right-of-column-0 blocks of the 8x8 block triangle (J >= 1).
+__device__ __forceinline__ void diag2_block_of(int m, int& I, int& J) {
+    J = 1;
+    while (m >= NDB - J) {
+        m -= NDB - J;
+        ++J;
+    }
+    I = J + m;
+}
+
+// Store block column s of L (blocks (I, s), I = s..7) to global, pairs of rows: every
+// 16-row column segment (one 128-byte line) by 8 consecutive lanes of one instruction; the
+// diagonal 16x16 block's upper part goes out as the zeros sweep A left in LDS. Threads
+// tt = 0 .. nthr-1 (a multiple of 64) of the storing waves.
+template <int AUX>
+__device__ __forceinline__ void diag2_store_column(const double* Ab, double* Ag, int64_t lda, int s, int tt, int nthr) {
+    const int npairs = (NDB - s) * 128;
+    const Gm<AUX> g(Ag);
+    for (int q = tt; q < npairs; q += nthr) {
+        const int I = s + (q >> 7), pr = q & 127;
+        const int c = pr >> 3, r = 2 * (pr & 7);
+        const double2 x = *reinterpret_cast<const double2*>(&Ab[bidx(I, s) * 256 + c * 16 + r]);
+        g.st2((uint32_t)((int64_t)(16 * s + c) * lda + 16 * I + r), x);
+    }
+}
+
+// 512 threads: wave 0 = A (the pivot chain), wave 1 = B (rows 64+ of panels 0-3), waves 2-7
+// the trailing updates, the stores of finished block columns and (wave 7) the inverses.
+// Waves w and w + 4 share a SIMD, so every SIMD's matrix pipe takes trailing work.
+template <int AUX>
+__device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restrict__ Ag, int64_t lda, int64_t N,
+                                                 int64_t g0, double* __restrict__ Dinv, EvalResult* __restrict__ res,
+                                                 double* Dl = nullptr) {
+    double* colbuf = smem;
+    double* rdiag = colbuf + DIAG2_COLBUF;
+    double* Ab = rdiag + NB;
+    const int t = otid(), wave = t >> 6, lane = t & 63;
+    // the chain first (wave-uniform branches: s_setprio takes an immediate)
+    if (wave == 0) __builtin_amdgcn_s_setprio(3);
+    else if (wave == 1) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(1);
+    STAMP(20);
+    // Load: block column 0 by everyone first (panel 0 needs it), the other 28 blocks by
+    // waves 2-7, written to LDS while panel 0 is swept.
+    double2 rest[10];
+    const int tt = t - 128;  // waves 2-7: 0 .. 383
+    {
+        const Gm<AUX> g(Ag);
+        double2 col0[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int q = t + 512 * i, I = q >> 7, pr = q & 127, c = pr >> 3, r = 2 * (pr & 7);
+            col0[i] = g.ld2((uint32_t)((int64_t)c * lda + 16 * I + r));
+        }
+        if (wave >= 2) {
+#pragma unroll
+            for (int i = 0; i < 10; ++i) {
+                const int q = tt + 384 * i;
+                if (q < 28 * 128) {
+                    int I, J;
+                    diag2_block_of(q >> 7, I, J);
+                    const int pr = q & 127, c = pr >> 3, r = 2 * (pr & 7);
+                    rest[i] = g.ld2((uint32_t)((int64_t)(16 * J + c) * lda + 16 * I + r));
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int q = t + 512 * i, I = q >> 7, pr = q & 127;
+            *reinterpret_cast<double2*>(&Ab[bidx(I, 0) * 256 + 2 * pr]) = col0[i];
+        }
+    }
+    if (wave == 3 && lane < 16) colbuf[lane * 64 + lane] = -1.0;  // the records' flags
+    // a barrier that does not wait for the other blocks' loads (__syncthreads would)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    STAMP(0);
+    for (int s = 0; s < NDB; ++s) {
+        if (s >= 1) {
+            // phase 1: panel s-1 into block column s (the diagonal block first, on wave 0)
+            for (int I = s + wave; I < NDB; I += 8) dblk_update(Ab, I, s, s - 1, lane);
+            if (wave == 3 && lane < 16) {
+                rdiag[16 * (s - 1) + lane] = colbuf[lane * 64 + lane];  // rd of panel s-1's columns
+                colbuf[lane * 64 + lane] = -1.0;                        // the records' flags
+            }
+            __syncthreads();
+        }
+        STAMP(1 + 2 * s);
+        // phase 2
+        if (wave == 0) {
+            diag2_sweep_a(Ab, colbuf, s, lane, g0, N, res);
+        } else if (wave == 1 && s < 4) {
+            diag2_sweep_b(Ab, colbuf, s, lane, res);
+        } else {
+            if (s == 0 && wave >= 2) {  // the rest of the block into LDS
+#pragma unroll
+                for (int i = 0; i < 10; ++i) {
+                    const int q = tt + 384 * i;
+                    if (q < 28 * 128) {
+                        int I, J;
+                        diag2_block_of(q >> 7, I, J);
+                        *reinterpret_cast<double2*>(&Ab[bidx(I, J) * 256 + 2 * (q & 127)]) = rest[i];
+                    }
+                }
+            }
+            if (s >= 1) {
+                // wave 4 shares wave A's SIMD: it only stores and inverts (light), the
+                // trailing blocks go to waves 2, 3, 5, 6, 7 (and 1 from panel 4 on)
+                if (wave >= 2) diag2_store_column<AUX>(Ab, Ag, lda, s - 1, t - 128, 384);
+                if (wave == 4) {
+                    diag2_dinv<AUX>(Ab, Dinv, rdiag, s - 1, lane, Dl);
+                } else {
+                    const int w = wave == 1 ? 0 : (s < 4 ? 0 : 1) + (wave < 4 ? wave - 2 : wave - 3);
+                    diag2_trailing(Ab, s, w, s < 4 ? 5 : 6, lane);
+                }
+            }
+        }
+        if (wave == 0) STAMP(2 + 2 * s);
+        STAMPT(64, 29 + s);
+        STAMPT(128, 21 + s);
+        __syncthreads();
+    }
+    if (wave == 3 && lane < 16) rdiag[16 * (NDB - 1) + lane] = colbuf[lane * 64 + lane];
+    __syncthreads();
+    STAMP(17);
+    if (wave == 4) diag2_dinv<AUX>(Ab, Dinv, rdiag, NDB - 1, lane, Dl);
+    STAMP(18);
+    if (wave != 4) diag2_store_column<AUX>(Ab, Ag, lda, NDB - 1, wave < 4 ? t : t - 64, 448);
+    STAMP(19);
+}
+#undef SB
+#undef PIN
+
 // Ag: the diagonal block (global rows/cols g0 .. g0+127) in its storage, leading dim lda.
-__global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ Ag, int64_t lda,
+__global__ __launch_bounds__(512) void potrf_diag_kernel(double* __restrict__ Ag, int64_t lda,
                                                          int64_t N, int64_t g0,
                                                          double* __restrict__ Dinv,
                                                          EvalResult* __restrict__ res,
                                                          KTime* __restrict__ kt) {
+    __shared__ double smem[DIAG2_SMEM];
     kt_begin(kt);
-    potrf_diag_kernel_body(Ag, lda, N, g0, Dinv, res);
+    potrf_diag2_body<0>(smem, Ag, lda, N, g0, Dinv, res);
     kt_end(kt);
 }
 
@@ -1267,6 +1683,7 @@ __global__ void init_result_kernel(EvalResult* res) {
     res->quad = 0.0;
     res->info = ~0ull;
     res->gram_ticket = 0u;
+    res->err = 0u;
 }
 
 // ---------------------------------------------------------------------------------
@@ -1696,6 +2113,344 @@ __global__ __launch_bounds__(256) void lower_mv_reduce_kernel(const double* __re
     out[i] = a;
 }
 
+// =================================================================================
+// Persistent tail: the last T <= TAIL_TMAX tile columns ts .. nt-1
+// of the factorisation in ONE launch, as a dataflow of tile tasks instead of per-column
+// kernel launches (the serial tail paid the full K = 128 update of the remaining triangle
+// and three launch boundaries per column on its critical path):
+//   D(k)      diagonal block of tile column k            (potrf_diag2_body)
+//   S(i,k,h)  TRSM of rows 64h.. of tile (i,k), i > k   (tail_trsm, 4 waves x 16 rows)
+//   U(i,j;k)  tile (i,j) -= L(i,k) L(j,k)^T, k < j <= i  (tail_update, whole tile)
+//   Q(i,i;k)  the same for one quadrant of the next diagonal tile (the critical path)
+// Tasks are dequeued from one counter in a fixed order that is a topological order of
+// their dependencies (tail_task_list): D(0), then for each k the critical set of column
+// k+1 (S(k+1,k), the three quadrants of U(k+1,k+1;k), D(k+1), the other S(i,k), U(i,k+1;k))
+// followed by the rest of column k's updates. A workgroup waits only for tasks dequeued
+// before its own, so the earliest unfinished task always has its inputs: no deadlock, and
+// no co-residency assumption (a workgroup that never starts holds no task).
+// Hand-offs between workgroups (any XCD): the producer stores its tile with sc1
+// (write-through) stores, every wave waits vmcnt(0), the workgroup meets a barrier and one
+// lane bumps the task's counter with an agent-scope atomic; the consumer's lane 0 polls
+// the counters with sc1 loads, the workgroup meets a barrier, and every load of handed-off
+// data is an sc1 load (MI355X_MICROARCH.md "Valid forms", table row 1). Every wait is
+// bounded (0.2 s); an expired wait sets TailCtl::err, which the host turns into GAPLAC_E_HIP.
+// =================================================================================
+enum { TK_D = 0, TK_S = 1, TK_U = 2, TK_Q = 3 };
+
+__host__ __device__ __forceinline__ uint32_t tail_enc(int type, int q, int k, int i, int j) {
+    return (uint32_t)type | ((uint32_t)q << 2) | ((uint32_t)k << 4) | ((uint32_t)i << 10) | ((uint32_t)j << 16);
+}
+
+// TRSM of rows 64h .. 64h+63 of tile (bi, k): X = B L_kk^{-T} by blocked substitution
+// (trsm_subst_kernel_body's arithmetic). Waves 0-3 (one per SIMD, so the four dependent
+// MFMA chains do not share a matrix pipe) own 16 rows each; all 8 waves stage L_kk's 28
+// strictly-lower 16x16 blocks and the 8 inverses in LDS.
+template <int AUX>
+__device__ __forceinline__ void tail_trsm(double* smem, double* Acol, int64_t lda, int k, int bi, int h,
+                                          const double* Dk) {
+    double* Ls = smem;  // (TRSM_LBLK + NDB) x 256
+    const int tid = otid(), wave = tid >> 6, lane = tid & 63;
+    const int fr = lane >> 4, fc = lane & 15;
+    const int64_t k0 = (int64_t)k * NB;
+    const Gm<AUX> gA(Acol), gD(Dk);
+    const uint32_t rowb = (uint32_t)((int64_t)bi * NB + 64 * h + 16 * (wave & 3));
+    d4 Bt[NDB];
+    if (wave < 4) {
+#pragma unroll
+        for (int b = 0; b < NDB; ++b)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Bt[b][q] = gA.ld((uint32_t)((int64_t)(16 * b + fr + 4 * q) * lda + rowb + fc));
+    }
+    {
+        // block (b, c), c < b, at p = b(b-1)/2 + c: Ls[p*256 + m*16 + j] = L(16b + j, 16c + m)
+        const int e = tid & 255, m = e >> 4, j = e & 15;
+        double x[18];
+#pragma unroll
+        for (int hh = 0; hh < 18; ++hh) {
+            const int p = (tid >> 8) + 2 * hh;
+            if (p < TRSM_LBLK) {
+                int b = 1;
+                while ((b + 1) * b / 2 <= p) ++b;
+                const int c = p - b * (b - 1) / 2;
+                x[hh] = gA.ld((uint32_t)((16 * c + m) * lda + k0 + 16 * b + j));
+            } else {
+                x[hh] = gD.ld((uint32_t)((p - TRSM_LBLK) * 256 + e));
+            }
+        }
+#pragma unroll
+        for (int hh = 0; hh < 18; ++hh) Ls[((tid >> 8) + 2 * hh) * 256 + e] = x[hh];
+    }
+    __syncthreads();
+    if (wave >= 4) return;
+    d4 Y[NDB];
+#pragma unroll
+    for (int b = 0; b < NDB; ++b) {
+        d4 s0 = Bt[b], s1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int c = 0; c < b; ++c) {
+            const double* Lbc = Ls + (b * (b - 1) / 2 + c) * 256;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const double lbc = -Lbc[(4 * kk + fr) * 16 + fc];
+                if (c & 1)
+                    s1 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s1, 0, 0, 0);
+                else
+                    s0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s0, 0, 0, 0);
+            }
+        }
+        s0 += s1;
+        const double* Di = Ls + (TRSM_LBLK + b) * 256;
+        d4 y = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+            y = __builtin_amdgcn_mfma_f64_16x16x4f64(Di[(4 * kk + fr) * 16 + fc], s0[kk], y, 0, 0, 0);
+        Y[b] = y;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gA.st((uint32_t)((int64_t)(16 * b + fr + 4 * q) * lda + rowb + fc), y[q]);
+    }
+}
+
+// TRSM of tile (bi, k) right after the diagonal block in the same workgroup: L_kk's
+// 16x16 blocks are still in LDS (Ab, packed as potrf_diag2_body keeps them) and so are the
+// inverses (Dl); wave w owns rows 16w .. 16w+15 (the arithmetic of tail_trsm).
+template <int AUX>
+__device__ __forceinline__ void tail_trsm_lds(const double* Ab, const double* Dl, double* Acol, int64_t lda, int bi) {
+    const int tid = otid(), wave = tid >> 6, lane = tid & 63;
+    const int fr = lane >> 4, fc = lane & 15;
+    const Gm<AUX> gA(Acol);
+    const uint32_t rowb = (uint32_t)((int64_t)bi * NB + 16 * wave);
+    d4 Bt[NDB];
+#pragma unroll
+    for (int b = 0; b < NDB; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Bt[b][q] = gA.ld((uint32_t)((int64_t)(16 * b + fr + 4 * q) * lda + rowb + fc));
+    d4 Y[NDB];
+#pragma unroll
+    for (int b = 0; b < NDB; ++b) {
+        d4 s0 = Bt[b], s1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int c = 0; c < b; ++c) {
+            const double* Lbc = Ab + bidx(b, c) * 256;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const double lbc = -Lbc[(4 * kk + fr) * 16 + fc];
+                if (c & 1)
+                    s1 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s1, 0, 0, 0);
+                else
+                    s0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s0, 0, 0, 0);
+            }
+        }
+        s0 += s1;
+        const double* Di = Dl + b * 256;
+        d4 y = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+            y = __builtin_amdgcn_mfma_f64_16x16x4f64(Di[(4 * kk + fr) * 16 + fc], s0[kk], y, 0, 0, 0);
+        Y[b] = y;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gA.st((uint32_t)((int64_t)(16 * b + fr + 4 * q) * lda + rowb + fc), y[q]);
+    }
+}
+
+// C -= P Q^T over the K = 128 columns of tile column k, for a region of RB*32 rows x CB*64
+// columns of tile column j (whole tile: RB = 4, CB = 2; quadrant: RB = 2, CB = 1). 8 waves
+// as 2 (rows) x 4 (columns), each RB x CB blocks of 16x16; fragments straight from global
+// (sc1), two groups of 4 k-steps in flight. P rows start at row0, Q rows at qrow0 (global
+// rows of the panel), C columns at ccol0 within tile column j's storage.
+template <int AUX, int RB, int CB>
+__device__ __forceinline__ void tail_update(const Gm<AUX>& gC, const Gm<AUX>& gP, int64_t lda, int row0, int ccol0,
+                                            int qrow0) {
+    const int tid = otid(), wave = tid >> 6, lane = tid & 63;
+    const int fr = lane >> 4, fc = lane & 15;
+    const int wr = wave & 1, wc = wave >> 1;
+    const int r0 = row0 + wr * RB * 16, c0 = ccol0 + wc * CB * 16, q0 = qrow0 + wc * CB * 16;
+    d4 acc[RB][CB];
+#pragma unroll
+    for (int mi = 0; mi < RB; ++mi)
+#pragma unroll
+        for (int mj = 0; mj < CB; ++mj)
+#pragma unroll
+            for (int rg = 0; rg < 4; ++rg)
+                acc[mi][mj][rg] = gC.ld((uint32_t)((int64_t)(c0 + 16 * mj + fr + 4 * rg) * lda + r0 + 16 * mi + fc));
+    constexpr int G = 4;  // k-steps per group
+    double fa[2][G][CB], fb[2][G][RB];
+    auto load = [&](int buf, int g) {
+#pragma unroll
+        for (int st = 0; st < G; ++st) {
+            const int64_t col = (int64_t)(4 * (G * g + st) + fr) * lda;
+#pragma unroll
+            for (int mi = 0; mi < RB; ++mi) fb[buf][st][mi] = gP.ld((uint32_t)(col + r0 + 16 * mi + fc));
+#pragma unroll
+            for (int mj = 0; mj < CB; ++mj) fa[buf][st][mj] = gP.ld((uint32_t)(col + q0 + 16 * mj + fc));
+        }
+    };
+    auto compute = [&](int buf) {
+#pragma unroll
+        for (int st = 0; st < G; ++st)
+#pragma unroll
+            for (int mi = 0; mi < RB; ++mi) {
+                const double b = -fb[buf][st][mi];
+#pragma unroll
+                for (int mj = 0; mj < CB; ++mj)
+                    acc[mi][mj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][st][mj], b, acc[mi][mj], 0, 0, 0);
+            }
+    };
+    constexpr int NG = NB / (4 * G);  // 8 groups
+    load(0, 0);
+#pragma unroll 1
+    for (int g = 0; g < NG; g += 2) {
+        load(1, g + 1);
+        compute(0);
+        if (g + 2 < NG) load(0, g + 2);
+        compute(1);
+    }
+#pragma unroll
+    for (int mi = 0; mi < RB; ++mi)
+#pragma unroll
+        for (int mj = 0; mj < CB; ++mj)
+#pragma unroll
+            for (int rg = 0; rg < 4; ++rg)
+                gC.st((uint32_t)((int64_t)(c0 + 16 * mj + fr + 4 * rg) * lda + r0 + 16 * mi + fc), acc[mi][mj][rg]);
+}
+
+// One quadrant (64x64) of C -= P Q^T, K = 128 (the critical diagonal-tile update): every
+// fragment (32 k-steps x 3 per lane, in two halves) is loaded before the first MFMA, so the
+// handed-off panel's memory latency is paid once. 8 waves as 2 x 4, each 32 x 16.
+template <int AUX>
+__device__ __forceinline__ void tail_quad(const Gm<AUX>& gC, const Gm<AUX>& gP, int64_t lda, int row0, int ccol0,
+                                          int qrow0) {
+    const int tid = otid(), wave = tid >> 6, lane = tid & 63;
+    const int fr = lane >> 4, fc = lane & 15;
+    const int wr = wave & 1, wc = wave >> 1;
+    const int r0 = row0 + wr * 32, c0 = ccol0 + wc * 16, q0 = qrow0 + wc * 16;
+    d4 acc[2];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg)
+            acc[mi][rg] = gC.ld((uint32_t)((int64_t)(c0 + fr + 4 * rg) * lda + r0 + 16 * mi + fc));
+    constexpr int H = NB / 8;  // k-steps per half
+    double fa[2][H], fb[2][H][2];
+    auto load = [&](int h) {
+#pragma unroll
+        for (int st = 0; st < H; ++st) {
+            const int64_t col = (int64_t)(4 * (H * h + st) + fr) * lda;
+            fb[h][st][0] = gP.ld((uint32_t)(col + r0 + fc));
+            fb[h][st][1] = gP.ld((uint32_t)(col + r0 + 16 + fc));
+            fa[h][st] = gP.ld((uint32_t)(col + q0 + fc));
+        }
+    };
+    load(0);
+    load(1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int st = 0; st < H; ++st) {
+            acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[h][st], -fb[h][st][0], acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[h][st], -fb[h][st][1], acc[1], 0, 0, 0);
+        }
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg)
+            gC.st((uint32_t)((int64_t)(c0 + fr + 4 * rg) * lda + r0 + 16 * mi + fc), acc[mi][rg]);
+}
+
+__device__ __forceinline__ unsigned tail_ld(const unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Lane 0: wait until the task's inputs are final (bounded: 0.2 s of the 100 MHz clock).
+__device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int k, int i, int j) {
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+        bool ok;
+        if (type == TK_D) {
+            ok = tail_ld(&c->units[k * TAIL_TMAX + k]) >= 3u * k;
+        } else if (type == TK_S) {
+            ok = tail_ld(&c->ddone[k]) != 0u && tail_ld(&c->units[i * TAIL_TMAX + k]) >= 4u * k;
+        } else {
+            const unsigned ups = i == j ? 3u : 4u;
+            ok = tail_ld(&c->sdone[i * TAIL_TMAX + k]) >= 2u && tail_ld(&c->sdone[j * TAIL_TMAX + k]) >= 2u &&
+                 tail_ld(&c->units[i * TAIL_TMAX + j]) >= ups * k;
+        }
+        if (ok) return true;
+        if (wall_clock64() - t0 > 20000000ull) return false;  // 0.2 s
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+__global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict__ kt) {
+    __shared__ double smem[DIAG2_SMEM];
+    __shared__ unsigned s_task;
+    kt_begin(kt);
+    TailCtl* ctl = a.ctl;
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) s_task = atomicAdd(&ctl->head, 1u);
+        __syncthreads();
+        const unsigned tk = s_task;
+        if (tk >= (unsigned)a.ntasks) break;
+        const uint32_t e = a.tasks[tk];
+        const int type = (int)(e & 3u), q = (int)((e >> 2) & 3u), k = (int)((e >> 4) & 63u);
+        const int i = (int)((e >> 10) & 63u), j = (int)((e >> 16) & 63u);
+        if (a.trace && threadIdx.x == 0) a.trace[3 * tk] = wall_clock64();
+        if (threadIdx.x == 0 && !tail_wait(ctl, type, k, i, j)) atomicOr(&ctl->err, 1u);
+        __syncthreads();
+        if (a.trace && threadIdx.x == 0) a.trace[3 * tk + 1] = wall_clock64();
+        const int gk = a.ts + k;
+        double* colk = a.A + (int64_t)gk * NB * a.lda;
+        if (type == TK_D) {
+            if ((int64_t)gk * NB < a.N)
+                potrf_diag2_body<GM_SC1>(smem, colk + (int64_t)gk * NB, a.lda, a.N, (int64_t)gk * NB,
+                                         a.Dinv + (size_t)gk * DINV_PER_BLOCK, a.res);
+        } else if (type == TK_S) {
+            tail_trsm<GM_SC1>(smem, colk, a.lda, gk, a.ts + i, q, a.Dinv + (size_t)gk * DINV_PER_BLOCK);
+        } else {
+            const int gi = a.ts + i, gj = a.ts + j;
+            const Gm<GM_SC1> gC(a.A + (int64_t)gj * NB * a.lda), gP(colk);
+            if (type == TK_U) {
+                tail_update<GM_SC1, 4, 2>(gC, gP, a.lda, gi * NB, 0, gj * NB);
+            } else {
+                const int qi = q >> 1, qj = q & 1;
+                tail_quad<GM_SC1>(gC, gP, a.lda, gi * NB + 64 * qi, 64 * qj, gj * NB + 64 * qj);
+            }
+        }
+        // publish: every wave's stores complete, then one lane bumps the counter
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (type == TK_D) {
+                __hip_atomic_fetch_add(&ctl->ddone[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (type == TK_S) {  // two halves per tile: done at 2
+                __hip_atomic_fetch_add(&ctl->sdone[i * TAIL_TMAX + k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                const unsigned add = type == TK_Q ? 1u : (i == j ? 3u : 4u);
+                __hip_atomic_fetch_add(&ctl->units[i * TAIL_TMAX + j], add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (a.trace) a.trace[3 * tk + 2] = wall_clock64();
+        }
+    }
+    if (threadIdx.x == 0 && ctl->err) atomicOr(&a.res->err, 2u);
+    kt_end(kt);
+}
+
+// Dequeue order of the tail's tasks (see the block comment above).
+void build_tail_tasks(int T, std::vector<uint32_t>& out) {
+    out.clear();
+    out.push_back(tail_enc(TK_D, 0, 0, 0, 0));
+    for (int k = 0; k + 1 < T; ++k) {
+        for (int h = 0; h < 2; ++h) out.push_back(tail_enc(TK_S, h, k, k + 1, 0));  // row halves
+        for (int q : {0, 2, 3}) out.push_back(tail_enc(TK_Q, q, k, k + 1, k + 1));  // lower quadrants
+        out.push_back(tail_enc(TK_D, 0, k + 1, 0, 0));
+        for (int i = k + 2; i < T; ++i)
+            for (int h = 0; h < 2; ++h) out.push_back(tail_enc(TK_S, h, k, i, 0));
+        for (int i = k + 2; i < T; ++i) out.push_back(tail_enc(TK_U, 0, k, i, k + 1));
+        for (int j = k + 2; j < T; ++j)
+            for (int i = j; i < T; ++i) out.push_back(tail_enc(TK_U, 0, k, i, j));
+    }
+}
+
 // ------------------------------- launchers ---------------------------------------
 // Every launcher first passes the element range its grid will touch to guard_launch
 // (gaplac_internal.h): derived from the same tile counts / decodes the
@@ -1792,7 +2547,7 @@ void launch_gram_list(hipStream_t s, double* C, int64_t ldc, int64_t N, const do
 void launch_potrf_diag(hipStream_t s, double* Ablk, int64_t lda, int64_t N, int64_t g0, double* Dinv,
                        EvalResult* res, KTime* kt) {
     if (!guard_launch("potrf_diag_kernel", Ablk, 0, tiles_end(lda, 0, 0))) return;
-    potrf_diag_kernel<<<dim3(1), dim3(256), 0, s>>>(Ablk, lda, N, g0, Dinv, res, kt);
+    potrf_diag_kernel<<<dim3(1), dim3(512), 0, s>>>(Ablk, lda, N, g0, Dinv, res, kt);
 }
 
 void launch_trsm(hipStream_t s, double* Acol, int64_t lda, int nt, int k, const double* Dinv, KTime* kt) {
@@ -1966,6 +2721,12 @@ void launch_lower_mv(hipStream_t s, const double* A, int64_t lda, int64_t N, con
     lower_mv_partial_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nk), dim3(256), 0, s>>>(A, lda, N, z,
                                                                                                 partial);
     lower_mv_reduce_kernel<<<dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s>>>(partial, N, nk, out);
+}
+
+void launch_tail(hipStream_t s, const TailArgs& a, int grid, KTime* kt) {
+    if (a.ntasks <= 0 || a.T <= 0) return;
+    if (!guard_launch("tail_kernel", a.A, 0, tiles_end(a.lda, a.ts + a.T - 1, a.ts + a.T - 1))) return;
+    tail_kernel<<<dim3((unsigned)grid), dim3(512), 0, s>>>(a, kt);
 }
 
 void launch_init_result(hipStream_t s, EvalResult* res) {

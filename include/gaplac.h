@@ -205,6 +205,9 @@ typedef struct gaplac_stats {
     int64_t cinv_launches;      /* -C^{-1} = -L^{-T} L^{-1} tile launches (cinv_tile_kernel) */
     double  cinv_ms;
     double  contract_ms;        /* dC/dtheta contraction (grad_contract_kernel) */
+    /* persistent tail (tail_kernel: the last tile columns as one dataflow launch) */
+    int64_t tail_launches;
+    double  tail_ms;
 } gaplac_stats;
 int gaplac_set_profiling(gaplac_ctx* ctx, int mode);
 int gaplac_get_stats(gaplac_ctx* ctx, gaplac_stats* out);

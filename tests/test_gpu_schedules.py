@@ -10,7 +10,9 @@ these sizes) and agree with the default schedule.
 * GAPLAC_PAIR_M / GAPLAC_PAIR_EXT / GAPLAC_BAND_TILES_M: paired bulk updates (every other
   step the columns beyond the next band receive two super-panels at once; 1: whenever
   possible), with or without the second band, bands as whole tiles or quadrants;
-* GAPLAC_SERIAL: everything on one stream.
+* GAPLAC_SERIAL: everything on one stream;
+* GAPLAC_TAILK=0: the serial tail as per-column launches instead of the persistent dataflow
+  kernel (tail_kernel).
 The settings are read when a context is created (gaplac_ctx_create).
 """
 import os
@@ -40,6 +42,9 @@ SCHEDULES = {
     "pair_ext_spw3_whole": {"GAPLAC_PAIR_M": "1", "GAPLAC_PAIR_EXT": "1", "GAPLAC_SPW": "3", "GAPLAC_BAND_TILES_M": "1"},
     "pair_no_tail": {"GAPLAC_PAIR_M": "1", "GAPLAC_TAIL_S": "0"},
     "serial_stream": {"GAPLAC_SERIAL": "1"},
+    "tail_launches": {"GAPLAC_TAILK": "0"},
+    "tailk_everything": {"GAPLAC_TAIL_S": "1000"},
+    "tailk_spw1": {"GAPLAC_SPW": "1", "GAPLAC_TAIL_S": "40"},
 }
 SIZES = [1, 127, 129, 700, 2049, 3000, 9000]
 TERMS = [(SQEXP, 0, 1.5, 0), (OU, 0, 3.0, 1), (CAT, 1, 0.0, 2), (NOISE, -1, 1.0, 3)]

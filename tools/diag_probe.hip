@@ -13,6 +13,10 @@ using namespace gaplac;
 __global__ __launch_bounds__(256) void diag_v1(double* Ag, int64_t lda, int64_t N, int64_t g0, double* Dinv, EvalResult* res) {
   potrf_diag_kernel_body(Ag, lda, N, g0, Dinv, res);
 }
+__global__ __launch_bounds__(512) void diag_v2(double* Ag, int64_t lda, int64_t N, int64_t g0, double* Dinv, EvalResult* res) {
+  __shared__ double smem[DIAG2_SMEM];
+  potrf_diag2_body<0>(smem, Ag, lda, N, g0, Dinv, res);
+}
 
 int main() {
   const int nt = 4, Np = nt * NB;
@@ -40,17 +44,24 @@ int main() {
   CK(hipMalloc(&res, sizeof(EvalResult)));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   std::vector<double> out(h.size()), dinv(DINV_PER_BLOCK);
-  for (int v = 1; v <= 1; ++v) {
+  auto run = [&](int v, const std::vector<double>& in, int64_t N, float* ms) -> int {
+    CK(hipMemcpy(A, in.data(), in.size() * 8, hipMemcpyHostToDevice));
+    CK(hipMemset(Dinv, 0, DINV_PER_BLOCK * 8));
+    launch_init_result(0, res);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    if (v == 1) diag_v1<<<1, 256>>>(A, Np, N, 0, Dinv, res);
+    else diag_v2<<<1, 512>>>(A, Np, N, 0, Dinv, res);
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(ms, e0, e1));
+    CK(hipMemcpy(out.data(), A, out.size() * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(dinv.data(), Dinv, dinv.size() * 8, hipMemcpyDeviceToHost));
+    return 0;
+  };
+  for (int v = 1; v <= 2; ++v) {
     for (int rep = 0; rep < 4; ++rep) {
-      CK(hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice));
-      launch_init_result(0, res);
-      CK(hipDeviceSynchronize());
-      CK(hipEventRecord(e0));
-      if (v == 1) diag_v1<<<1, 256>>>(A, Np, 1 << 30, 0, Dinv, res);
-      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
-      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-      CK(hipMemcpy(out.data(), A, out.size() * 8, hipMemcpyDeviceToHost));
-      CK(hipMemcpy(dinv.data(), Dinv, dinv.size() * 8, hipMemcpyDeviceToHost));
+      float ms;
+      if (run(v, h, 1 << 30, &ms)) return 1;
       EvalResult hr; CK(hipMemcpy(&hr, res, sizeof hr, hipMemcpyDeviceToHost));
       double errL = 0, errD = 0;
       for (int j = 0; j < NB; ++j)
@@ -63,27 +74,48 @@ int main() {
             for (int m = 0; m < 16; ++m) s += dinv[b * 256 + m * 16 + r] * (m >= c ? L[(16 * b + c) * NB + 16 * b + m] : 0.0);
             errD = std::fmax(errD, std::fabs(s - (r == c ? 1.0 : 0.0)));
           }
-      printf("diag v%d: %.1f us (event)  max|L-Lcpu| %.2e  max|Dinv L - I| %.2e  info %llx\n", v, ms * 1e3, errL, errD,
-             (unsigned long long)hr.info);
-      if (v == 1 && rep == 3) {  // v1: per panel s, phase 2 of each wave (cycles, s_memtime)
+      double upper = 0;  // the block's upper triangle must be written as zeros
+      for (int j = 0; j < NB; ++j)
+        for (int i = 0; i < j; ++i) upper = std::fmax(upper, std::fabs(out[(size_t)j * Np + i]));
+      printf("diag v%d: %.1f us (event)  max|L-Lcpu| %.2e  max|Dinv L - I| %.2e  upper %.1e  info %llx err %u\n", v, ms * 1e3,
+             errL, errD, upper, (unsigned long long)hr.info, hr.err);
+      if (rep == 3) {  // per panel s, phase 2 of each wave (cycles, s_memtime)
         unsigned long long st[128]; CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof st));
-        printf("  v1 load %llu\n", st[0] - st[20]);
+        printf("  v%d load %llu\n", v, st[0] - st[20]);
         for (int s = 0; s < 8; ++s) {
           const unsigned long long p2 = st[1 + 2 * s];
-          printf("  v1 s=%d: phase1+barrier %5llu | phase2 w0 dpanel %5llu w1 trailing %5llu w3 dinv+trailing %5llu\n", s,
-                 p2 - (s ? st[2 * s] : st[0]), st[2 + 2 * s] - p2, st[29 + s] - p2, st[21 + s] - p2);
+          printf("  v%d s=%d: phase1+barrier %5llu | phase2 w0 %5llu w1 %5llu w%d %5llu\n", v, s,
+                 p2 - (s ? st[2 * s] : st[0]), st[2 + 2 * s] - p2, st[29 + s] - p2, v == 1 ? 3 : 2, st[21 + s] - p2);  // v2: stamps of waves 1 and 2
         }
-        printf("  v1 last dinv+store %llu total %llu cycles\n", st[19] - st[17], st[19] - st[20]);
+        printf("  v%d last dinv %llu store %llu total %llu cycles\n", v, st[18] - st[17], st[19] - st[18], st[19] - st[20]);
       }
     }
   }
+  // v2 against v1 with padding inside the block (N = 100, 127, 37: unit pivots from there)
+  for (int64_t Npad : {100, 127, 37, 1}) {
+    float ms;
+    std::vector<double> hp = h;
+    for (int j = 0; j < Np; ++j)
+      for (int i = 0; i < Np; ++i)
+        if ((i >= Npad || j >= Npad) && i != j) hp[(size_t)j * Np + i] = (i == Npad && j < Npad) ? 0.3 * std::sin(j) : 0.0;
+    if (run(1, hp, Npad, &ms)) return 1;
+    std::vector<double> o1 = out, d1 = dinv;
+    EvalResult h1; CK(hipMemcpy(&h1, res, sizeof h1, hipMemcpyDeviceToHost));
+    if (run(2, hp, Npad, &ms)) return 1;
+    EvalResult h2; CK(hipMemcpy(&h2, res, sizeof h2, hipMemcpyDeviceToHost));
+    double dl = 0, dd = 0;
+    for (int j = 0; j < NB; ++j)
+      for (int i = j; i < NB; ++i) dl = std::fmax(dl, std::fabs(out[(size_t)j * Np + i] - o1[(size_t)j * Np + i]));
+    for (int k = 0; k < DINV_PER_BLOCK; ++k) dd = std::fmax(dd, std::fabs(dinv[k] - d1[k]));
+    printf("padded N=%lld: max|L2-L1| %.2e  max|Dinv2-Dinv1| %.2e  info %llx/%llx\n", (long long)Npad, dl, dd,
+           (unsigned long long)h1.info, (unsigned long long)h2.info);
+  }
   // non-PD: zero the block's (37,37) pivot region -> info must be 38 in both
-  for (int v = 1; v <= 1; ++v) {
+  for (int v = 1; v <= 2; ++v) {
     std::vector<double> hb = h;
     for (int i = 0; i < Np; ++i) { hb[(size_t)37 * Np + i] = 0; hb[(size_t)i * Np + 37] = 0; }
-    CK(hipMemcpy(A, hb.data(), hb.size() * 8, hipMemcpyHostToDevice));
-    launch_init_result(0, res);
-    if (v == 1) diag_v1<<<1, 256>>>(A, Np, 1 << 30, 0, Dinv, res);
+    float ms;
+    if (run(v, hb, 1 << 30, &ms)) return 1;
     EvalResult hr; CK(hipMemcpy(&hr, res, sizeof hr, hipMemcpyDeviceToHost));
     printf("non-PD v%d: info %llu (expect 38)\n", v, (unsigned long long)hr.info);
   }
