@@ -89,7 +89,7 @@ struct TailCtl {
     unsigned err;   // an expired wait
     unsigned ddone[TAIL_TMAX];                // D(k) finished
     unsigned sdone[TAIL_TMAX * TAIL_TMAX];    // S(i,k) finished ([i][k], relative tile indices)
-    unsigned units[TAIL_TMAX * TAIL_TMAX];    // tile (i,j): update units applied (4 per column, 3 on the diagonal)
+    unsigned units[TAIL_TMAX * TAIL_TMAX];    // tile (i,j): update units applied per column (4; 10 on the diagonal)
 };
 struct TailArgs {
     double* A;

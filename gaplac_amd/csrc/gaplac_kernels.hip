@@ -2121,10 +2121,11 @@ __global__ __launch_bounds__(256) void lower_mv_reduce_kernel(const double* __re
 //   D(k)      diagonal block of tile column k            (potrf_diag2_body)
 //   S(i,k,h)  TRSM of rows 64h.. of tile (i,k), i > k   (tail_trsm, 4 waves x 16 rows)
 //   U(i,j;k)  tile (i,j) -= L(i,k) L(j,k)^T, k < j <= i  (tail_update, whole tile)
-//   Q(i,i;k)  the same for one quadrant of the next diagonal tile (the critical path)
+//   Q(i,i;k)  the same for one 32x32 block (10 of them: the lower block triangle) of the
+//             next diagonal tile (the critical path; tail_q32)
 // Tasks are dequeued from one counter in a fixed order that is a topological order of
 // their dependencies (tail_task_list): D(0), then for each k the critical set of column
-// k+1 (S(k+1,k), the three quadrants of U(k+1,k+1;k), D(k+1), the other S(i,k), U(i,k+1;k))
+// k+1 (S(k+1,k), the ten blocks of U(k+1,k+1;k), D(k+1), the other S(i,k), U(i,k+1;k))
 // followed by the rest of column k's updates. A workgroup waits only for tasks dequeued
 // before its own, so the earliest unfinished task always has its inputs: no deadlock, and
 // no co-residency assumption (a workgroup that never starts holds no task).
@@ -2136,9 +2137,41 @@ __global__ __launch_bounds__(256) void lower_mv_reduce_kernel(const double* __re
 // bounded (0.2 s); an expired wait sets TailCtl::err, which the host turns into GAPLAC_E_HIP.
 // =================================================================================
 enum { TK_D = 0, TK_S = 1, TK_U = 2, TK_Q = 3 };
+constexpr unsigned TAIL_NQ = 10;  // Q blocks per diagonal tile (= units a diagonal U adds)
 
 __host__ __device__ __forceinline__ uint32_t tail_enc(int type, int q, int k, int i, int j) {
-    return (uint32_t)type | ((uint32_t)q << 2) | ((uint32_t)k << 4) | ((uint32_t)i << 10) | ((uint32_t)j << 16);
+    return (uint32_t)type | ((uint32_t)q << 2) | ((uint32_t)k << 6) | ((uint32_t)i << 12) | ((uint32_t)j << 18);
+}
+
+// Stage L_kk's 28 strictly-lower 16x16 blocks and the 8 inverses in LDS for the tail's
+// TRSM: block (b, c), c < b, at p = b(b-1)/2 + c, Ls[p*256 + m*16 + j] = L(16b + j, 16c + m);
+// inverses at p = 28 + b. Half the block (tid >> 8) takes the even p, half the odd; every
+// address is a select between two compile-time block positions, so the 18 loads of a
+// thread are issued back to back (a data-dependent decode here put a divergent branch and
+// a full vmcnt wait around every load: 11 us of the task, round 3).
+__host__ __device__ constexpr int tri_b_of(int p) {
+    int b = 1;
+    while ((b + 1) * b / 2 <= p) ++b;
+    return b;
+}
+template <int AUX>
+__device__ __forceinline__ void tail_trsm_stage(double* Ls, const Gm<AUX>& gA, const Gm<AUX>& gD, int64_t lda,
+                                                int64_t k0, int tid) {
+    const int e = tid & 255, m = e >> 4, j = e & 15;
+    const bool odd = (tid >> 8) != 0;
+    double x[18];
+#pragma unroll
+    for (int hh = 0; hh < 14; ++hh) {
+        const int p0 = 2 * hh, p1 = 2 * hh + 1;
+        const int b0 = tri_b_of(p0), b1 = tri_b_of(p1);
+        const int c0 = p0 - b0 * (b0 - 1) / 2, c1 = p1 - b1 * (b1 - 1) / 2;
+        const int b = odd ? b1 : b0, c = odd ? c1 : c0;
+        x[hh] = gA.ld((uint32_t)((16 * c + m) * lda + k0 + 16 * b + j));
+    }
+#pragma unroll
+    for (int hh = 14; hh < 18; ++hh) x[hh] = gD.ld((uint32_t)((2 * hh + (odd ? 1 : 0) - TRSM_LBLK) * 256 + e));
+#pragma unroll
+    for (int hh = 0; hh < 18; ++hh) Ls[(2 * hh + (odd ? 1 : 0)) * 256 + e] = x[hh];
 }
 
 // TRSM of rows 64h .. 64h+63 of tile (bi, k): X = B L_kk^{-T} by blocked substitution
@@ -2161,25 +2194,7 @@ __device__ __forceinline__ void tail_trsm(double* smem, double* Acol, int64_t ld
 #pragma unroll
             for (int q = 0; q < 4; ++q) Bt[b][q] = gA.ld((uint32_t)((int64_t)(16 * b + fr + 4 * q) * lda + rowb + fc));
     }
-    {
-        // block (b, c), c < b, at p = b(b-1)/2 + c: Ls[p*256 + m*16 + j] = L(16b + j, 16c + m)
-        const int e = tid & 255, m = e >> 4, j = e & 15;
-        double x[18];
-#pragma unroll
-        for (int hh = 0; hh < 18; ++hh) {
-            const int p = (tid >> 8) + 2 * hh;
-            if (p < TRSM_LBLK) {
-                int b = 1;
-                while ((b + 1) * b / 2 <= p) ++b;
-                const int c = p - b * (b - 1) / 2;
-                x[hh] = gA.ld((uint32_t)((16 * c + m) * lda + k0 + 16 * b + j));
-            } else {
-                x[hh] = gD.ld((uint32_t)((p - TRSM_LBLK) * 256 + e));
-            }
-        }
-#pragma unroll
-        for (int hh = 0; hh < 18; ++hh) Ls[((tid >> 8) + 2 * hh) * 256 + e] = x[hh];
-    }
+    tail_trsm_stage(Ls, gA, gD, lda, k0, tid);
     __syncthreads();
     if (wave >= 4) return;
     d4 Y[NDB];
@@ -2200,48 +2215,6 @@ __device__ __forceinline__ void tail_trsm(double* smem, double* Acol, int64_t ld
         }
         s0 += s1;
         const double* Di = Ls + (TRSM_LBLK + b) * 256;
-        d4 y = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-            y = __builtin_amdgcn_mfma_f64_16x16x4f64(Di[(4 * kk + fr) * 16 + fc], s0[kk], y, 0, 0, 0);
-        Y[b] = y;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) gA.st((uint32_t)((int64_t)(16 * b + fr + 4 * q) * lda + rowb + fc), y[q]);
-    }
-}
-
-// TRSM of tile (bi, k) right after the diagonal block in the same workgroup: L_kk's
-// 16x16 blocks are still in LDS (Ab, packed as potrf_diag2_body keeps them) and so are the
-// inverses (Dl); wave w owns rows 16w .. 16w+15 (the arithmetic of tail_trsm).
-template <int AUX>
-__device__ __forceinline__ void tail_trsm_lds(const double* Ab, const double* Dl, double* Acol, int64_t lda, int bi) {
-    const int tid = otid(), wave = tid >> 6, lane = tid & 63;
-    const int fr = lane >> 4, fc = lane & 15;
-    const Gm<AUX> gA(Acol);
-    const uint32_t rowb = (uint32_t)((int64_t)bi * NB + 16 * wave);
-    d4 Bt[NDB];
-#pragma unroll
-    for (int b = 0; b < NDB; ++b)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) Bt[b][q] = gA.ld((uint32_t)((int64_t)(16 * b + fr + 4 * q) * lda + rowb + fc));
-    d4 Y[NDB];
-#pragma unroll
-    for (int b = 0; b < NDB; ++b) {
-        d4 s0 = Bt[b], s1 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int c = 0; c < b; ++c) {
-            const double* Lbc = Ab + bidx(b, c) * 256;
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                const double lbc = -Lbc[(4 * kk + fr) * 16 + fc];
-                if (c & 1)
-                    s1 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s1, 0, 0, 0);
-                else
-                    s0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s0, 0, 0, 0);
-            }
-        }
-        s0 += s1;
-        const double* Di = Dl + b * 256;
         d4 y = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk)
@@ -2313,47 +2286,34 @@ __device__ __forceinline__ void tail_update(const Gm<AUX>& gC, const Gm<AUX>& gP
                 gC.st((uint32_t)((int64_t)(c0 + 16 * mj + fr + 4 * rg) * lda + r0 + 16 * mi + fc), acc[mi][mj][rg]);
 }
 
-// One quadrant (64x64) of C -= P Q^T, K = 128 (the critical diagonal-tile update): every
-// fragment (32 k-steps x 3 per lane, in two halves) is loaded before the first MFMA, so the
-// handed-off panel's memory latency is paid once. 8 waves as 2 x 4, each 32 x 16.
+// One 32x32 block of C -= P Q^T, K = 128 (the critical diagonal-tile update, split ten
+// ways): waves 0-3 take one 16x16 sub-block each and load all 32 k-steps of their two
+// fragments before the first MFMA, so the handed-off panel's memory latency is paid once.
+// Each accumulator starts from C and takes the k-steps in order: the same rounding as the
+// per-column chain kernels, so a matrix factored in the tail and through super-panels
+// (gradient / posterior workspaces) gives bitwise the same factor.
 template <int AUX>
-__device__ __forceinline__ void tail_quad(const Gm<AUX>& gC, const Gm<AUX>& gP, int64_t lda, int row0, int ccol0,
-                                          int qrow0) {
+__device__ __forceinline__ void tail_q32(const Gm<AUX>& gC, const Gm<AUX>& gP, int64_t lda, int row0, int ccol0,
+                                         int qrow0) {
     const int tid = otid(), wave = tid >> 6, lane = tid & 63;
+    if (wave >= 4) return;
     const int fr = lane >> 4, fc = lane & 15;
-    const int wr = wave & 1, wc = wave >> 1;
-    const int r0 = row0 + wr * 32, c0 = ccol0 + wc * 16, q0 = qrow0 + wc * 16;
-    d4 acc[2];
+    const int r0 = row0 + 16 * (wave & 1), c0 = ccol0 + 16 * (wave >> 1), q0 = qrow0 + 16 * (wave >> 1);
+    d4 acc;
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+    for (int rg = 0; rg < 4; ++rg) acc[rg] = gC.ld((uint32_t)((int64_t)(c0 + fr + 4 * rg) * lda + r0 + fc));
+    constexpr int KS = NB / 4;  // 32 k-steps
+    double fa[KS], fb[KS];
 #pragma unroll
-        for (int rg = 0; rg < 4; ++rg)
-            acc[mi][rg] = gC.ld((uint32_t)((int64_t)(c0 + fr + 4 * rg) * lda + r0 + 16 * mi + fc));
-    constexpr int H = NB / 8;  // k-steps per half
-    double fa[2][H], fb[2][H][2];
-    auto load = [&](int h) {
+    for (int st = 0; st < KS; ++st) {
+        const int64_t col = (int64_t)(4 * st + fr) * lda;
+        fb[st] = gP.ld((uint32_t)(col + r0 + fc));
+        fa[st] = gP.ld((uint32_t)(col + q0 + fc));
+    }
 #pragma unroll
-        for (int st = 0; st < H; ++st) {
-            const int64_t col = (int64_t)(4 * (H * h + st) + fr) * lda;
-            fb[h][st][0] = gP.ld((uint32_t)(col + r0 + fc));
-            fb[h][st][1] = gP.ld((uint32_t)(col + r0 + 16 + fc));
-            fa[h][st] = gP.ld((uint32_t)(col + q0 + fc));
-        }
-    };
-    load(0);
-    load(1);
+    for (int st = 0; st < KS; ++st) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[st], -fb[st], acc, 0, 0, 0);
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int st = 0; st < H; ++st) {
-            acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[h][st], -fb[h][st][0], acc[0], 0, 0, 0);
-            acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[h][st], -fb[h][st][1], acc[1], 0, 0, 0);
-        }
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int rg = 0; rg < 4; ++rg)
-            gC.st((uint32_t)((int64_t)(c0 + fr + 4 * rg) * lda + r0 + 16 * mi + fc), acc[mi][rg]);
+    for (int rg = 0; rg < 4; ++rg) gC.st((uint32_t)((int64_t)(c0 + fr + 4 * rg) * lda + r0 + fc), acc[rg]);
 }
 
 __device__ __forceinline__ unsigned tail_ld(const unsigned* p) {
@@ -2366,11 +2326,11 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int k, int
     for (;;) {
         bool ok;
         if (type == TK_D) {
-            ok = tail_ld(&c->units[k * TAIL_TMAX + k]) >= 3u * k;
+            ok = tail_ld(&c->units[k * TAIL_TMAX + k]) >= TAIL_NQ * k;
         } else if (type == TK_S) {
             ok = tail_ld(&c->ddone[k]) != 0u && tail_ld(&c->units[i * TAIL_TMAX + k]) >= 4u * k;
         } else {
-            const unsigned ups = i == j ? 3u : 4u;
+            const unsigned ups = i == j ? TAIL_NQ : 4u;
             ok = tail_ld(&c->sdone[i * TAIL_TMAX + k]) >= 2u && tail_ld(&c->sdone[j * TAIL_TMAX + k]) >= 2u &&
                  tail_ld(&c->units[i * TAIL_TMAX + j]) >= ups * k;
         }
@@ -2392,8 +2352,8 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         const unsigned tk = s_task;
         if (tk >= (unsigned)a.ntasks) break;
         const uint32_t e = a.tasks[tk];
-        const int type = (int)(e & 3u), q = (int)((e >> 2) & 3u), k = (int)((e >> 4) & 63u);
-        const int i = (int)((e >> 10) & 63u), j = (int)((e >> 16) & 63u);
+        const int type = (int)(e & 3u), q = (int)((e >> 2) & 15u), k = (int)((e >> 6) & 63u);
+        const int i = (int)((e >> 12) & 63u), j = (int)((e >> 18) & 63u);
         if (a.trace && threadIdx.x == 0) a.trace[3 * tk] = wall_clock64();
         if (threadIdx.x == 0 && !tail_wait(ctl, type, k, i, j)) atomicOr(&ctl->err, 1u);
         __syncthreads();
@@ -2412,8 +2372,9 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
             if (type == TK_U) {
                 tail_update<GM_SC1, 4, 2>(gC, gP, a.lda, gi * NB, 0, gj * NB);
             } else {
-                const int qi = q >> 1, qj = q & 1;
-                tail_quad<GM_SC1>(gC, gP, a.lda, gi * NB + 64 * qi, 64 * qj, gj * NB + 64 * qj);
+                // q = qa (qa + 1) / 2 + qb, qb <= qa: 32x32 block (qa, qb) of the diagonal tile
+                const int qa = q >= 6 ? 3 : q >= 3 ? 2 : q >= 1 ? 1 : 0, qb = q - qa * (qa + 1) / 2;
+                tail_q32<GM_SC1>(gC, gP, a.lda, gi * NB + 32 * qa, 32 * qb, gj * NB + 32 * qb);
             }
         }
         // publish: every wave's stores complete, then one lane bumps the counter
@@ -2425,7 +2386,7 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
             } else if (type == TK_S) {  // two halves per tile: done at 2
                 __hip_atomic_fetch_add(&ctl->sdone[i * TAIL_TMAX + k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
-                const unsigned add = type == TK_Q ? 1u : (i == j ? 3u : 4u);
+                const unsigned add = type == TK_Q ? 1u : (i == j ? TAIL_NQ : 4u);
                 __hip_atomic_fetch_add(&ctl->units[i * TAIL_TMAX + j], add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             if (a.trace) a.trace[3 * tk + 2] = wall_clock64();
@@ -2441,7 +2402,7 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out) {
     out.push_back(tail_enc(TK_D, 0, 0, 0, 0));
     for (int k = 0; k + 1 < T; ++k) {
         for (int h = 0; h < 2; ++h) out.push_back(tail_enc(TK_S, h, k, k + 1, 0));  // row halves
-        for (int q : {0, 2, 3}) out.push_back(tail_enc(TK_Q, q, k, k + 1, k + 1));  // lower quadrants
+        for (int q = 0; q < (int)TAIL_NQ; ++q) out.push_back(tail_enc(TK_Q, q, k, k + 1, k + 1));
         out.push_back(tail_enc(TK_D, 0, k + 1, 0, 0));
         for (int i = k + 2; i < T; ++i)
             for (int h = 0; h < 2; ++h) out.push_back(tail_enc(TK_S, h, k, i, 0));
