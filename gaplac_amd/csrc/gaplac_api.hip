@@ -98,6 +98,7 @@ struct gaplac_ctx {
     // own workspace and streams; they read the parent's uploaded X and v).
     std::vector<gaplac_ctx*> lanes;
     int batch_lanes = 2;           // GAPLAC_BATCH_LANES (measured at N=8192: 1 lane 138, 2 lanes 191, 3-6 lanes 161-187 evals/s)
+    int tail_share = 1;            // lanes sharing the GPU (gaplac_logpdf_batch): tail grid = CUs / share
     bool borrowed_inputs = false;  // dX / dv belong to the parent
     // Extra rows below the matrix, factored along (lda = Np + 128 xr_tiles):
     //   1 = identity rows E = [I 0] -> L^{-T} (gradient, gaplac_logpdf_grad)
@@ -575,7 +576,9 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             }
             TailArgs ta{ctx->A, lda, N, ts, T, ctx->Dinv, ctx->dres, ctx->tctl, ctx->ttasks, nts,
                         ctx->ttrace_path.empty() ? nullptr : ctx->ttrace};
-            launch_tail(sm, ta, std::min(ctx->ncu, nts), slot(ctx, 10, 0));
+            // batch lanes run their tails side by side: each persistent grid takes its share
+            // of the CUs (one tail workgroup fills a CU's LDS), so no tail waits for another
+            launch_tail(sm, ta, std::min(std::max(1, ctx->ncu / std::max(1, ctx->tail_share)), nts), slot(ctx, 10, 0));
         } else {
             serial_tail(ctx, sm, N, lda, nt, ts);
         }
@@ -1009,9 +1012,11 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     };
     hipError_t e;
     if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
-    // s_panel: highest priority; s_main: lowest priority. A CU mask for the
-    // chain and hipGraph replay were both measured slower (graph nodes lose the stream
-    // priorities) and are not kept.
+    // s_panel: highest priority; s_main: lowest priority. A CU mask that
+    // keeps CUs free of s_main's workgroups for the chain (the 512-thread diagonal-block
+    // kernel cannot share a CU with a bulk workgroup) and hipGraph replay were both measured
+    // slower (round 3, N=16384: no mask 28.8 ms, 4/8/16 CUs 29.8-30.1 ms: the masked bulk
+    // kernel lost ~15%) and are not kept.
     int ncu = 0;
     if ((e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
         return fail("attribute", e);
@@ -1201,6 +1206,14 @@ int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D, 
         c->dv_elems = ctx->dv_elems;
         lane[(size_t)l] = c;
     }
+    const char* tsh = std::getenv("GAPLAC_TAIL_SHARE");  // TEMPORARY measurement switch
+    for (int l = 0; l < nl; ++l) lane[(size_t)l]->tail_share = (tsh && tsh[0] == '0') ? 1 : nl;
+    struct ShareReset {
+        std::vector<gaplac_ctx*>& ls;
+        ~ShareReset() {
+            for (gaplac_ctx* c : ls) c->tail_share = 1;
+        }
+    } share_reset{lane};
     std::vector<int> pending((size_t)nl, -1);
     auto drain = [&](int l) -> int {
         const int m = pending[(size_t)l];

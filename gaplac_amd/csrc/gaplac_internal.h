@@ -88,6 +88,7 @@ struct TailCtl {
     unsigned head;  // dequeue counter
     unsigned err;   // an expired wait
     unsigned ddone[TAIL_TMAX];                // D(k) finished
+    unsigned dprog[TAIL_TMAX];                // D(k): block columns (and inverses) 0 .. dprog-1 final
     unsigned sdone[TAIL_TMAX * TAIL_TMAX];    // S(i,k) finished ([i][k], relative tile indices)
     unsigned units[TAIL_TMAX * TAIL_TMAX];    // tile (i,j): update units applied per column (4; 10 on the diagonal)
 };

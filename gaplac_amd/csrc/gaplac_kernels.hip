@@ -800,6 +800,10 @@ __device__ __forceinline__ int otid() {
 }
 typedef unsigned gm_u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned gm_u32x4 __attribute__((ext_vector_type(4)));
+// address-space views for __builtin_amdgcn_global_load_lds (LDS-DMA)
+typedef __attribute__((address_space(1))) const void* GlobalCPtr;
+typedef __attribute__((address_space(3))) void* LdsPtr;
+
 template <int AUX>
 struct Gm {
     __amdgpu_buffer_rsrc_t r;
@@ -1097,7 +1101,7 @@ __device__ __forceinline__ void diag2_store_column(const double* Ab, double* Ag,
 template <int AUX>
 __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restrict__ Ag, int64_t lda, int64_t N,
                                                  int64_t g0, double* __restrict__ Dinv, EvalResult* __restrict__ res,
-                                                 double* Dl = nullptr) {
+                                                 double* Dl = nullptr, unsigned* prog = nullptr) {
     double* colbuf = smem;
     double* rdiag = colbuf + DIAG2_COLBUF;
     double* Ab = rdiag + NB;
@@ -1119,6 +1123,14 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
             const int q = t + 512 * i, I = q >> 7, pr = q & 127, c = pr >> 3, r = 2 * (pr & 7);
             col0[i] = g.ld2((uint32_t)((int64_t)c * lda + 16 * I + r));
         }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int q = t + 512 * i, I = q >> 7, pr = q & 127;
+            *reinterpret_cast<double2*>(&Ab[bidx(I, 0) * 256 + 2 * pr]) = col0[i];
+        }
+        // issued after column 0 is in LDS: behind the wave-dependent branch the compiler
+        // can no longer count the loads in flight, and a column-0 write placed after it
+        // waited for all of them (vmcnt(0)), the whole block's latency before panel 0
         if (wave >= 2) {
 #pragma unroll
             for (int i = 0; i < 10; ++i) {
@@ -1130,11 +1142,6 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
                     rest[i] = g.ld2((uint32_t)((int64_t)(16 * J + c) * lda + 16 * I + r));
                 }
             }
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int q = t + 512 * i, I = q >> 7, pr = q & 127;
-            *reinterpret_cast<double2*>(&Ab[bidx(I, 0) * 256 + 2 * pr]) = col0[i];
         }
     }
     if (wave == 3 && lane < 16) colbuf[lane * 64 + lane] = -1.0;  // the records' flags
@@ -1150,10 +1157,15 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
                 rdiag[16 * (s - 1) + lane] = colbuf[lane * 64 + lane];  // rd of panel s-1's columns
                 colbuf[lane * 64 + lane] = -1.0;                        // the records' flags
             }
+            // progress hand-off (tail_kernel): the stores of block column s-2 and Dinv(s-2)
+            // (phase 2 of panel s-1) complete before this phase's barrier, published after it
+            if (prog && wave >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
         STAMP(1 + 2 * s);
         // phase 2
+        if (prog && s >= 2 && wave == 3 && lane == 0)  // columns and inverses 0 .. s-2 final
+            __hip_atomic_store(prog, (unsigned)(s - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (wave == 0) {
             diag2_sweep_a(Ab, colbuf, s, lane, g0, N, res);
         } else if (wave == 1 && s < 4) {
@@ -1188,7 +1200,10 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
         __syncthreads();
     }
     if (wave == 3 && lane < 16) rdiag[16 * (NDB - 1) + lane] = colbuf[lane * 64 + lane];
+    if (prog && wave >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (prog && wave == 3 && lane == 0)  // columns and inverses 0 .. 6 final
+        __hip_atomic_store(prog, (unsigned)(NDB - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     STAMP(17);
     if (wave == 4) diag2_dinv<AUX>(Ab, Dinv, rdiag, NDB - 1, lane, Dl);
     STAMP(18);
@@ -1197,6 +1212,16 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
 }
 #undef SB
 #undef PIN
+
+// The round-2 diagonal block (256 threads, 255 VGPRs: one wave per SIMD, so it fits on a
+// CU beside one bulk workgroup, which the 512-thread kernel does not).
+__global__ __launch_bounds__(256) void potrf_diag1_kernel(double* __restrict__ Ag, int64_t lda, int64_t N,
+                                                          int64_t g0, double* __restrict__ Dinv,
+                                                          EvalResult* __restrict__ res, KTime* __restrict__ kt) {
+    kt_begin(kt);
+    potrf_diag_kernel_body(Ag, lda, N, g0, Dinv, res);
+    kt_end(kt);
+}
 
 // Ag: the diagonal block (global rows/cols g0 .. g0+127) in its storage, leading dim lda.
 __global__ __launch_bounds__(512) void potrf_diag_kernel(double* __restrict__ Ag, int64_t lda,
@@ -2119,14 +2144,16 @@ __global__ __launch_bounds__(256) void lower_mv_reduce_kernel(const double* __re
 // kernel launches (the serial tail paid the full K = 128 update of the remaining triangle
 // and three launch boundaries per column on its critical path):
 //   D(k)      diagonal block of tile column k            (potrf_diag2_body)
-//   S(i,k,h)  TRSM of rows 64h.. of tile (i,k), i > k   (tail_trsm, 4 waves x 16 rows)
-//   U(i,j;k)  tile (i,j) -= L(i,k) L(j,k)^T, k < j <= i  (tail_update, whole tile)
+//   S(i,k,h)  TRSM of rows 64h.. of tile (i,k), i > k   (tail_trsm_pipe, 4 waves x 16
+//             rows, block row b as soon as D(k) has published L_kk's rows up to b)
+//   U(i,j;k)  tile (i,j) -= L(i,k) L(j,k)^T, k < j <= i  (tail_update, whole tile, or four
+//             64x64 quadrant tasks for the tile (k+2,k+1) the next TRSM needs first)
 //   Q(i,i;k)  the same for one 32x32 block (10 of them: the lower block triangle) of the
 //             next diagonal tile (the critical path; tail_q32)
 // Tasks are dequeued from one counter in a fixed order that is a topological order of
-// their dependencies (tail_task_list): D(0), then for each k the critical set of column
-// k+1 (S(k+1,k), the ten blocks of U(k+1,k+1;k), D(k+1), the other S(i,k), U(i,k+1;k))
-// followed by the rest of column k's updates. A workgroup waits only for tasks dequeued
+// their dependencies (build_tail_tasks): per column the critical set first (the next
+// diagonal tile's ten blocks, D, the TRSM behind it and the tile it needs), then the rest
+// of the column's TRSMs and updates. A workgroup waits only for tasks dequeued
 // before its own, so the earliest unfinished task always has its inputs: no deadlock, and
 // no co-residency assumption (a workgroup that never starts holds no task).
 // Hand-offs between workgroups (any XCD): the producer stores its tile with sc1
@@ -2200,6 +2227,116 @@ __device__ __forceinline__ void tail_trsm(double* smem, double* Acol, int64_t ld
     d4 Y[NDB];
 #pragma unroll
     for (int b = 0; b < NDB; ++b) {
+        d4 s0 = Bt[b], s1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int c = 0; c < b; ++c) {
+            const double* Lbc = Ls + (b * (b - 1) / 2 + c) * 256;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const double lbc = -Lbc[(4 * kk + fr) * 16 + fc];
+                if (c & 1)
+                    s1 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s1, 0, 0, 0);
+                else
+                    s0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s0, 0, 0, 0);
+            }
+        }
+        s0 += s1;
+        const double* Di = Ls + (TRSM_LBLK + b) * 256;
+        d4 y = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+            y = __builtin_amdgcn_mfma_f64_16x16x4f64(Di[(4 * kk + fr) * 16 + fc], s0[kk], y, 0, 0, 0);
+        Y[b] = y;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gA.st((uint32_t)((int64_t)(16 * b + fr + 4 * q) * lda + rowb + fc), y[q]);
+    }
+}
+
+// The same TRSM pipelined behind the diagonal block: it may start while D(k) is still
+// running. Waves 4-7 stage block row b of L_kk (blocks (b, c), c < b) and Dinv_b as soon as
+// D(k) has published them (prog >= b + 1: potrf_diag2_body's progress counter, b <= 6;
+// row 7 when D(k) is done), each wave the blocks c = w - 4 (mod 4), then mark the row in
+// LDS (rowf[b] counts the four waves); waves 0-3 (16 rows each) take rows as they arrive:
+// Y_b = Dinv_b (B_b - sum_{c<b} L_bc Y_c), the arithmetic of tail_trsm. The chain after
+// D(k) ends is the last two rows instead of the whole substitution.
+template <int AUX>
+__device__ __forceinline__ void tail_trsm_pipe(double* smem, unsigned* rowf, double* Acol, int64_t lda, int k, int bi,
+                                               int h, const double* Dk, const unsigned* prog, const unsigned* ddone,
+                                               unsigned* err) {
+    double* Ls = smem;  // (TRSM_LBLK + NDB) x 256, as tail_trsm_stage lays it out
+    const int tid = otid(), wave = tid >> 6, lane = tid & 63;
+    const int fr = lane >> 4, fc = lane & 15;
+    const int64_t k0 = (int64_t)k * NB;
+    const Gm<AUX> gA(Acol), gD(Dk);
+    if (tid < NDB) rowf[tid] = 0u;
+    __syncthreads();
+    if (wave >= 4) {
+        const int w = wave - 4;
+        bool timeout = false;
+        int next = 0;  // first row not staged yet
+        while (next < NDB) {
+            // lane 0 polls D(k)'s progress (sc1 loads), bounded; the wave follows its verdict:
+            // rows next .. avail-1 are final (row b <= 6 needs prog >= b + 1, row 7 D done)
+            int avail = 0;
+            if (lane == 0) {
+                const unsigned long long t0 = wall_clock64();
+                for (;;) {
+                    if (__hip_atomic_load(ddone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+                        avail = NDB;
+                    } else {
+                        const int pr = (int)__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        avail = pr < NDB - 1 ? pr : NDB - 1;
+                    }
+                    if (avail > next) break;
+                    if (wall_clock64() - t0 > 20000000ull) {
+                        avail = NDB;  // expired: stage what is there, flag the error
+                        timeout = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            avail = __builtin_amdgcn_readfirstlane(avail);
+            // every block c = w, w + 4, ... <= b of the rows b in [next, avail) (c == b: Dinv_b)
+            // by LDS-DMA (global_load_lds, 16 B per lane: half a block per instruction, the
+            // LDS image lane-linear), all in flight together, then one wait
+            for (int b = next; b < avail; ++b) {
+                for (int c = w; c <= b; c += 4) {
+                    const int p = c < b ? b * (b - 1) / 2 + c : TRSM_LBLK + b;
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int q = 64 * u + lane, m = q >> 3, j = 2 * (q & 7);  // pair q = (m, j..j+1)
+                        const double* src = c < b ? Acol + (int64_t)(16 * c + m) * lda + k0 + 16 * b + j
+                                                  : Dk + b * 256 + 2 * q;
+                        __builtin_amdgcn_global_load_lds((GlobalCPtr)src, (LdsPtr)(Ls + p * 256 + 128 * u), 16, 0, AUX);
+                    }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0)
+                for (int b = next; b < avail; ++b)
+                    __hip_atomic_fetch_add(&rowf[b], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            next = avail;
+        }
+        if (timeout && lane == 0) atomicOr(err, 1u);
+        return;
+    }
+    const uint32_t rowb = (uint32_t)((int64_t)bi * NB + 64 * h + 16 * wave);
+    d4 Bt[NDB];
+#pragma unroll
+    for (int b = 0; b < NDB; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Bt[b][q] = gA.ld((uint32_t)((int64_t)(16 * b + fr + 4 * q) * lda + rowb + fc));
+    d4 Y[NDB];
+#pragma unroll
+    for (int b = 0; b < NDB; ++b) {
+        // row b staged by all four staging waves (bounded: they always get there, a
+        // timed-out wait above stages stale data and flags the error)
+        for (int it = 0; it < (1 << 22); ++it) {
+            if (__hip_atomic_load(&rowf[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= 4u) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         d4 s0 = Bt[b], s1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int c = 0; c < b; ++c) {
@@ -2327,8 +2464,8 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int k, int
         bool ok;
         if (type == TK_D) {
             ok = tail_ld(&c->units[k * TAIL_TMAX + k]) >= TAIL_NQ * k;
-        } else if (type == TK_S) {
-            ok = tail_ld(&c->ddone[k]) != 0u && tail_ld(&c->units[i * TAIL_TMAX + k]) >= 4u * k;
+        } else if (type == TK_S) {  // the block itself; D(k)'s progress inside tail_trsm_pipe
+            ok = tail_ld(&c->units[i * TAIL_TMAX + k]) >= 4u * k;
         } else {
             const unsigned ups = i == j ? TAIL_NQ : 4u;
             ok = tail_ld(&c->sdone[i * TAIL_TMAX + k]) >= 2u && tail_ld(&c->sdone[j * TAIL_TMAX + k]) >= 2u &&
@@ -2343,6 +2480,7 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int k, int
 __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict__ kt) {
     __shared__ double smem[DIAG2_SMEM];
     __shared__ unsigned s_task;
+    __shared__ unsigned s_rowf[NDB];
     kt_begin(kt);
     TailCtl* ctl = a.ctl;
     for (;;) {
@@ -2363,14 +2501,18 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         if (type == TK_D) {
             if ((int64_t)gk * NB < a.N)
                 potrf_diag2_body<GM_SC1>(smem, colk + (int64_t)gk * NB, a.lda, a.N, (int64_t)gk * NB,
-                                         a.Dinv + (size_t)gk * DINV_PER_BLOCK, a.res);
+                                         a.Dinv + (size_t)gk * DINV_PER_BLOCK, a.res, nullptr, &ctl->dprog[k]);
         } else if (type == TK_S) {
-            tail_trsm<GM_SC1>(smem, colk, a.lda, gk, a.ts + i, q, a.Dinv + (size_t)gk * DINV_PER_BLOCK);
+            tail_trsm_pipe<GM_SC1>(smem, s_rowf, colk, a.lda, gk, a.ts + i, q, a.Dinv + (size_t)gk * DINV_PER_BLOCK,
+                                   &ctl->dprog[k], &ctl->ddone[k], &ctl->err);
         } else {
             const int gi = a.ts + i, gj = a.ts + j;
             const Gm<GM_SC1> gC(a.A + (int64_t)gj * NB * a.lda), gP(colk);
-            if (type == TK_U) {
+            if (type == TK_U && q == 0) {
                 tail_update<GM_SC1, 4, 2>(gC, gP, a.lda, gi * NB, 0, gj * NB);
+            } else if (type == TK_U) {  // quadrant q - 1 of an off-diagonal tile
+                const int qi = (q - 1) >> 1, qj = (q - 1) & 1;
+                tail_update<GM_SC1, 2, 1>(gC, gP, a.lda, gi * NB + 64 * qi, 64 * qj, gj * NB + 64 * qj);
             } else {
                 // q = qa (qa + 1) / 2 + qb, qb <= qa: 32x32 block (qa, qb) of the diagonal tile
                 const int qa = q >= 6 ? 3 : q >= 3 ? 2 : q >= 1 ? 1 : 0, qb = q - qa * (qa + 1) / 2;
@@ -2386,7 +2528,7 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
             } else if (type == TK_S) {  // two halves per tile: done at 2
                 __hip_atomic_fetch_add(&ctl->sdone[i * TAIL_TMAX + k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
-                const unsigned add = type == TK_Q ? 1u : (i == j ? TAIL_NQ : 4u);
+                const unsigned add = (type == TK_Q || q != 0) ? 1u : (i == j ? TAIL_NQ : 4u);
                 __hip_atomic_fetch_add(&ctl->units[i * TAIL_TMAX + j], add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             if (a.trace) a.trace[3 * tk + 2] = wall_clock64();
@@ -2396,19 +2538,46 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
     kt_end(kt);
 }
 
-// Dequeue order of the tail's tasks (see the block comment above).
+// Dequeue order of the tail's tasks (see the block comment above). Every task waits only
+// for tasks listed before it. Per g = 0 .. T-2 the tasks of column g, the ones the chain
+// needs soonest first:
+//   S(g+2,g)  Q(g+1,g+1;g) x10  U(g+2,g+1;g) x4 quadrants  D(g+1)  S(g+2,g+1) (pipelined
+//   behind D(g+1))  Q(g+2,g+2;g) x10  S(g+3,g)  U(g+3,g+1;g) x4  S(i,g) i >= g+4
+//   U(i,g+1;g) x4 i >= g+4  U(i,j;g) j >= g+2 (but (g+2,g+2))
+// after D(0) and S(1,0): the next tile column's tiles are updated in small (quadrant)
+// tasks early, so each TRSM, the one behind D(g+1) above all, and the next diagonal
+// update find their inputs final instead of queued behind the bulk of column g's updates
+// (a tile's S -> U -> S -> ... chain down the sub-diagonals must keep the chain's pace).
 void build_tail_tasks(int T, std::vector<uint32_t>& out) {
     out.clear();
+    auto S = [&](int i, int k) {
+        if (i < T)
+            for (int h = 0; h < 2; ++h) out.push_back(tail_enc(TK_S, h, k, i, 0));  // row halves
+    };
+    auto Qs = [&](int i, int k) {  // the ten 32x32 blocks of diagonal tile i
+        if (i < T)
+            for (int q = 0; q < (int)TAIL_NQ; ++q) out.push_back(tail_enc(TK_Q, q, k, i, i));
+    };
+    auto Uq = [&](int i, int j, int k) {  // quadrants of off-diagonal tile (i, j)
+        if (i < T)
+            for (int q = 1; q <= 4; ++q) out.push_back(tail_enc(TK_U, q, k, i, j));
+    };
     out.push_back(tail_enc(TK_D, 0, 0, 0, 0));
-    for (int k = 0; k + 1 < T; ++k) {
-        for (int h = 0; h < 2; ++h) out.push_back(tail_enc(TK_S, h, k, k + 1, 0));  // row halves
-        for (int q = 0; q < (int)TAIL_NQ; ++q) out.push_back(tail_enc(TK_Q, q, k, k + 1, k + 1));
-        out.push_back(tail_enc(TK_D, 0, k + 1, 0, 0));
-        for (int i = k + 2; i < T; ++i)
-            for (int h = 0; h < 2; ++h) out.push_back(tail_enc(TK_S, h, k, i, 0));
-        for (int i = k + 2; i < T; ++i) out.push_back(tail_enc(TK_U, 0, k, i, k + 1));
-        for (int j = k + 2; j < T; ++j)
-            for (int i = j; i < T; ++i) out.push_back(tail_enc(TK_U, 0, k, i, j));
+    S(1, 0);
+    for (int g = 0; g + 1 < T; ++g) {
+        S(g + 2, g);
+        Qs(g + 1, g);
+        Uq(g + 2, g + 1, g);
+        out.push_back(tail_enc(TK_D, 0, g + 1, 0, 0));
+        S(g + 2, g + 1);
+        Qs(g + 2, g);
+        S(g + 3, g);
+        Uq(g + 3, g + 1, g);
+        for (int i = g + 4; i < T; ++i) S(i, g);
+        for (int i = g + 4; i < T; ++i) Uq(i, g + 1, g);
+        for (int j = g + 2; j < T; ++j)
+            for (int i = j; i < T; ++i)
+                if (i != g + 2 || j != g + 2) out.push_back(tail_enc(TK_U, 0, g, i, j));
     }
 }
 
@@ -2508,7 +2677,14 @@ void launch_gram_list(hipStream_t s, double* C, int64_t ldc, int64_t N, const do
 void launch_potrf_diag(hipStream_t s, double* Ablk, int64_t lda, int64_t N, int64_t g0, double* Dinv,
                        EvalResult* res, KTime* kt) {
     if (!guard_launch("potrf_diag_kernel", Ablk, 0, tiles_end(lda, 0, 0))) return;
-    potrf_diag_kernel<<<dim3(1), dim3(512), 0, s>>>(Ablk, lda, N, g0, Dinv, res, kt);
+    static const bool v1 = [] {
+        const char* e = std::getenv("GAPLAC_DIAG1");  // TEMPORARY measurement switch
+        return e && e[0] == '1';
+    }();
+    if (v1)
+        potrf_diag1_kernel<<<dim3(1), dim3(256), 0, s>>>(Ablk, lda, N, g0, Dinv, res, kt);
+    else
+        potrf_diag_kernel<<<dim3(1), dim3(512), 0, s>>>(Ablk, lda, N, g0, Dinv, res, kt);
 }
 
 void launch_trsm(hipStream_t s, double* Acol, int64_t lda, int nt, int k, const double* Dinv, KTime* kt) {

@@ -8,12 +8,18 @@ import sys
 
 tr = list(csv.DictReader(open(f"{sys.argv[1]}/run_kernel_trace.csv")))
 tr.sort(key=lambda r: int(r["Start_Timestamp"]))
-grams = [i for i, r in enumerate(tr) if "gram_kernel" in r["Kernel_Name"]]
-ev = tr[grams[-2]:]  # the last evaluation: both Gram parts onwards
+# the last evaluation with bulk updates: from its first Gram launch to its reduction
+# (the bench's later extras, e.g. the N = 4096 line, run after it)
+last_bulk = max(i for i, r in enumerate(tr) if "tile_syrk" in r["Kernel_Name"])
+g0 = max(i for i in range(last_bulk) if "gram_kernel" in tr[i]["Kernel_Name"])
+while g0 > 0 and "gram_kernel" in tr[g0 - 1]["Kernel_Name"]:
+    g0 -= 1
+g1 = min(i for i in range(last_bulk, len(tr)) if "reduce_final" in tr[i]["Kernel_Name"])
+ev = tr[g0:g1 + 1]
 t0 = int(ev[0]["Start_Timestamp"])
 end = max(int(r["End_Timestamp"]) for r in ev) - t0
 bulk = [(int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0, "quad" if "quad_bulk" in r["Kernel_Name"] else "syrk")
-        for r in ev if "tile_syrk" in r["Kernel_Name"] or "quad_bulk" in r["Kernel_Name"]]
+        for r in ev if "tile_syrk" in r["Kernel_Name"]]
 head = bulk[0][0]
 tail = end - bulk[-1][1]
 busy = sum(b - a for a, b, _ in bulk)

@@ -1,5 +1,5 @@
 """A/B of the tail length at N = 4096 and 16384 (configs[1], configs[2] workloads,
-device-resident inputs): ms per evaluation for GAPLAC_TAIL_S in a list, and TAILK off."""
+device-resident inputs): ms per evaluation for GAPLAC_TAIL_S in a list (default 48)."""
 import os
 import sys
 import time
@@ -45,8 +45,8 @@ def bench(env, N, terms_fn, reps):
 def main():
     t1 = lambda i: CF.config1_terms(CF.LENGTHSCALES_1[i % 4])  # noqa: E731
     t2 = lambda i: [(SQEXP, 0, (0.8, 1.0, 1.2, 1.5)[i % 4], 0), (OU, 0, 3.0, 1), (CAT, 1, 0.0, 2), (NOISE, -1, 1.0, 3)]  # noqa: E731
-    envs = [("tailk64", {}), ("tailk48", {"GAPLAC_TAIL_S": "48"}), ("tailk32", {"GAPLAC_TAIL_S": "32"}),
-            ("launches32", {"GAPLAC_TAILK": "0"})]
+    envs = [("tail64", {"GAPLAC_TAIL_S": "64"}), ("tail48", {}), ("tail40", {"GAPLAC_TAIL_S": "40"}),
+            ("tail32", {"GAPLAC_TAIL_S": "32"}), ("tail24", {"GAPLAC_TAIL_S": "24"})]
     for N, fn, reps in ((4096, t1, 20), (16384, t2, 6)):
         for name, env in envs:
             ms, lp = bench(env, N, fn, reps)
