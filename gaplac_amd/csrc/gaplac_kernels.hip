@@ -1213,25 +1213,18 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
 #undef SB
 #undef PIN
 
-// The round-2 diagonal block (256 threads, 255 VGPRs: one wave per SIMD, so it fits on a
-// CU beside one bulk workgroup, which the 512-thread kernel does not).
-__global__ __launch_bounds__(256) void potrf_diag1_kernel(double* __restrict__ Ag, int64_t lda, int64_t N,
-                                                          int64_t g0, double* __restrict__ Dinv,
-                                                          EvalResult* __restrict__ res, KTime* __restrict__ kt) {
+// The diagonal block of the super-panel chain (256 threads: 255 + 16 registers, one wave per
+// SIMD, 75 KB of LDS) fits on a CU beside ONE resident bulk workgroup (208 registers, 72 KB).
+// potrf_diag2_body (512 threads, 199 registers, two waves per SIMD: 27 us alone against
+// ~32) does not: beside the bulk updates it waited for a CU with both bulk workgroups
+// retired, i.e. for the end of the launch (3.2 ms of a 3.6 ms K = 1024 update in a kernel
+// trace, profiles/r03r_timeline.txt), so the chain kernel here is this one and diag2 runs
+// only inside the persistent tail, where nothing else is resident.
+__global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ Ag, int64_t lda, int64_t N,
+                                                         int64_t g0, double* __restrict__ Dinv,
+                                                         EvalResult* __restrict__ res, KTime* __restrict__ kt) {
     kt_begin(kt);
     potrf_diag_kernel_body(Ag, lda, N, g0, Dinv, res);
-    kt_end(kt);
-}
-
-// Ag: the diagonal block (global rows/cols g0 .. g0+127) in its storage, leading dim lda.
-__global__ __launch_bounds__(512) void potrf_diag_kernel(double* __restrict__ Ag, int64_t lda,
-                                                         int64_t N, int64_t g0,
-                                                         double* __restrict__ Dinv,
-                                                         EvalResult* __restrict__ res,
-                                                         KTime* __restrict__ kt) {
-    __shared__ double smem[DIAG2_SMEM];
-    kt_begin(kt);
-    potrf_diag2_body<0>(smem, Ag, lda, N, g0, Dinv, res);
     kt_end(kt);
 }
 
@@ -2677,14 +2670,7 @@ void launch_gram_list(hipStream_t s, double* C, int64_t ldc, int64_t N, const do
 void launch_potrf_diag(hipStream_t s, double* Ablk, int64_t lda, int64_t N, int64_t g0, double* Dinv,
                        EvalResult* res, KTime* kt) {
     if (!guard_launch("potrf_diag_kernel", Ablk, 0, tiles_end(lda, 0, 0))) return;
-    static const bool v1 = [] {
-        const char* e = std::getenv("GAPLAC_DIAG1");  // TEMPORARY measurement switch
-        return e && e[0] == '1';
-    }();
-    if (v1)
-        potrf_diag1_kernel<<<dim3(1), dim3(256), 0, s>>>(Ablk, lda, N, g0, Dinv, res, kt);
-    else
-        potrf_diag_kernel<<<dim3(1), dim3(512), 0, s>>>(Ablk, lda, N, g0, Dinv, res, kt);
+    potrf_diag_kernel<<<dim3(1), dim3(256), 0, s>>>(Ablk, lda, N, g0, Dinv, res, kt);
 }
 
 void launch_trsm(hipStream_t s, double* Acol, int64_t lda, int nt, int k, const double* Dinv, KTime* kt) {
