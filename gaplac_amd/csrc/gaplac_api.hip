@@ -69,12 +69,13 @@ struct gaplac_ctx {
     int spw = 4;          // GAPLAC_SPW: super-panel width in 128-column tiles (bulk K = 128 spw)
     int tail_s = 32;      // GAPLAC_TAIL_S: the last ~tail_s tile columns run serially on one stream
                           //   (default 48 with the persistent tail, 32 without)
-    int pair_ext = 1;     // GAPLAC_PAIR_EXT: 1 = a deferring step also updates the band after next
+    int pair_ext = 1;     // 1 = a deferring step also updates the band after next (§3.2)
     int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
     int pair_m = 40;      // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
     int ncu = 256;        // compute units of the device
-    int gram_queue = 2;   // GAPLAC_GRAM_QUEUE: second Gram launch as a work queue of this many
-                          //   workgroups per CU, leaving room for the panel chain (0 = plain grid)
+    int gram_lazy = -1;   // this evaluation: tile columns >= gram_lazy get their Gram tiles in the
+                          //   first bulk update (tile_syrk_gram_kernel), -1 = built by the Gram launches
+    bool gram_lazy_done = false;
     bool tailk = true;    // GAPLAC_TAILK: the serial tail as one persistent dataflow launch (tail_kernel)
     TailCtl* tctl = nullptr;     // its completion counters (zeroed per launch)
     uint32_t* ttasks = nullptr;  // its task list for ttasks_T tile columns
@@ -442,6 +443,37 @@ static void serial_tail(gaplac_ctx* ctx, hipStream_t sm, int64_t N, int64_t lda,
     }
 }
 
+// Paired bulk updates (GAPLAC_PAIR_M): does step p defer its bulk update
+// (only the next-needed bands get SP p; the columns after them get SPs p and p+1 together
+// at step p+1)? pend: the super-panel still pending (-1: none).
+static bool pair_defer(const gaplac_ctx* ctx, const std::vector<int>& spc, int nt, int p, int pend) {
+    const int nsp = (int)spc.size() - 1;
+    const int jb = p + 2 <= nsp ? spc[(size_t)p + 2] : spc[(size_t)nsp];
+    const int je = p + 3 <= nsp ? spc[(size_t)p + 3] : spc[(size_t)nsp];
+    return ctx->pair_m > 0 && pend < 0 && !ctx->serial && !ctx->xr_mode && je > jb && p + 1 + ctx->pair_ext < nsp &&
+           p + 3 + ctx->pair_ext <= nsp && nt - spc[(size_t)p + 3 + ctx->pair_ext] >= ctx->pair_m;
+}
+
+// First tile column of the first bulk_tri update of the schedule below (the columns it
+// reaches have not been touched by any earlier update), or nt if it is not a large
+// tile-kernel launch: the columns before it are the Gram launches' (enqueue_eval_body).
+static int first_bulk_col(const gaplac_ctx* ctx, const std::vector<int>& spc, int nt) {
+    const int nsp = (int)spc.size() - 1;
+    if (nsp <= 0) return nt;
+    int j0;
+    if (pair_defer(ctx, spc, nt, 0, -1)) {
+        if (nsp < 2) return nt;  // (pair_defer needs more super-panels than this)
+        const int je = 4 <= nsp ? spc[4] : spc[(size_t)nsp];
+        const int dcol = ctx->pair_ext > 0 ? spc[4] : spc[3 <= nsp ? 3 : (size_t)nsp];
+        j0 = std::max(je, dcol);
+    } else {
+        j0 = 2 <= nsp ? spc[2] : spc[(size_t)nsp];
+    }
+    const int m = nt - j0;
+    if (m <= 0 || syrk_is_small(m * (m + 1) / 2)) return nt;
+    return j0;
+}
+
 int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     hipStream_t sm = ctx->s_main;
     hipStream_t sp = ctx->serial ? sm : ctx->s_panel;
@@ -461,6 +493,14 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         BulkArgs ba{ctx->A, lda, pn, ctx->tiles + ctx->tile_off[(size_t)m], m * (m + 1) / 2, kdep, j0, j0,
                     ColMap{1, 0, W}};
         const bool small = syrk_is_small(ba.ntiles);
+        if (j0 == ctx->gram_lazy && !ctx->gram_lazy_done) {  // these tiles' Gram entries: in the prologue
+            ba.gtp = ctx->dtp;
+            ba.gX = ctx->dX;
+            ba.gv = ctx->dv;
+            ba.gldx = N;
+            ba.gN = N;
+            ctx->gram_lazy_done = true;
+        }
         const double fl = syrk_flops(m) * (kdep / NB), by = syrk_bytes(m, kdep);
         KTime* kt = small ? slot(ctx, 6, 0) : slot(ctx, 0, fl, by);
         const bool ev = ctx->prof_mode == 2 && !small;
@@ -505,9 +545,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         // columns after it get SPs p and p+1 in one K = 2 x 128W update at step p+1 (band
         // first, then R(p), then the rest). Columns >= dcol lack SP pend.
         const int je = p + 3 <= nsp ? spc[(size_t)p + 3] : spc[(size_t)nsp];
-        const bool defer = ctx->pair_m > 0 && pend < 0 && sp != sm && !ctx->xr_mode && je > jb &&
-                           p + 1 + ctx->pair_ext < nsp && p + 3 + ctx->pair_ext <= nsp &&
-                           nt - spc[(size_t)p + 3 + ctx->pair_ext] >= ctx->pair_m;
+        const bool defer = pair_defer(ctx, spc, nt, p, pend);
         // a band [b0, b1) with the panel columns pc .. c1-1
         auto band = [&](int b0, int b1, int pc) {
             if (b1 <= b0) return;
@@ -587,6 +625,9 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         HIPQ(ctx, hipEventRecord(ctx->ev_xdone, ctx->s_extra));
         HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_xdone, 0));
     }
+    if (ctx->gram_lazy >= 0 && ctx->gram_lazy < nt && !ctx->gram_lazy_done)
+        return set_err(ctx, GAPLAC_E_ARG, "schedule: no bulk update built the Gram tiles of columns >= %d",
+                       ctx->gram_lazy);
     launch_reduce(sm, ctx->A, lda, N, (int64_t)nt * NB, ColMap{1, 0, 1}, ctx->dres);
     HIPQ(ctx, hipGetLastError());
     return 0;
@@ -629,20 +670,24 @@ int enqueue_eval_body(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt)
     const int64_t lda = Np + (int64_t)NB * ctx->xr_tiles;
     launch_init_result(ctx->s_main, ctx->dres);
     if (ctx->recording) launch_kt_reset(ctx->s_main, ctx->dkt, (int)ctx->kt_cap);
-    // Gram in two launches: the first super-panel's tile columns, then the rest (the panel
-    // chain starts on the first part while the second is still being written).
-    const double bytes = 8.0 * (double)Np * (double)(Np + 1) / 2.0 + 8.0 * (double)N * (D + 1);
-    const int rest = std::max(0, nt - ctx->spw);  // tile columns of the second Gram launch
-    const double frac = nt > 0 ? 1.0 - (double)rest * (rest + 1) / ((double)nt * (nt + 1)) : 1.0;
-    launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 1, ctx->spw,
-                slot(ctx, 1, bytes * frac));
+    // Gram in two launches: the first super-panel's tile columns, then the columns up to the
+    // first bulk update's (the panel chain starts on the first part while the second is
+    // still being written); the first bulk update evaluates the Gram tiles of the columns it
+    // reaches itself (tile_syrk_gram_kernel) when every group is a single term.
+    bool all_single = true;
+    for (int t = 0; t < ctx->htp->T; ++t) all_single = all_single && ctx->htp->last_in_group[t];
+    ctx->gram_lazy = all_single ? first_bulk_col(ctx, superpanel_starts(ctx, nt), nt) : nt;
+    if (ctx->gram_lazy >= nt) ctx->gram_lazy = -1;
+    ctx->gram_lazy_done = false;
+    const int g1 = ctx->gram_lazy >= 0 ? ctx->gram_lazy : nt;  // end of the second launch's columns
+    auto tri = [](double m) { return m * (m + 1) / 2; };
+    const double bpt = 8.0 * NB * NB;  // bytes per tile
+    const double b1 = bpt * (tri(nt) - tri(std::max(0, nt - ctx->spw))) + 8.0 * (double)N * (D + 1);
+    const double b2 = bpt * (tri(std::max(0, nt - ctx->spw)) - tri(nt - g1));
+    launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 1, ctx->spw, slot(ctx, 1, b1));
     HIPQ(ctx, hipEventRecord(ctx->ev_gram, ctx->s_main));
-    if (ctx->gram_queue > 0)
-        launch_gram_queue(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, ctx->spw,
-                          ctx->gram_queue, ctx->dres, slot(ctx, 1, bytes * (1.0 - frac)));
-    else
-        launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 2, ctx->spw,
-                    slot(ctx, 1, bytes * (1.0 - frac)));
+    launch_gram_queue(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, ctx->spw, g1, 2, ctx->dres,
+                      slot(ctx, 1, b2));
     HIPQ(ctx, hipEventRecord(ctx->ev_gram2, ctx->s_main));
     if (ctx->xr_mode == 1) launch_init_identity_rows(ctx->s_main, ctx->A, lda, Np, nt, ctx->spw);
     if (ctx->xr_mode == 2)
@@ -996,9 +1041,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_SERIAL")) ctx->serial = s[0] == '1';
     if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAIL_S")) ctx->tail_s = std::max(0, std::atoi(s));
-    if (const char* s = std::getenv("GAPLAC_GRAM_QUEUE")) ctx->gram_queue = std::max(0, std::min(4, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_PAIR_M")) ctx->pair_m = std::max(0, std::atoi(s));
-    if (const char* s = std::getenv("GAPLAC_PAIR_EXT")) ctx->pair_ext = std::max(0, std::min(1, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BAND_TILES_M")) ctx->band_tiles_m = std::max(1, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAILK")) ctx->tailk = s[0] != '0';
@@ -1206,8 +1249,7 @@ int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D, 
         c->dv_elems = ctx->dv_elems;
         lane[(size_t)l] = c;
     }
-    const char* tsh = std::getenv("GAPLAC_TAIL_SHARE");  // TEMPORARY measurement switch
-    for (int l = 0; l < nl; ++l) lane[(size_t)l]->tail_share = (tsh && tsh[0] == '0') ? 1 : nl;
+    for (int l = 0; l < nl; ++l) lane[(size_t)l]->tail_share = nl;
     struct ShareReset {
         std::vector<gaplac_ctx*>& ls;
         ~ShareReset() {
@@ -1450,6 +1492,7 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
     }
     TermPack tp{};
     tp.T = 1;
+    tp.last_in_group[0] = 1;  // a single-term formula: the walk takes the Gram-in-bulk schedule
     c.htp = &tp;
     LaunchGuard g;
     g.base = fake;

@@ -79,6 +79,13 @@ struct BulkArgs {
     int rect_rows = 0;
     int max_r = -1, max_c = -1;  // largest lo16 / hi16 list entry (-1: an m x m triangle list)
     int whole = 0;    // 1: a band list as 128x128 tile workgroups (tile_band_kernel), never quadrants
+    // Gram-evaluating update (tile_syrk_gram_kernel): the C tiles are computed from X / v
+    // with the terms at gtp instead of loaded (single-GPU layout, triangle list, > 512 tiles,
+    // single-term groups only)
+    const TermPack* gtp = nullptr;
+    const double* gX = nullptr;
+    const double* gv = nullptr;
+    int64_t gldx = 0, gN = 0;
 };
 
 // Persistent tail (gaplac_kernels.hip tail_kernel): completion counters of
@@ -143,8 +150,10 @@ int pack_terms(int32_t D, int32_t T, const gaplac_term* terms, TermPack* tp, std
 // block indices >= w (parts 1 + 2 = part 0).
 // Tiles of part 2 as a work queue with per_cu workgroups per CU (room for the panel
 // chain beside them); res->gram_ticket must be zero (init_result_kernel) on the same stream.
+// Tiles of tile columns w .. w1-1 only when w1 < nt (the rest is left to the first bulk
+// update, tile_syrk_gram_kernel).
 void launch_gram_queue(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const double* X, int64_t ldx,
-                       const double* v, const TermPack* dtp, int w, int per_cu, EvalResult* res, KTime* kt);
+                       const double* v, const TermPack* dtp, int w, int w1, int per_cu, EvalResult* res, KTime* kt);
 void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt,
                  const double* X, int64_t ldx, const double* v, const TermPack* dtp, int part, int w,
                  KTime* kt);

@@ -19,6 +19,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
@@ -194,14 +195,14 @@ __device__ __forceinline__ double gram_term(double xi, double xj, double p, int6
     }
 }
 
-template <int KIND, int MODE>
-__device__ __forceinline__ void gram_batch(double (&tot0)[GRAM_CB], double (&tot1)[GRAM_CB],
-                                           double (&pr0)[GRAM_CB], double (&pr1)[GRAM_CB],
+template <int KIND, int MODE, int CB>
+__device__ __forceinline__ void gram_batch(double (&tot0)[CB], double (&tot1)[CB],
+                                           double (&pr0)[CB], double (&pr1)[CB],
                                            const double* __restrict__ xc, double2 xr, double p,
                                            int64_t i0, int64_t j0, const double* __restrict__ etbl) {
 #pragma clang fp contract(off)
 #pragma unroll
-    for (int q = 0; q < GRAM_CB; ++q) {
+    for (int q = 0; q < CB; ++q) {
         const double xj = xc[4 * q];
         const int64_t j = j0 + 4 * q;
         const double k0 = gram_term<KIND>(xr.x, xj, p, i0, j, etbl);
@@ -215,18 +216,18 @@ __device__ __forceinline__ void gram_batch(double (&tot0)[GRAM_CB], double (&tot
     }
 }
 
-template <int KIND>
-__device__ __forceinline__ void gram_batch_mode(int mode, double (&tot0)[GRAM_CB], double (&tot1)[GRAM_CB],
-                                                double (&pr0)[GRAM_CB], double (&pr1)[GRAM_CB],
+template <int KIND, int CB>
+__device__ __forceinline__ void gram_batch_mode(int mode, double (&tot0)[CB], double (&tot1)[CB],
+                                                double (&pr0)[CB], double (&pr1)[CB],
                                                 const double* __restrict__ xc, double2 xr, double p,
                                                 int64_t i0, int64_t j0, const double* __restrict__ etbl) {
     switch (mode) {
-        case GM_SUM_FIRST: gram_batch<KIND, GM_SUM_FIRST>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-        case GM_SUM: gram_batch<KIND, GM_SUM>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-        case GM_PR_FIRST: gram_batch<KIND, GM_PR_FIRST>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-        case GM_PR: gram_batch<KIND, GM_PR>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-        case GM_PR_LAST0: gram_batch<KIND, GM_PR_LAST0>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-        default: gram_batch<KIND, GM_PR_LAST>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        case GM_SUM_FIRST: gram_batch<KIND, GM_SUM_FIRST, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        case GM_SUM: gram_batch<KIND, GM_SUM, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        case GM_PR_FIRST: gram_batch<KIND, GM_PR_FIRST, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        case GM_PR: gram_batch<KIND, GM_PR, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        case GM_PR_LAST0: gram_batch<KIND, GM_PR_LAST0, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        default: gram_batch<KIND, GM_PR_LAST, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
     }
 }
 
@@ -242,10 +243,13 @@ __device__ __forceinline__ void gram_batch_mode(int mode, double (&tot0)[GRAM_CB
 // (16-byte stores, a wave writes one 1 KiB column segment per instruction); the tile's
 // column coordinates are staged once in LDS and read as wave-wide broadcasts.
 // ---------------------------------------------------------------------------------
+constexpr int GRAM_LDS = 2 * GAPLAC_MAX_TERMS * NB + NB + 256;  // doubles of LDS gram_tile works in
+
+template <int CB = GRAM_CB>
 __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda, int64_t N,
                                           const double* __restrict__ X, int64_t ldx,
                                           const double* __restrict__ v,
-                                          const TermPack* __restrict__ tpp, int bi, int bj) {
+                                          const TermPack* __restrict__ tpp, int bi, int bj, double* lds) {
     // Ccol: storage of global column bj*NB (row 0); rows are global
     // No FMA contraction: KernelFunctions scales each coordinate (rounded) and then
     // differences, so equal coordinates give exactly 0 (p*xa - p*xj fused would not).
@@ -257,10 +261,10 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
     // SqExp / OU coordinates are stored already scaled (OU: p * x, rounded exactly as
     // KernelFunctions' ScaleTransform; SqExp: by p/sqrt(2), within an ulp of it);
     // Linear / Cat keep the raw coordinate.
-    __shared__ double xcol[GAPLAC_MAX_TERMS][NB];
-    __shared__ double xrow[GAPLAC_MAX_TERMS][NB];
-    __shared__ double vcol[NB];
-    __shared__ double etbl[256];
+    double (*xcol)[NB] = reinterpret_cast<double (*)[NB]>(lds);
+    double (*xrow)[NB] = xcol + GAPLAC_MAX_TERMS;
+    double* vcol = lds + 2 * GAPLAC_MAX_TERMS * NB;
+    double* etbl = vcol + NB;
     const int tid = threadIdx.x;
     const int T = tp.T;
     // Staging: thread tid owns coordinate slot c = tid % NB of the columns (tid < NB) or
@@ -297,9 +301,9 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
     const int64_t i0 = r0 + 2 * lane, i1 = i0 + 1;
     __syncthreads();
 
-    // Wave w: tile columns cc = w + 4 (cb + q), in batches of GRAM_CB columns. Kind and
+    // Wave w: tile columns cc = w + 4 (cb + q), in batches of CB columns. Kind and
     // group position are switched on once per term and batch (uniform branches); each
-    // term gives 2 GRAM_CB independent evaluations for the VALU pipeline to overlap.
+    // term gives 2 CB independent evaluations for the VALU pipeline to overlap.
     // Off the diagonal a singleton Noise group is all zeros and is skipped; interior
     // off-diagonal tiles (no padding row/column, no diagonal, no v row) store the sums
     // as they are. Formulas whose groups are all single terms (the common case) take a
@@ -334,9 +338,9 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
             *reinterpret_cast<double2*>(Ccol + (int64_t)cc * lda + i0) = make_double2(o0, o1);
         }
     };
-    auto store_batch = [&](int j0l, const double (&tot0)[GRAM_CB], const double (&tot1)[GRAM_CB]) {
+    auto store_batch = [&](int j0l, const double (&tot0)[CB], const double (&tot1)[CB]) {
 #pragma unroll
-        for (int q = 0; q < GRAM_CB; ++q) {
+        for (int q = 0; q < CB; ++q) {
             const int cc = j0l + 4 * q;
             const int64_t j = c0 + cc;
             double o0 = tot0[q], o1 = tot1[q];
@@ -353,10 +357,10 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
         }
     };
     if (all_single) {
-        for (int cb = 0; cb < NB / 4; cb += GRAM_CB) {
-            double tot0[GRAM_CB], tot1[GRAM_CB], pr0[GRAM_CB], pr1[GRAM_CB];
+        for (int cb = 0; cb < NB / 4; cb += CB) {
+            double tot0[CB], tot1[CB], pr0[CB], pr1[CB];
 #pragma unroll
-            for (int q = 0; q < GRAM_CB; ++q) tot0[q] = tot1[q] = 0.0;  // 0 + k = k
+            for (int q = 0; q < CB; ++q) tot0[q] = tot1[q] = 0.0;  // 0 + k = k
             const int j0l = wu + 4 * cb;
             for (int t = 0; t < T; ++t) {
                 const int kind = tp.kind[t];
@@ -366,19 +370,19 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
                 const double2 xr = *reinterpret_cast<const double2*>(&xrow[t][2 * lane]);
                 const int64_t j0 = c0 + j0l;
                 switch (kind) {
-                    case GAPLAC_SQEXP: gram_batch<GAPLAC_SQEXP, GM_SUM>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                    case GAPLAC_OU: gram_batch<GAPLAC_OU, GM_SUM>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                    case GAPLAC_LINEAR: gram_batch<GAPLAC_LINEAR, GM_SUM>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                    case GAPLAC_CAT: gram_batch<GAPLAC_CAT, GM_SUM>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                    default: gram_batch<GAPLAC_NOISE, GM_SUM>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                    case GAPLAC_SQEXP: gram_batch<GAPLAC_SQEXP, GM_SUM, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                    case GAPLAC_OU: gram_batch<GAPLAC_OU, GM_SUM, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                    case GAPLAC_LINEAR: gram_batch<GAPLAC_LINEAR, GM_SUM, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                    case GAPLAC_CAT: gram_batch<GAPLAC_CAT, GM_SUM, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                    default: gram_batch<GAPLAC_NOISE, GM_SUM, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
                 }
             }
             store_batch(j0l, tot0, tot1);
         }
         return;
     }
-    for (int cb = 0; cb < NB / 4; cb += GRAM_CB) {
-        double tot0[GRAM_CB], tot1[GRAM_CB], pr0[GRAM_CB], pr1[GRAM_CB];
+    for (int cb = 0; cb < NB / 4; cb += CB) {
+        double tot0[CB], tot1[CB], pr0[CB], pr1[CB];
         bool have_tot = false;
         const int j0l = wu + 4 * cb;  // tile column of q = 0
         for (int t = 0; t < T; ++t) {
@@ -394,16 +398,16 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
             const double2 xr = *reinterpret_cast<const double2*>(&xrow[t][2 * lane]);
             const int64_t j0 = c0 + j0l;
             switch (kind) {
-                case GAPLAC_SQEXP: gram_batch_mode<GAPLAC_SQEXP>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                case GAPLAC_OU: gram_batch_mode<GAPLAC_OU>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                case GAPLAC_LINEAR: gram_batch_mode<GAPLAC_LINEAR>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                case GAPLAC_CAT: gram_batch_mode<GAPLAC_CAT>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                default: gram_batch_mode<GAPLAC_NOISE>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                case GAPLAC_SQEXP: gram_batch_mode<GAPLAC_SQEXP, CB>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                case GAPLAC_OU: gram_batch_mode<GAPLAC_OU, CB>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                case GAPLAC_LINEAR: gram_batch_mode<GAPLAC_LINEAR, CB>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                case GAPLAC_CAT: gram_batch_mode<GAPLAC_CAT, CB>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                default: gram_batch_mode<GAPLAC_NOISE, CB>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
             }
         }
         if (!have_tot) {
 #pragma unroll
-            for (int q = 0; q < GRAM_CB; ++q) tot0[q] = tot1[q] = 0.0;
+            for (int q = 0; q < CB; ++q) tot0[q] = tot1[q] = 0.0;
         }
         store_batch(j0l, tot0, tot1);
     }
@@ -431,7 +435,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
         bi += w0;
         bj += w0;
     }
-    gram_tile(A + (int64_t)bj * NB * lda, lda, N, X, ldx, v, tpp, bi, bj);
+    __shared__ double glds[GRAM_LDS];
+    gram_tile(A + (int64_t)bj * NB * lda, lda, N, X, ldx, v, tpp, bi, bj, glds);
     kt_end(kt);
 }
 
@@ -446,21 +451,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
 // on every CU.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gram_queue_kernel(
     double* __restrict__ A, int64_t lda, int64_t N, const double* __restrict__ X, int64_t ldx,
-    const double* __restrict__ v, const TermPack* __restrict__ tpp, int w0, int ntiles,
+    const double* __restrict__ v, const TermPack* __restrict__ tpp, int w0, int w1, int nt, int ntiles,
     EvalResult* __restrict__ res, KTime* __restrict__ kt) {
     kt_begin(kt);
     __shared__ int s_tile;
+    __shared__ double glds[GRAM_LDS];
     for (;;) {
         __syncthreads();  // the previous tile's LDS reads are complete
         if (threadIdx.x == 0) s_tile = (int)atomicAdd(&res->gram_ticket, 1u);
         __syncthreads();
-        const int t = s_tile;
+        int t = s_tile;
         if (t >= ntiles) break;
         int bi, bj;
-        tri_index(t, bi, bj);
-        bi += w0;
-        bj += w0;
-        gram_tile(A + (int64_t)bj * NB * lda, lda, N, X, ldx, v, tpp, bi, bj);
+        if (w1 >= nt) {  // the triangle of tile blocks w0 .. nt-1
+            tri_index(t, bi, bj);
+            bi += w0;
+            bj += w0;
+        } else {  // the lower tiles of tile columns w0 .. w1-1, column by column
+            bj = w0;
+            while (t >= nt - bj) {
+                t -= nt - bj;
+                ++bj;
+            }
+            bi = bj + t;
+        }
+        gram_tile(A + (int64_t)bj * NB * lda, lda, N, X, ldx, v, tpp, bi, bj, glds);
     }
     kt_end(kt);
 }
@@ -475,7 +490,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
     kt_begin(kt);
     const uint32_t tv = tiles[blockIdx.x];
     const int bi = (int)(tv & 0xffffu), lj = (int)(tv >> 16);
-    gram_tile(C + (int64_t)lj * NB * ldc, ldc, N, X, ldx, v, tpp, bi, cm.global(lj));
+    __shared__ double glds[GRAM_LDS];
+    gram_tile(C + (int64_t)lj * NB * ldc, ldc, N, X, ldx, v, tpp, bi, cm.global(lj), glds);
     kt_end(kt);
 }
 
@@ -1372,9 +1388,11 @@ __device__ __forceinline__ void tile_decode(const BulkArgs& a, int idx, int& bi,
 // tile j) are column-major with leading dimension ldp. Lane element (mi, mj, rg) is tile
 // entry (row 64 wi + 16 mi + (lane & 15), column 64 wj + 16 mj + (lane >> 4) + 4 rg).
 // Inactive waves (upper quadrant of a diagonal tile) only help with the staging.
+typedef double MmaLds[2][2][KB][LR];  // the k-chunk staging buffers of tile_mma_neg
+static_assert(sizeof(MmaLds) >= GRAM_LDS * sizeof(double), "gram_tile reuses the staging LDS");
+
 __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const double* __restrict__ Q,
-                                             int64_t ldp, int kdepth, bool active, d4 (&acc)[4][4]) {
-    __shared__ double sm[2][2][KB][LR];
+                                             int64_t ldp, int kdepth, bool active, d4 (&acc)[4][4], MmaLds& sm) {
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
     const int wi = w & 1, wj = w >> 1;
@@ -1447,10 +1465,24 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
 #undef GAPLAC_LSTORE
 }
 
+template <bool GRAM>
 __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
     const int chunk = (a.ntiles + 7) >> 3;
-    const int idx = (b & 7) * chunk + (b >> 3);
+    int idx = (b & 7) * chunk + (b >> 3);
     if (idx >= a.ntiles) return;
+    __shared__ MmaLds sm;
+    if constexpr (GRAM) {
+        // the Gram kernel's own tile code (bitwise its values) into the tile's storage, in
+        // the staging LDS; then the tile is read back below, from this XCD's L2. Nothing
+        // computed here stays live into the k-loop (the tile is decoded again after it), so
+        // the kernel keeps the plain kernel's register count.
+        int gbi, gbj, glj;
+        tile_decode(a, idx, gbi, gbj, glj);
+        gram_tile<2>(a.C + (int64_t)glj * NB * a.ldc, a.ldc, a.gN, a.gX, a.gldx, a.gv, a.gtp, gbi, gbj, &sm[0][0][0][0]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        asm volatile("" : "+s"(idx));
+    }
     int bi, bj, lj;
     tile_decode(a, idx, bi, bj, lj);
     const int64_t r0 = (int64_t)bi * NB;
@@ -1476,7 +1508,7 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
                     acc[mi][mj][rg] = Ci[(int64_t)(64 * wj + 16 * mj + fr + 4 * rg) * ldc];
         }
     }
-    tile_mma_neg(P, Q, a.pn.ld, a.kdepth, active, acc);
+    tile_mma_neg(P, Q, a.pn.ld, a.kdepth, active, acc, sm);
     if (!active) return;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
@@ -1493,7 +1525,17 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
 // registers a quadrant chain kernel needs.
 __global__ __launch_bounds__(256, 2) void tile_syrk_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
-    tile_syrk_body(a, (int)blockIdx.x);
+    tile_syrk_body<false>(a, (int)blockIdx.x);
+    kt_end(kt);
+}
+
+// The first bulk update of the trailing tile columns with their Gram tiles built in the
+// prologue (BulkArgs::gtp set): the Gram kernel's tile code runs in the workgroup that
+// updates the tile, so the tile is read back from L2 instead of HBM, and no Gram launch
+// over these columns runs beside the first super-panels' chain.
+__global__ __launch_bounds__(256, 2) void tile_syrk_gram_kernel(BulkArgs a, KTime* __restrict__ kt) {
+    kt_begin(kt);
+    tile_syrk_body<true>(a, (int)blockIdx.x);
     kt_end(kt);
 }
 
@@ -1502,7 +1544,7 @@ __global__ __launch_bounds__(256, 2) void tile_syrk_kernel(BulkArgs a, KTime* __
 // bulk launches (tile_syrk_kernel, the roofline kernel) apart.
 __global__ __launch_bounds__(256, 2) void tile_band_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
-    tile_syrk_body(a, (int)blockIdx.x);
+    tile_syrk_body<false>(a, (int)blockIdx.x);
     kt_end(kt);
 }
 
@@ -1840,8 +1882,9 @@ __global__ __launch_bounds__(256, 2) void cinv_tile_kernel(double* __restrict__ 
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
             for (int mj = 0; mj < 4; ++mj) acc[mi][mj] = d4{0.0, 0.0, 0.0, 0.0};
+        __shared__ MmaLds sm;
         tile_mma_neg(Y + k0 * lda + (int64_t)I * NB, Y + k0 * lda + (int64_t)J * NB, lda, (int)(Np - k0), active,
-                     acc);
+                     acc, sm);
         if (active) {
             double* Ct = A + (int64_t)J * NB * lda + (int64_t)I * NB;
 #pragma unroll
@@ -2649,14 +2692,23 @@ void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const
 static int device_cus();
 
 void launch_gram_queue(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const double* X, int64_t ldx,
-                       const double* v, const TermPack* dtp, int w, int per_cu, EvalResult* res, KTime* kt) {
-    const int64_t m = nt - w;
-    const int64_t ntiles = m > 0 ? m * (m + 1) / 2 : 0;
+                       const double* v, const TermPack* dtp, int w, int w1, int per_cu, EvalResult* res, KTime* kt) {
+    w1 = std::min(w1, nt);
+    int64_t ntiles, max_b;
+    if (w1 >= nt) {
+        const int64_t m = nt - w;
+        ntiles = m > 0 ? m * (m + 1) / 2 : 0;
+        max_b = ntiles > 0 ? w + tri_row(ntiles - 1) : 0;
+    } else {
+        ntiles = 0;
+        for (int c = w; c < w1; ++c) ntiles += nt - c;
+        max_b = nt - 1;
+    }
     if (ntiles <= 0) return;
-    const int64_t max_b = w + tri_row(ntiles - 1);
-    if (!guard_launch("gram_queue_kernel", A, 0, tiles_end(lda, max_b, max_b))) return;
+    if (!guard_launch("gram_queue_kernel", A, 0, tiles_end(lda, max_b, w1 >= nt ? max_b : w1 - 1))) return;
     const int grid = (int)std::min<int64_t>(ntiles, (int64_t)per_cu * device_cus());
-    gram_queue_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(A, lda, N, X, ldx, v, dtp, w, (int)ntiles, res, kt);
+    gram_queue_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(A, lda, N, X, ldx, v, dtp, w, w1, nt, (int)ntiles,
+                                                                 res, kt);
 }
 
 void launch_gram_list(hipStream_t s, double* C, int64_t ldc, int64_t N, const double* X, int64_t ldx,
@@ -2714,7 +2766,13 @@ void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt) {
     }
     if (!guard_launch("bulk update", a.C, 0, tiles_end(a.ldc, a.bi0 + max_r, a.lj0 + max_c))) return;
     const int grid = ((a.ntiles + 7) >> 3) << 3;
-    if (syrk_is_small(a.ntiles) && !a.whole)
+    if (a.gtp) {  // the Gram-evaluating first update (the host only asks for a large one)
+        if (syrk_is_small(a.ntiles) || a.whole || a.rect_rows > 0 || a.cm.nranks != 1) {
+            guard_launch("tile_syrk_gram_kernel", a.C, 1, 0);  // not a valid request: recorded as a violation
+            return;
+        }
+        tile_syrk_gram_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
+    } else if (syrk_is_small(a.ntiles) && !a.whole)
         quad_bulk_kernel<<<dim3((unsigned)(4 * grid)), dim3(256), 0, s>>>(a, kt);
     else if (a.whole)
         tile_band_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);

@@ -5,15 +5,17 @@ these sizes) and agree with the default schedule.
 
 * GAPLAC_TAIL_S: the last tile columns factored right-looking on one stream (serial tail;
   1000 makes it everything after the first super-panel, 0 turns it off);
-* GAPLAC_GRAM_QUEUE: the second Gram launch as a work queue (0 = plain grid);
 * GAPLAC_SPW: the super-panel width;
-* GAPLAC_PAIR_M / GAPLAC_PAIR_EXT / GAPLAC_BAND_TILES_M: paired bulk updates (every other
-  step the columns beyond the next band receive two super-panels at once; 1: whenever
-  possible), with or without the second band, bands as whole tiles or quadrants;
+* GAPLAC_PAIR_M / GAPLAC_BAND_TILES_M: paired bulk updates (every other step the columns
+  beyond the next bands receive two super-panels at once; 1: whenever possible), bands as
+  whole tiles or quadrants;
 * GAPLAC_SERIAL: everything on one stream;
 * GAPLAC_TAILK=0: the serial tail as per-column launches instead of the persistent dataflow
   kernel (tail_kernel).
-The settings are read when a context is created (gaplac_ctx_create).
+The settings are read when a context is created (gaplac_ctx_create). Every schedule with a
+bulk update of more than 512 tiles (N = 9000 here) builds the Gram tiles of the columns that
+update reaches inside it (tile_syrk_gram_kernel); the product-group formula
+(PRODUCT_TERMS) takes the Gram launches for all of them instead.
 """
 import os
 
@@ -31,15 +33,12 @@ SCHEDULES = {
     "default": {},
     "serial_everything": {"GAPLAC_TAIL_S": "1000"},
     "no_serial_tail": {"GAPLAC_TAIL_S": "0"},
-    "plain_gram_grid": {"GAPLAC_GRAM_QUEUE": "0"},
-    "gram_queue_1": {"GAPLAC_GRAM_QUEUE": "1"},
     "spw3_serial8": {"GAPLAC_SPW": "3", "GAPLAC_TAIL_S": "8"},
     "spw1_no_tail": {"GAPLAC_SPW": "1", "GAPLAC_TAIL_S": "0"},
     "pair_all": {"GAPLAC_PAIR_M": "1"},
     "pair_band_whole_tiles": {"GAPLAC_PAIR_M": "1", "GAPLAC_BAND_TILES_M": "1"},
     "no_pair": {"GAPLAC_PAIR_M": "0"},
-    "pair_no_ext": {"GAPLAC_PAIR_M": "1", "GAPLAC_PAIR_EXT": "0"},
-    "pair_ext_spw3_whole": {"GAPLAC_PAIR_M": "1", "GAPLAC_PAIR_EXT": "1", "GAPLAC_SPW": "3", "GAPLAC_BAND_TILES_M": "1"},
+    "pair_spw3_whole": {"GAPLAC_PAIR_M": "1", "GAPLAC_SPW": "3", "GAPLAC_BAND_TILES_M": "1"},
     "pair_no_tail": {"GAPLAC_PAIR_M": "1", "GAPLAC_TAIL_S": "0"},
     "serial_stream": {"GAPLAC_SERIAL": "1"},
     "tail_launches": {"GAPLAC_TAILK": "0"},
@@ -48,6 +47,8 @@ SCHEDULES = {
 }
 SIZES = [1, 127, 129, 700, 2049, 3000, 9000]
 TERMS = [(SQEXP, 0, 1.5, 0), (OU, 0, 3.0, 1), (CAT, 1, 0.0, 2), (NOISE, -1, 1.0, 3)]
+# SqExp * Cat + OU (a product group: no Gram-in-bulk)
+PRODUCT_TERMS = [(SQEXP, 0, 1.5, 0), (CAT, 1, 0.0, 0), (OU, 0, 3.0, 1)]
 
 
 def inputs(N):
@@ -90,6 +91,16 @@ def test_schedules_match_oracle_and_each_other(ctxs, N):
         assert abs(ld - rd) <= 1e-12 * abs(rl), (name, ld, rd)
         assert abs(q - rq) <= 1e-12 * abs(rl), (name, q, rq)
         assert abs(lp - base[0]) <= 1e-12 * abs(rl), (name, lp, base[0])
+
+
+@pytest.mark.parametrize("N", [3000, 9000])
+def test_schedules_product_group(ctxs, N):
+    X, v = inputs(N)
+    rl, rd, rq = R.logpdf(X, PRODUCT_TERMS, 0.1, v)
+    for name in ("default", "no_pair", "serial_stream", "pair_all"):
+        lp, ld, q = ctxs[name].logpdf(X, PRODUCT_TERMS, 0.1, v, full=True)
+        assert abs(lp - rl) <= 1e-12 * abs(rl), (name, lp, rl)
+        assert abs(q - rq) <= 1e-12 * abs(rl), (name, q, rq)
 
 
 def test_serial_tail_reports_posdef_failure(ctxs):
