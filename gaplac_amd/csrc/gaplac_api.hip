@@ -73,9 +73,6 @@ struct gaplac_ctx {
     int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
     int pair_m = 40;      // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
     int ncu = 256;        // compute units of the device
-    int gram_lazy = -1;   // this evaluation: tile columns >= gram_lazy get their Gram tiles in the
-                          //   first bulk update (tile_syrk_gram_kernel), -1 = built by the Gram launches
-    bool gram_lazy_done = false;
     bool tailk = true;    // GAPLAC_TAILK: the serial tail as one persistent dataflow launch (tail_kernel)
     TailCtl* tctl = nullptr;     // its completion counters (zeroed per launch)
     uint32_t* ttasks = nullptr;  // its task list for ttasks_T tile columns
@@ -454,26 +451,6 @@ static bool pair_defer(const gaplac_ctx* ctx, const std::vector<int>& spc, int n
            p + 3 + ctx->pair_ext <= nsp && nt - spc[(size_t)p + 3 + ctx->pair_ext] >= ctx->pair_m;
 }
 
-// First tile column of the first bulk_tri update of the schedule below (the columns it
-// reaches have not been touched by any earlier update), or nt if it is not a large
-// tile-kernel launch: the columns before it are the Gram launches' (enqueue_eval_body).
-static int first_bulk_col(const gaplac_ctx* ctx, const std::vector<int>& spc, int nt) {
-    const int nsp = (int)spc.size() - 1;
-    if (nsp <= 0) return nt;
-    int j0;
-    if (pair_defer(ctx, spc, nt, 0, -1)) {
-        if (nsp < 2) return nt;  // (pair_defer needs more super-panels than this)
-        const int je = 4 <= nsp ? spc[4] : spc[(size_t)nsp];
-        const int dcol = ctx->pair_ext > 0 ? spc[4] : spc[3 <= nsp ? 3 : (size_t)nsp];
-        j0 = std::max(je, dcol);
-    } else {
-        j0 = 2 <= nsp ? spc[2] : spc[(size_t)nsp];
-    }
-    const int m = nt - j0;
-    if (m <= 0 || syrk_is_small(m * (m + 1) / 2)) return nt;
-    return j0;
-}
-
 int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     hipStream_t sm = ctx->s_main;
     hipStream_t sp = ctx->serial ? sm : ctx->s_panel;
@@ -493,14 +470,6 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         BulkArgs ba{ctx->A, lda, pn, ctx->tiles + ctx->tile_off[(size_t)m], m * (m + 1) / 2, kdep, j0, j0,
                     ColMap{1, 0, W}};
         const bool small = syrk_is_small(ba.ntiles);
-        if (j0 == ctx->gram_lazy && !ctx->gram_lazy_done) {  // these tiles' Gram entries: in the prologue
-            ba.gtp = ctx->dtp;
-            ba.gX = ctx->dX;
-            ba.gv = ctx->dv;
-            ba.gldx = N;
-            ba.gN = N;
-            ctx->gram_lazy_done = true;
-        }
         const double fl = syrk_flops(m) * (kdep / NB), by = syrk_bytes(m, kdep);
         KTime* kt = small ? slot(ctx, 6, 0) : slot(ctx, 0, fl, by);
         const bool ev = ctx->prof_mode == 2 && !small;
@@ -595,6 +564,12 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         const int ts = spc[(size_t)nsp], T = nt - ts;
         if (ctx->tailk && T <= TAIL_TMAX) {
             // the tail as one persistent dataflow launch
+            if (ctx->dry) {  // gaplac_plan_check: the task list's dependency order
+                std::vector<uint32_t> host;
+                build_tail_tasks(T, host);
+                std::string why;
+                if (!check_tail_tasks(T, host, &why)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
+            }
             if (ctx->ttasks_T != T && !ctx->dry) {
                 std::vector<uint32_t> host;
                 build_tail_tasks(T, host);
@@ -625,9 +600,6 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         HIPQ(ctx, hipEventRecord(ctx->ev_xdone, ctx->s_extra));
         HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_xdone, 0));
     }
-    if (ctx->gram_lazy >= 0 && ctx->gram_lazy < nt && !ctx->gram_lazy_done)
-        return set_err(ctx, GAPLAC_E_ARG, "schedule: no bulk update built the Gram tiles of columns >= %d",
-                       ctx->gram_lazy);
     launch_reduce(sm, ctx->A, lda, N, (int64_t)nt * NB, ColMap{1, 0, 1}, ctx->dres);
     HIPQ(ctx, hipGetLastError());
     return 0;
@@ -670,23 +642,16 @@ int enqueue_eval_body(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt)
     const int64_t lda = Np + (int64_t)NB * ctx->xr_tiles;
     launch_init_result(ctx->s_main, ctx->dres);
     if (ctx->recording) launch_kt_reset(ctx->s_main, ctx->dkt, (int)ctx->kt_cap);
-    // Gram in two launches: the first super-panel's tile columns, then the columns up to the
-    // first bulk update's (the panel chain starts on the first part while the second is
-    // still being written); the first bulk update evaluates the Gram tiles of the columns it
-    // reaches itself (tile_syrk_gram_kernel) when every group is a single term.
-    bool all_single = true;
-    for (int t = 0; t < ctx->htp->T; ++t) all_single = all_single && ctx->htp->last_in_group[t];
-    ctx->gram_lazy = all_single ? first_bulk_col(ctx, superpanel_starts(ctx, nt), nt) : nt;
-    if (ctx->gram_lazy >= nt) ctx->gram_lazy = -1;
-    ctx->gram_lazy_done = false;
-    const int g1 = ctx->gram_lazy >= 0 ? ctx->gram_lazy : nt;  // end of the second launch's columns
+    // Gram in two launches: the first super-panel's tile columns, then the rest (the panel
+    // chain starts on the first part while the second is still being written; the second as
+    // a work queue of two workgroups per CU, so the chain's kernels fit beside it, §4).
     auto tri = [](double m) { return m * (m + 1) / 2; };
     const double bpt = 8.0 * NB * NB;  // bytes per tile
     const double b1 = bpt * (tri(nt) - tri(std::max(0, nt - ctx->spw))) + 8.0 * (double)N * (D + 1);
-    const double b2 = bpt * (tri(std::max(0, nt - ctx->spw)) - tri(nt - g1));
+    const double b2 = bpt * tri(std::max(0, nt - ctx->spw));
     launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 1, ctx->spw, slot(ctx, 1, b1));
     HIPQ(ctx, hipEventRecord(ctx->ev_gram, ctx->s_main));
-    launch_gram_queue(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, ctx->spw, g1, 2, ctx->dres,
+    launch_gram_queue(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, ctx->spw, nt, 2, ctx->dres,
                       slot(ctx, 1, b2));
     HIPQ(ctx, hipEventRecord(ctx->ev_gram2, ctx->s_main));
     if (ctx->xr_mode == 1) launch_init_identity_rows(ctx->s_main, ctx->A, lda, Np, nt, ctx->spw);
@@ -1490,9 +1455,25 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
         build_grad_list((int)((N + NB - 1) / NB), gl);
         c.glist_blocks = (int)gl.size();
     }
+    c.tail_s = 48;  // as gaplac_ctx_create sets it with the persistent tail
+    {
+        // every tail length the library can launch: the task list is a topological order
+        static std::string tail_bad = [] {
+            for (int T = 1; T <= TAIL_TMAX; ++T) {
+                std::vector<uint32_t> l;
+                build_tail_tasks(T, l);
+                std::string why;
+                if (!check_tail_tasks(T, l, &why)) return why;
+            }
+            return std::string();
+        }();
+        if (!tail_bad.empty()) {
+            if (msg && msglen > 0) std::snprintf(msg, (size_t)msglen, "%s", tail_bad.c_str());
+            return GAPLAC_E_ARG;
+        }
+    }
     TermPack tp{};
     tp.T = 1;
-    tp.last_in_group[0] = 1;  // a single-term formula: the walk takes the Gram-in-bulk schedule
     c.htp = &tp;
     LaunchGuard g;
     g.base = fake;

@@ -79,18 +79,11 @@ struct BulkArgs {
     int rect_rows = 0;
     int max_r = -1, max_c = -1;  // largest lo16 / hi16 list entry (-1: an m x m triangle list)
     int whole = 0;    // 1: a band list as 128x128 tile workgroups (tile_band_kernel), never quadrants
-    // Gram-evaluating update (tile_syrk_gram_kernel): the C tiles are computed from X / v
-    // with the terms at gtp instead of loaded (single-GPU layout, triangle list, > 512 tiles,
-    // single-term groups only)
-    const TermPack* gtp = nullptr;
-    const double* gX = nullptr;
-    const double* gv = nullptr;
-    int64_t gldx = 0, gN = 0;
 };
 
 // Persistent tail (gaplac_kernels.hip tail_kernel): completion counters of
 // the tile tasks of the last T <= TAIL_TMAX tile columns, zeroed before every launch.
-constexpr int TAIL_TMAX = 64;
+constexpr int TAIL_TMAX = 128;
 struct TailCtl {
     unsigned head;  // dequeue counter
     unsigned err;   // an expired wait
@@ -111,6 +104,8 @@ struct TailArgs {
     unsigned long long* trace;  // diagnostics (GAPLAC_TAIL_TRACE): per task dequeue / start / end times, or nullptr
 };
 void build_tail_tasks(int T, std::vector<uint32_t>& out);
+// The list is a topological order of the tail's dataflow that applies every update once.
+bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why);
 void launch_tail(hipStream_t s, const TailArgs& a, int grid, KTime* kt);
 
 // Host-side footprint guard. Before launching, every launcher computes the
@@ -150,8 +145,7 @@ int pack_terms(int32_t D, int32_t T, const gaplac_term* terms, TermPack* tp, std
 // block indices >= w (parts 1 + 2 = part 0).
 // Tiles of part 2 as a work queue with per_cu workgroups per CU (room for the panel
 // chain beside them); res->gram_ticket must be zero (init_result_kernel) on the same stream.
-// Tiles of tile columns w .. w1-1 only when w1 < nt (the rest is left to the first bulk
-// update, tile_syrk_gram_kernel).
+// Tiles of tile columns w .. w1-1 only when w1 < nt.
 void launch_gram_queue(hipStream_t s, double* A, int64_t lda, int64_t N, int nt, const double* X, int64_t ldx,
                        const double* v, const TermPack* dtp, int w, int w1, int per_cu, EvalResult* res, KTime* kt);
 void launch_gram(hipStream_t s, double* A, int64_t lda, int64_t N, int nt,

@@ -1465,24 +1465,11 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
 #undef GAPLAC_LSTORE
 }
 
-template <bool GRAM>
 __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
     const int chunk = (a.ntiles + 7) >> 3;
-    int idx = (b & 7) * chunk + (b >> 3);
+    const int idx = (b & 7) * chunk + (b >> 3);
     if (idx >= a.ntiles) return;
     __shared__ MmaLds sm;
-    if constexpr (GRAM) {
-        // the Gram kernel's own tile code (bitwise its values) into the tile's storage, in
-        // the staging LDS; then the tile is read back below, from this XCD's L2. Nothing
-        // computed here stays live into the k-loop (the tile is decoded again after it), so
-        // the kernel keeps the plain kernel's register count.
-        int gbi, gbj, glj;
-        tile_decode(a, idx, gbi, gbj, glj);
-        gram_tile<2>(a.C + (int64_t)glj * NB * a.ldc, a.ldc, a.gN, a.gX, a.gldx, a.gv, a.gtp, gbi, gbj, &sm[0][0][0][0]);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        asm volatile("" : "+s"(idx));
-    }
     int bi, bj, lj;
     tile_decode(a, idx, bi, bj, lj);
     const int64_t r0 = (int64_t)bi * NB;
@@ -1525,17 +1512,7 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
 // registers a quadrant chain kernel needs.
 __global__ __launch_bounds__(256, 2) void tile_syrk_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
-    tile_syrk_body<false>(a, (int)blockIdx.x);
-    kt_end(kt);
-}
-
-// The first bulk update of the trailing tile columns with their Gram tiles built in the
-// prologue (BulkArgs::gtp set): the Gram kernel's tile code runs in the workgroup that
-// updates the tile, so the tile is read back from L2 instead of HBM, and no Gram launch
-// over these columns runs beside the first super-panels' chain.
-__global__ __launch_bounds__(256, 2) void tile_syrk_gram_kernel(BulkArgs a, KTime* __restrict__ kt) {
-    kt_begin(kt);
-    tile_syrk_body<true>(a, (int)blockIdx.x);
+    tile_syrk_body(a, (int)blockIdx.x);
     kt_end(kt);
 }
 
@@ -1544,7 +1521,7 @@ __global__ __launch_bounds__(256, 2) void tile_syrk_gram_kernel(BulkArgs a, KTim
 // bulk launches (tile_syrk_kernel, the roofline kernel) apart.
 __global__ __launch_bounds__(256, 2) void tile_band_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
-    tile_syrk_body<false>(a, (int)blockIdx.x);
+    tile_syrk_body(a, (int)blockIdx.x);
     kt_end(kt);
 }
 
@@ -2202,9 +2179,13 @@ __global__ __launch_bounds__(256) void lower_mv_reduce_kernel(const double* __re
 enum { TK_D = 0, TK_S = 1, TK_U = 2, TK_Q = 3 };
 constexpr unsigned TAIL_NQ = 10;  // Q blocks per diagonal tile (= units a diagonal U adds)
 
+// task word: type (2 bits) | q (4) | k (7) | i (7) | j (7), tile indices relative to ts
 __host__ __device__ __forceinline__ uint32_t tail_enc(int type, int q, int k, int i, int j) {
-    return (uint32_t)type | ((uint32_t)q << 2) | ((uint32_t)k << 6) | ((uint32_t)i << 12) | ((uint32_t)j << 18);
+    return (uint32_t)type | ((uint32_t)q << 2) | ((uint32_t)k << 6) | ((uint32_t)i << 13) | ((uint32_t)j << 20);
 }
+constexpr int TAIL_UD = 5;     // U task q: a whole tile with TAIL_GW columns k .. k+TAIL_GW-1 (K = 512)
+constexpr int TAIL_GW = 4;     // columns per deep update
+constexpr int TAIL_NEAR = 4;   // tile columns j < 4b + 4 + TAIL_NEAR get per-column updates in block b
 
 // Stage L_kk's 28 strictly-lower 16x16 blocks and the 8 inverses in LDS for the tail's
 // TRSM: block (b, c), c < b, at p = b(b-1)/2 + c, Ls[p*256 + m*16 + j] = L(16b + j, 16c + m);
@@ -2398,12 +2379,14 @@ __device__ __forceinline__ void tail_trsm_pipe(double* smem, unsigned* rowf, dou
     }
 }
 
-// C -= P Q^T over the K = 128 columns of tile column k, for a region of RB*32 rows x CB*64
+// C -= P Q^T over the K = 128 KD columns of tile columns k .. k+KD-1 (contiguous in
+// storage; the k-steps in order, so a deep update rounds exactly as KD successive ones),
+// for a region of RB*32 rows x CB*64
 // columns of tile column j (whole tile: RB = 4, CB = 2; quadrant: RB = 2, CB = 1). 8 waves
 // as 2 (rows) x 4 (columns), each RB x CB blocks of 16x16; fragments straight from global
 // (sc1), two groups of 4 k-steps in flight. P rows start at row0, Q rows at qrow0 (global
 // rows of the panel), C columns at ccol0 within tile column j's storage.
-template <int AUX, int RB, int CB>
+template <int AUX, int RB, int CB, int KD = 1>
 __device__ __forceinline__ void tail_update(const Gm<AUX>& gC, const Gm<AUX>& gP, int64_t lda, int row0, int ccol0,
                                             int qrow0) {
     const int tid = otid(), wave = tid >> 6, lane = tid & 63;
@@ -2441,7 +2424,7 @@ __device__ __forceinline__ void tail_update(const Gm<AUX>& gC, const Gm<AUX>& gP
                     acc[mi][mj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][st][mj], b, acc[mi][mj], 0, 0, 0);
             }
     };
-    constexpr int NG = NB / (4 * G);  // 8 groups
+    constexpr int NG = KD * NB / (4 * G);  // 8 groups per 128 panel columns
     load(0, 0);
 #pragma unroll 1
     for (int g = 0; g < NG; g += 2) {
@@ -2494,7 +2477,7 @@ __device__ __forceinline__ unsigned tail_ld(const unsigned* p) {
 }
 
 // Lane 0: wait until the task's inputs are final (bounded: 0.2 s of the 100 MHz clock).
-__device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int k, int i, int j) {
+__device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int k, int i, int j) {
     const unsigned long long t0 = wall_clock64();
     for (;;) {
         bool ok;
@@ -2504,8 +2487,10 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int k, int
             ok = tail_ld(&c->units[i * TAIL_TMAX + k]) >= 4u * k;
         } else {
             const unsigned ups = i == j ? TAIL_NQ : 4u;
-            ok = tail_ld(&c->sdone[i * TAIL_TMAX + k]) >= 2u && tail_ld(&c->sdone[j * TAIL_TMAX + k]) >= 2u &&
-                 tail_ld(&c->units[i * TAIL_TMAX + j]) >= ups * k;
+            const int nk = (type == TK_U && q == TAIL_UD) ? TAIL_GW : 1;  // panel columns k .. k+nk-1
+            ok = tail_ld(&c->units[i * TAIL_TMAX + j]) >= ups * k;
+            for (int c2 = 0; c2 < nk && ok; ++c2)
+                ok = tail_ld(&c->sdone[i * TAIL_TMAX + k + c2]) >= 2u && tail_ld(&c->sdone[j * TAIL_TMAX + k + c2]) >= 2u;
         }
         if (ok) return true;
         if (wall_clock64() - t0 > 20000000ull) return false;  // 0.2 s
@@ -2526,10 +2511,10 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         const unsigned tk = s_task;
         if (tk >= (unsigned)a.ntasks) break;
         const uint32_t e = a.tasks[tk];
-        const int type = (int)(e & 3u), q = (int)((e >> 2) & 15u), k = (int)((e >> 6) & 63u);
-        const int i = (int)((e >> 12) & 63u), j = (int)((e >> 18) & 63u);
+        const int type = (int)(e & 3u), q = (int)((e >> 2) & 15u), k = (int)((e >> 6) & 127u);
+        const int i = (int)((e >> 13) & 127u), j = (int)((e >> 20) & 127u);
         if (a.trace && threadIdx.x == 0) a.trace[3 * tk] = wall_clock64();
-        if (threadIdx.x == 0 && !tail_wait(ctl, type, k, i, j)) atomicOr(&ctl->err, 1u);
+        if (threadIdx.x == 0 && !tail_wait(ctl, type, q, k, i, j)) atomicOr(&ctl->err, 1u);
         __syncthreads();
         if (a.trace && threadIdx.x == 0) a.trace[3 * tk + 1] = wall_clock64();
         const int gk = a.ts + k;
@@ -2546,6 +2531,8 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
             const Gm<GM_SC1> gC(a.A + (int64_t)gj * NB * a.lda), gP(colk);
             if (type == TK_U && q == 0) {
                 tail_update<GM_SC1, 4, 2>(gC, gP, a.lda, gi * NB, 0, gj * NB);
+            } else if (type == TK_U && q == TAIL_UD) {
+                tail_update<GM_SC1, 4, 2, TAIL_GW>(gC, gP, a.lda, gi * NB, 0, gj * NB);
             } else if (type == TK_U) {  // quadrant q - 1 of an off-diagonal tile
                 const int qi = (q - 1) >> 1, qj = (q - 1) & 1;
                 tail_update<GM_SC1, 2, 1>(gC, gP, a.lda, gi * NB + 64 * qi, 64 * qj, gj * NB + 64 * qj);
@@ -2564,7 +2551,8 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
             } else if (type == TK_S) {  // two halves per tile: done at 2
                 __hip_atomic_fetch_add(&ctl->sdone[i * TAIL_TMAX + k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
-                const unsigned add = (type == TK_Q || q != 0) ? 1u : (i == j ? TAIL_NQ : 4u);
+                const unsigned whole = i == j ? TAIL_NQ : 4u;
+                const unsigned add = type == TK_Q ? 1u : q == 0 ? whole : q == TAIL_UD ? TAIL_GW * whole : 1u;
                 __hip_atomic_fetch_add(&ctl->units[i * TAIL_TMAX + j], add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             if (a.trace) a.trace[3 * tk + 2] = wall_clock64();
@@ -2579,11 +2567,17 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
 // needs soonest first:
 //   S(g+2,g)  Q(g+1,g+1;g) x10  U(g+2,g+1;g) x4 quadrants  D(g+1)  S(g+2,g+1) (pipelined
 //   behind D(g+1))  Q(g+2,g+2;g) x10  S(g+3,g)  U(g+3,g+1;g) x4  S(i,g) i >= g+4
-//   U(i,g+1;g) x4 i >= g+4  U(i,j;g) j >= g+2 (but (g+2,g+2))
+//   U(i,g+1;g) x4 i >= g+4  U(i,j;g) for the near tile columns g+2 <= j < 4b+4+TAIL_NEAR
+//   (but (g+2,g+2)), b = g / 4
 // after D(0) and S(1,0): the next tile column's tiles are updated in small (quadrant)
 // tasks early, so each TRSM, the one behind D(g+1) above all, and the next diagonal
 // update find their inputs final instead of queued behind the bulk of column g's updates
 // (a tile's S -> U -> S -> ... chain down the sub-diagonals must keep the chain's pace).
+// Far tiles (j >= 4b+4+TAIL_NEAR) of a complete block b of TAIL_GW columns get the block's
+// four columns in ONE deep task (K = 512: a quarter of the dequeues, waits, tile loads and
+// stores of four K = 128 tasks): those that turn near in block b+1 right after column
+// 4b+3 (before their first per-column update), the rest spread over the lists of columns
+// 4b+4 .. 4b+7, nearest tile column first, behind each column's own tasks.
 void build_tail_tasks(int T, std::vector<uint32_t>& out) {
     out.clear();
     auto S = [&](int i, int k) {
@@ -2598,9 +2592,15 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out) {
         if (i < T)
             for (int q = 1; q <= 4; ++q) out.push_back(tail_enc(TK_U, q, k, i, j));
     };
+    // block b of TAIL_GW columns is deep-updated when all its columns update something
+    auto deep_block = [&](int b) { return TAIL_GW * b + TAIL_GW - 1 <= T - 2; };
+    auto far_from = [&](int b) { return TAIL_GW * b + TAIL_GW + TAIL_NEAR; };  // first far tile column
+    std::vector<std::vector<uint32_t>> later((size_t)std::max(T, 1));  // spread deep tasks per column
     out.push_back(tail_enc(TK_D, 0, 0, 0, 0));
     S(1, 0);
     for (int g = 0; g + 1 < T; ++g) {
+        const int b = g / TAIL_GW;
+        const int jfar = deep_block(b) ? far_from(b) : T;  // per-column updates below this tile column
         S(g + 2, g);
         Qs(g + 1, g);
         Uq(g + 2, g + 1, g);
@@ -2611,10 +2611,72 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out) {
         Uq(g + 3, g + 1, g);
         for (int i = g + 4; i < T; ++i) S(i, g);
         for (int i = g + 4; i < T; ++i) Uq(i, g + 1, g);
-        for (int j = g + 2; j < T; ++j)
+        for (int j = g + 2; j < std::min(jfar, T); ++j)
             for (int i = j; i < T; ++i)
                 if (i != g + 2 || j != g + 2) out.push_back(tail_enc(TK_U, 0, g, i, j));
+        for (uint32_t e : later[(size_t)g]) out.push_back(e);
+        if (deep_block(b) && g == TAIL_GW * b + TAIL_GW - 1) {
+            // block b's deep tasks: near in block b+1 -> now; the rest -> columns g+1 .. g+4
+            const int k0 = TAIL_GW * b, jnear = deep_block(b + 1) ? far_from(b + 1) : T;
+            std::vector<uint32_t> rest;
+            for (int j = jfar; j < T; ++j)
+                for (int i = j; i < T; ++i) (j < jnear ? out : rest).push_back(tail_enc(TK_U, TAIL_UD, k0, i, j));
+            const size_t n = rest.size();
+            for (size_t x = 0; x < n; ++x) {
+                const int col = g + 1 + (int)(x * TAIL_GW / std::max<size_t>(n, 1));
+                later[(size_t)std::min(col, T - 2)].push_back(rest[x]);
+            }
+        }
     }
+}
+
+// Host check of a task list (gaplac_plan_check's dry walk): run the tasks one at a time in
+// list order, each only once its wait condition (tail_wait) holds on the tasks before it,
+// i.e. the list is a topological order of the dataflow, and at the end every tile has
+// received every column's update exactly once, every TRSM and diagonal block has run.
+bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why) {
+    std::vector<unsigned> units((size_t)T * T, 0), sdone((size_t)T * T, 0), ddone((size_t)T, 0);
+    auto fail = [&](size_t n, const char* what) {
+        char b[160];
+        std::snprintf(b, sizeof b, "tail task %zu of %zu (T = %d): %s", n, list.size(), T, what);
+        *why = b;
+        return false;
+    };
+    for (size_t n = 0; n < list.size(); ++n) {
+        const uint32_t e = list[n];
+        const int type = (int)(e & 3u), q = (int)((e >> 2) & 15u), k = (int)((e >> 6) & 127u);
+        const int i = (int)((e >> 13) & 127u), j = (int)((e >> 20) & 127u);
+        const unsigned whole = i == j ? TAIL_NQ : 4u;
+        if (type == TK_D) {
+            if (units[(size_t)k * T + k] != TAIL_NQ * (unsigned)k) return fail(n, "D before its tile is updated");
+            ddone[(size_t)k] += 1;
+        } else if (type == TK_S) {
+            if (units[(size_t)i * T + k] != 4u * (unsigned)k || i <= k) return fail(n, "S before its tile is updated");
+            if (!ddone[(size_t)k]) return fail(n, "S before D is dequeued");  // (pipelined behind D)
+            sdone[(size_t)i * T + k] += 1;
+        } else {
+            const int nk = (type == TK_U && q == TAIL_UD) ? TAIL_GW : 1;
+            if (i < j || j <= k + nk - 1) return fail(n, "update of a tile not right of its panel");
+            if (units[(size_t)i * T + j] < whole * (unsigned)k) return fail(n, "update before the tile's earlier columns");
+            for (int c = 0; c < nk; ++c)
+                if (sdone[(size_t)i * T + k + c] < 2u || sdone[(size_t)j * T + k + c] < 2u)
+                    return fail(n, "update before its panel TRSMs");
+            const unsigned add = type == TK_Q ? 1u : q == 0 ? whole : q == TAIL_UD ? TAIL_GW * whole : 1u;
+            // a whole-column step must start exactly at column k (no column skipped or repeated)
+            if ((type == TK_U && (q == 0 || q == TAIL_UD)) && units[(size_t)i * T + j] != whole * (unsigned)k)
+                return fail(n, "update repeats or skips a column");
+            units[(size_t)i * T + j] += add;
+        }
+    }
+    for (int j = 0; j < T; ++j) {
+        if (ddone[(size_t)j] != 1u) return fail(list.size(), "a diagonal block missing or repeated");
+        for (int i = j; i < T; ++i) {
+            const unsigned whole = i == j ? TAIL_NQ : 4u;
+            if (units[(size_t)i * T + j] != whole * (unsigned)j) return fail(list.size(), "a tile missed an update");
+            if (i > j && sdone[(size_t)i * T + j] != 2u) return fail(list.size(), "a TRSM missing or repeated");
+        }
+    }
+    return true;
 }
 
 // ------------------------------- launchers ---------------------------------------
@@ -2766,13 +2828,7 @@ void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt) {
     }
     if (!guard_launch("bulk update", a.C, 0, tiles_end(a.ldc, a.bi0 + max_r, a.lj0 + max_c))) return;
     const int grid = ((a.ntiles + 7) >> 3) << 3;
-    if (a.gtp) {  // the Gram-evaluating first update (the host only asks for a large one)
-        if (syrk_is_small(a.ntiles) || a.whole || a.rect_rows > 0 || a.cm.nranks != 1) {
-            guard_launch("tile_syrk_gram_kernel", a.C, 1, 0);  // not a valid request: recorded as a violation
-            return;
-        }
-        tile_syrk_gram_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
-    } else if (syrk_is_small(a.ntiles) && !a.whole)
+    if (syrk_is_small(a.ntiles) && !a.whole)
         quad_bulk_kernel<<<dim3((unsigned)(4 * grid)), dim3(256), 0, s>>>(a, kt);
     else if (a.whole)
         tile_band_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);

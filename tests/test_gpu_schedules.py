@@ -12,10 +12,8 @@ these sizes) and agree with the default schedule.
 * GAPLAC_SERIAL: everything on one stream;
 * GAPLAC_TAILK=0: the serial tail as per-column launches instead of the persistent dataflow
   kernel (tail_kernel).
-The settings are read when a context is created (gaplac_ctx_create). Every schedule with a
-bulk update of more than 512 tiles (N = 9000 here) builds the Gram tiles of the columns that
-update reaches inside it (tile_syrk_gram_kernel); the product-group formula
-(PRODUCT_TERMS) takes the Gram launches for all of them instead.
+The settings are read when a context is created (gaplac_ctx_create). A product-group
+formula (PRODUCT_TERMS) runs through the main schedules too.
 """
 import os
 
@@ -47,7 +45,7 @@ SCHEDULES = {
 }
 SIZES = [1, 127, 129, 700, 2049, 3000, 9000]
 TERMS = [(SQEXP, 0, 1.5, 0), (OU, 0, 3.0, 1), (CAT, 1, 0.0, 2), (NOISE, -1, 1.0, 3)]
-# SqExp * Cat + OU (a product group: no Gram-in-bulk)
+# SqExp * Cat + OU (a product group)
 PRODUCT_TERMS = [(SQEXP, 0, 1.5, 0), (CAT, 1, 0.0, 0), (OU, 0, 3.0, 1)]
 
 

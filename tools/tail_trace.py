@@ -25,7 +25,7 @@ def main(path):
     wait = defaultdict(list)
     by = {}
     for e, t0, t1, t2 in rows:
-        ty, q, k, i, j = e & 3, (e >> 2) & 15, (e >> 6) & 63, (e >> 12) & 63, (e >> 18) & 63
+        ty, q, k, i, j = e & 3, (e >> 2) & 15, (e >> 6) & 127, (e >> 13) & 127, (e >> 20) & 127
         dur[ty].append((t2 - t1) / 100.0)
         wait[ty].append((t1 - t0) / 100.0)
         by[(ty, q, k, i, j)] = (us(t0), us(t1), us(t2))
