@@ -97,6 +97,27 @@ struct gaplac_ctx {
     std::vector<gaplac_ctx*> lanes;
     int batch_lanes = 2;           // GAPLAC_BATCH_LANES (measured at N=8192: 1 lane 138, 2 lanes 191, 3-6 lanes 161-187 evals/s)
     int tail_share = 1;            // lanes sharing the GPU (gaplac_logpdf_batch): tail grid = CUs / share
+    int tail_whole = 80;           // GAPLAC_TAIL_WHOLE: the whole matrix in the tail when nt <= this (and TAIL_TMAX)
+    int batch_w = 4;               // GAPLAC_BATCH_W: models per tail launch when the whole matrix is in the tail
+    // the batched-tail workspace (gaplac_logpdf_batch): batch_w matrices
+    struct BatchWs {
+        double* A = nullptr;
+        size_t A_elems = 0;
+        double* Dinv = nullptr;
+        size_t Dinv_elems = 0;
+        EvalResult* dres = nullptr;
+        size_t dres_elems = 0;
+        EvalResult* hres = nullptr;  // pinned
+        TermPack* dtp = nullptr;
+        size_t dtp_elems = 0;
+        TermPack* htp = nullptr;  // pinned
+        int host_cap = 0;
+        TailCtl* ctl = nullptr;
+        size_t ctl_elems = 0;
+        uint32_t* tasks = nullptr;
+        size_t tasks_elems = 0;
+        int tasks_T = -1, tasks_B = 0, tasks_n = 0;
+    } bw;
     bool borrowed_inputs = false;  // dX / dv belong to the parent
     // Extra rows below the matrix, factored along (lda = Np + 128 xr_tiles):
     //   1 = identity rows E = [I 0] -> L^{-T} (gradient, gaplac_logpdf_grad)
@@ -404,11 +425,18 @@ void extra_rows_step(gaplac_ctx* ctx, hipStream_t sm, int64_t lda, int nt, int p
 // Super-panel boundaries: tile columns sp[p] .. sp[p+1]-1 form SP p, width spw. With a
 // serial tail (tail_s > 0, plain logpdf) the list stops at the first boundary with at
 // most tail_s tile columns after it; those columns are factored by serial_tail().
+// The whole matrix in the persistent tail (no super-panels): plain logpdf with at most
+// tail_whole (and TAIL_TMAX) tile columns.
+static bool whole_in_tail(const gaplac_ctx* ctx, int nt) {
+    return ctx->xr_mode == 0 && ctx->tailk && ctx->tail_s > 0 && nt <= TAIL_TMAX &&
+           nt <= std::max(ctx->tail_whole, ctx->tail_s);
+}
+
 static std::vector<int> superpanel_starts(const gaplac_ctx* ctx, int nt) {
     std::vector<int> sp{0};
     // a matrix the persistent tail covers whole (plain logpdf, at most TAIL_TMAX tile
     // columns, within tail_s): no super-panel at all, every column in the tail kernel
-    if (ctx->xr_mode == 0 && ctx->tailk && nt <= TAIL_TMAX && nt <= ctx->tail_s) return sp;
+    if (whole_in_tail(ctx, nt)) return sp;
     int c = 0;
     while (c < nt) {
         if (ctx->xr_mode == 0 && ctx->tail_s > 0 && c > 0 && nt - c <= ctx->tail_s) break;
@@ -988,6 +1016,79 @@ int posterior_impl(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64
 
 }  // namespace
 
+
+// Batched tail: models m0 .. m0+B-1 of a select batch whose matrix lies
+// whole in the persistent tail, evaluated together: one Gram launch and one reduction per
+// model on s_main, and ONE tail launch whose task list interleaves the B models' lists
+// task by task, so the latency-bound diagonal-block chains of B models run side by side
+// and their far-tile updates fill the chip. Each model's tasks, and so its arithmetic, are
+// those of its single evaluation: the results are bitwise the same.
+int batch_tail_eval(gaplac_ctx* ctx, int64_t N, const std::vector<TermPack>& packs, int m0, int B,
+                    double* out_logpdf, int64_t* out_info) {
+    const int64_t Np = round_up(N + 1, NB);
+    const int nt = (int)(Np / NB);
+    const int64_t lda = Np;
+    const size_t astride = (size_t)Np * (size_t)Np, dstride = (size_t)nt * DINV_PER_BLOCK;
+    gaplac_ctx::BatchWs& w = ctx->bw;
+    int rc;
+    if ((rc = ensure(ctx, &w.A, &w.A_elems, astride * (size_t)B))) return rc;
+    if ((rc = ensure(ctx, &w.Dinv, &w.Dinv_elems, dstride * (size_t)B))) return rc;
+    if ((rc = ensure(ctx, &w.dres, &w.dres_elems, (size_t)B))) return rc;
+    if ((rc = ensure(ctx, &w.dtp, &w.dtp_elems, (size_t)B))) return rc;
+    if ((rc = ensure(ctx, &w.ctl, &w.ctl_elems, (size_t)B))) return rc;
+    if (w.host_cap < B) {
+        if (w.hres) (void)hipHostFree(w.hres);
+        if (w.htp) (void)hipHostFree(w.htp);
+        w.hres = nullptr;
+        w.htp = nullptr;
+        w.host_cap = 0;
+        HIPCK(ctx, hipHostMalloc(reinterpret_cast<void**>(&w.hres), sizeof(EvalResult) * (size_t)B, 0));
+        HIPCK(ctx, hipHostMalloc(reinterpret_cast<void**>(&w.htp), sizeof(TermPack) * (size_t)B, 0));
+        w.host_cap = B;
+    }
+    if (w.tasks_T != nt || w.tasks_B != B) {
+        std::vector<uint32_t> one, all;
+        build_tail_tasks(nt, one);
+        interleave_tail_tasks(one, B, all);
+        if ((rc = ensure(ctx, &w.tasks, &w.tasks_elems, all.size()))) return rc;
+        HIPCK(ctx, hipMemcpy(w.tasks, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        w.tasks_T = nt;
+        w.tasks_B = B;
+        w.tasks_n = (int)all.size();
+    }
+    hipStream_t s = ctx->s_main;
+    for (int b = 0; b < B; ++b) w.htp[b] = packs[(size_t)(m0 + b)];
+    HIPCK(ctx, hipMemcpyAsync(w.dtp, w.htp, sizeof(TermPack) * (size_t)B, hipMemcpyHostToDevice, s));
+    LaunchGuard g;
+    g.base = w.A;
+    g.elems = (int64_t)(astride * (size_t)B);
+    {
+        GuardScope scope(&g);
+        for (int b = 0; b < B; ++b) {
+            launch_init_result(s, w.dres + b);
+            launch_gram(s, w.A + astride * (size_t)b, lda, N, nt, ctx->dX, N, ctx->dv, w.dtp + b, 0, 0, nullptr);
+        }
+        HIPCK(ctx, hipMemsetAsync(w.ctl, 0, sizeof(TailCtl) * (size_t)B, s));
+        TailArgs ta{w.A, lda, N, 0, nt, w.Dinv, w.dres, w.ctl, w.tasks, w.tasks_n, nullptr};
+        ta.a_stride = (int64_t)astride;
+        ta.dinv_stride = (int64_t)dstride;
+        ta.nmodels = B;
+        launch_tail(s, ta, std::min(ctx->ncu, w.tasks_n), nullptr);
+        for (int b = 0; b < B; ++b)
+            launch_reduce(s, w.A + astride * (size_t)b, lda, N, (int64_t)nt * NB, ColMap{1, 0, 1}, w.dres + b);
+    }
+    if (g.violations) return set_err(ctx, GAPLAC_E_ARG, "batched tail: launch footprint outside the workspace: %s",
+                                     g.first.c_str());
+    HIPCK(ctx, hipGetLastError());
+    HIPCK(ctx, hipMemcpyAsync(w.hres, w.dres, sizeof(EvalResult) * (size_t)B, hipMemcpyDeviceToHost, s));
+    HIPCK(ctx, hipStreamSynchronize(s));
+    for (int b = 0; b < B; ++b) {
+        if (w.hres[b].err) return set_err(ctx, GAPLAC_E_HIP, "batched tail: in-kernel wait expired (code %u)", w.hres[b].err);
+        out_info[m0 + b] = finish(w.hres[b], &out_logpdf[m0 + b], nullptr, nullptr);
+    }
+    return 0;
+}
+
 extern "C" {
 
 int gaplac_abi_version(void) { return GAPLAC_ABI_VERSION; }
@@ -1010,9 +1111,11 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_BAND_TILES_M")) ctx->band_tiles_m = std::max(1, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAILK")) ctx->tailk = s[0] != '0';
-    if (ctx->tailk) ctx->tail_s = 48;  // the persistent tail (A/B at N = 16384: 48 < 32 < 64 columns)
+    if (ctx->tailk) ctx->tail_s = 80;  // the persistent tail (A/B at N = 16384)
     if (const char* s = std::getenv("GAPLAC_TAIL_S")) ctx->tail_s = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_TAIL_TRACE")) ctx->ttrace_path = s;  // diagnostics
+    if (const char* s = std::getenv("GAPLAC_TAIL_WHOLE")) ctx->tail_whole = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_BATCH_W")) ctx->batch_w = std::max(1, std::min(TAIL_MAX_MODELS, std::atoi(s)));
     auto fail = [&](const char* what, hipError_t e) {
         std::fprintf(stderr, "gaplac_ctx_create: %s: %s\n", what, hipGetErrorString(e));
         gaplac_ctx_destroy(ctx);
@@ -1111,6 +1214,14 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     if (ctx->hgp) (void)hipHostFree(ctx->hgp);
     if (ctx->glist) (void)hipFree(ctx->glist);
     if (ctx->tctl) (void)hipFree(ctx->tctl);
+    if (ctx->bw.A) (void)hipFree(ctx->bw.A);
+    if (ctx->bw.Dinv) (void)hipFree(ctx->bw.Dinv);
+    if (ctx->bw.dres) (void)hipFree(ctx->bw.dres);
+    if (ctx->bw.dtp) (void)hipFree(ctx->bw.dtp);
+    if (ctx->bw.hres) (void)hipHostFree(ctx->bw.hres);
+    if (ctx->bw.htp) (void)hipHostFree(ctx->bw.htp);
+    if (ctx->bw.ctl) (void)hipFree(ctx->bw.ctl);
+    if (ctx->bw.tasks) (void)hipFree(ctx->bw.tasks);
     if (ctx->ttasks) (void)hipFree(ctx->ttasks);
     if (ctx->ttrace) (void)hipFree(ctx->ttrace);
     if (ctx->dres) (void)hipFree(ctx->dres);
@@ -1191,6 +1302,19 @@ int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D, 
         return 0;
     }
     HIPCK(ctx, hipSetDevice(ctx->device));
+    {
+        const int nt = (int)(round_up(N + 1, NB) / NB);
+        if (nmodels >= 2 && whole_in_tail(ctx, nt)) {  // batched tail
+            for (gaplac_ctx* c : ctx->lanes) HIPCK(ctx, hipStreamSynchronize(c->s_main));
+            if ((rc = upload(ctx, N, D, X, ldx, v))) return rc;
+            for (int m = 0; m < nmodels; ++m) packs[(size_t)m].noise = noise;
+            for (int m0 = 0; m0 < nmodels; m0 += ctx->batch_w) {
+                const int B = std::min(ctx->batch_w, nmodels - m0);
+                if ((rc = batch_tail_eval(ctx, N, packs, m0, B, out_logpdf, out_info))) return rc;
+            }
+            return 0;
+        }
+    }
     // the lanes borrow dX / dv: nothing of an earlier call may still read them
     for (gaplac_ctx* c : ctx->lanes) HIPCK(ctx, hipStreamSynchronize(c->s_main));
     if ((rc = upload(ctx, N, D, X, ldx, v))) return rc;

@@ -102,8 +102,17 @@ struct TailArgs {
     const uint32_t* tasks;
     int ntasks;
     unsigned long long* trace;  // diagnostics (GAPLAC_TAIL_TRACE): per task dequeue / start / end times, or nullptr
+    // several models in one launch (gaplac_logpdf_batch): task bits 27.. hold the model m,
+    // whose matrix is A + m a_stride, inverses Dinv + m dinv_stride, result res + m,
+    // counters ctl + m (ctl[0].head is the one dequeue counter)
+    int64_t a_stride = 0, dinv_stride = 0;
+    int nmodels = 1;
 };
+constexpr int TAIL_MODEL_SHIFT = 27;
+constexpr int TAIL_MAX_MODELS = 32;
 void build_tail_tasks(int T, std::vector<uint32_t>& out);
+// B models' task lists interleaved task by task (each model's own order kept)
+void interleave_tail_tasks(const std::vector<uint32_t>& one, int B, std::vector<uint32_t>& out);
 // The list is a topological order of the tail's dataflow that applies every update once.
 bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why);
 void launch_tail(hipStream_t s, const TailArgs& a, int grid, KTime* kt);

@@ -2503,32 +2503,36 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
     __shared__ unsigned s_task;
     __shared__ unsigned s_rowf[NDB];
     kt_begin(kt);
-    TailCtl* ctl = a.ctl;
     for (;;) {
         __syncthreads();
-        if (threadIdx.x == 0) s_task = atomicAdd(&ctl->head, 1u);
+        if (threadIdx.x == 0) s_task = atomicAdd(&a.ctl->head, 1u);
         __syncthreads();
         const unsigned tk = s_task;
         if (tk >= (unsigned)a.ntasks) break;
         const uint32_t e = a.tasks[tk];
         const int type = (int)(e & 3u), q = (int)((e >> 2) & 15u), k = (int)((e >> 6) & 127u);
         const int i = (int)((e >> 13) & 127u), j = (int)((e >> 20) & 127u);
+        const int m = (int)(e >> TAIL_MODEL_SHIFT);
+        TailCtl* ctl = a.ctl + m;
+        double* const A = a.A + m * a.a_stride;
+        double* const Dinv = a.Dinv + m * a.dinv_stride;
+        EvalResult* const res = a.res + m;
         if (a.trace && threadIdx.x == 0) a.trace[3 * tk] = wall_clock64();
         if (threadIdx.x == 0 && !tail_wait(ctl, type, q, k, i, j)) atomicOr(&ctl->err, 1u);
         __syncthreads();
         if (a.trace && threadIdx.x == 0) a.trace[3 * tk + 1] = wall_clock64();
         const int gk = a.ts + k;
-        double* colk = a.A + (int64_t)gk * NB * a.lda;
+        double* colk = A + (int64_t)gk * NB * a.lda;
         if (type == TK_D) {
             if ((int64_t)gk * NB < a.N)
                 potrf_diag2_body<GM_SC1>(smem, colk + (int64_t)gk * NB, a.lda, a.N, (int64_t)gk * NB,
-                                         a.Dinv + (size_t)gk * DINV_PER_BLOCK, a.res, nullptr, &ctl->dprog[k]);
+                                         Dinv + (size_t)gk * DINV_PER_BLOCK, res, nullptr, &ctl->dprog[k]);
         } else if (type == TK_S) {
-            tail_trsm_pipe<GM_SC1>(smem, s_rowf, colk, a.lda, gk, a.ts + i, q, a.Dinv + (size_t)gk * DINV_PER_BLOCK,
+            tail_trsm_pipe<GM_SC1>(smem, s_rowf, colk, a.lda, gk, a.ts + i, q, Dinv + (size_t)gk * DINV_PER_BLOCK,
                                    &ctl->dprog[k], &ctl->ddone[k], &ctl->err);
         } else {
             const int gi = a.ts + i, gj = a.ts + j;
-            const Gm<GM_SC1> gC(a.A + (int64_t)gj * NB * a.lda), gP(colk);
+            const Gm<GM_SC1> gC(A + (int64_t)gj * NB * a.lda), gP(colk);
             if (type == TK_U && q == 0) {
                 tail_update<GM_SC1, 4, 2>(gC, gP, a.lda, gi * NB, 0, gj * NB);
             } else if (type == TK_U && q == TAIL_UD) {
@@ -2558,8 +2562,15 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
             if (a.trace) a.trace[3 * tk + 2] = wall_clock64();
         }
     }
-    if (threadIdx.x == 0 && ctl->err) atomicOr(&a.res->err, 2u);
+    if (threadIdx.x < a.nmodels && a.ctl[threadIdx.x].err) atomicOr(&a.res[threadIdx.x].err, 2u);
     kt_end(kt);
+}
+
+void interleave_tail_tasks(const std::vector<uint32_t>& one, int B, std::vector<uint32_t>& out) {
+    out.clear();
+    out.reserve(one.size() * (size_t)B);
+    for (uint32_t e : one)
+        for (int m = 0; m < B; ++m) out.push_back(e | ((uint32_t)m << TAIL_MODEL_SHIFT));
 }
 
 // Dequeue order of the tail's tasks (see the block comment above). Every task waits only
@@ -2962,7 +2973,10 @@ void launch_lower_mv(hipStream_t s, const double* A, int64_t lda, int64_t N, con
 
 void launch_tail(hipStream_t s, const TailArgs& a, int grid, KTime* kt) {
     if (a.ntasks <= 0 || a.T <= 0) return;
-    if (!guard_launch("tail_kernel", a.A, 0, tiles_end(a.lda, a.ts + a.T - 1, a.ts + a.T - 1))) return;
+    if (a.nmodels < 1 || a.nmodels > TAIL_MAX_MODELS ||
+        !guard_launch("tail_kernel", a.A, 0,
+                      (int64_t)(a.nmodels - 1) * a.a_stride + tiles_end(a.lda, a.ts + a.T - 1, a.ts + a.T - 1)))
+        return;
     tail_kernel<<<dim3((unsigned)grid), dim3(512), 0, s>>>(a, kt);
 }
 

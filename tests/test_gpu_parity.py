@@ -168,8 +168,9 @@ def test_batch_matches_individual(ctx):
 
 
 def test_batch_lanes_bitwise_equal_to_single_evals(ctx):
-    """Models run concurrently on the batch lanes give exactly the single-eval results
-    (same kernels, same schedule per model), with a non-PD model in the middle."""
+    """Models evaluated together (N = 3000: the whole matrix in the persistent tail, so one
+    tail launch for 8 models) give exactly the single-eval results (same
+    kernels, same tasks per model), with a non-PD model in the middle."""
     rng = np.random.default_rng(12)
     N = 3000
     X = np.column_stack([rng.uniform(-5, 5, N), rng.uniform(0, 10, N), rng.integers(0, 900, N).astype(float)])
@@ -223,3 +224,34 @@ def test_large_n_properties(ctx):
     perm = rng.permutation(N)
     lp2 = ctx.logpdf(X[perm], terms, 0.1, v[perm])
     assert rel(lp2, lp) <= RTOL
+
+
+def test_batch_on_lanes_bitwise_equal_to_single_evals():
+    """Beyond the whole-matrix tail (GAPLAC_TAIL_WHOLE=0, N = 7000: 55 tile columns, super-
+    panels then the tail) the models run concurrently on batch lanes: again exactly the
+    single-eval results."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import os
+    old = os.environ.get("GAPLAC_TAIL_WHOLE")
+    os.environ["GAPLAC_TAIL_WHOLE"] = "0"
+    try:
+        c = Context(0)
+    finally:
+        if old is None:
+            os.environ.pop("GAPLAC_TAIL_WHOLE")
+        else:
+            os.environ["GAPLAC_TAIL_WHOLE"] = old
+    try:
+        rng = np.random.default_rng(13)
+        N = 7000
+        X = np.column_stack([rng.uniform(0, 10, N), rng.integers(0, 2000, N).astype(float)])
+        v = rng.standard_normal(N)
+        models = [[(SQEXP, 0, l, 0), (CAT, 1, 0.0, 1)] for l in (0.7, 1.5)] + [[(OU, 0, 2.0, 0)], [(SQEXP, 0, 1.0, 0)]]
+        out, info = c.logpdf_batch(X, models, 0.1, v)
+        for m, lp, inf in zip(models, out, info):
+            assert inf == 0 and lp == c.logpdf(X, m, 0.1, v)
+        ref = R.logpdf(X, models[3], 0.1, v)[0]
+        assert abs(out[3] - ref) <= 1e-9 * abs(ref)
+    finally:
+        c.close()
