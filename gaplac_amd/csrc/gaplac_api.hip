@@ -1106,7 +1106,6 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     // the schedule switches
     if (const char* s = std::getenv("GAPLAC_SERIAL")) ctx->serial = s[0] == '1';
     if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
-    if (const char* s = std::getenv("GAPLAC_TAIL_S")) ctx->tail_s = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_PAIR_M")) ctx->pair_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_BAND_TILES_M")) ctx->band_tiles_m = std::max(1, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
@@ -1579,7 +1578,7 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
         build_grad_list((int)((N + NB - 1) / NB), gl);
         c.glist_blocks = (int)gl.size();
     }
-    c.tail_s = 48;  // as gaplac_ctx_create sets it with the persistent tail
+    c.tail_s = 80;  // as gaplac_ctx_create sets it with the persistent tail
     {
         // every tail length the library can launch: the task list is a topological order
         static std::string tail_bad = [] {
