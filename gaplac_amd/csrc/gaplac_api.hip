@@ -97,8 +97,10 @@ struct gaplac_ctx {
     std::vector<gaplac_ctx*> lanes;
     int batch_lanes = 2;           // GAPLAC_BATCH_LANES (measured at N=8192: 1 lane 138, 2 lanes 191, 3-6 lanes 161-187 evals/s)
     int tail_share = 1;            // lanes sharing the GPU (gaplac_logpdf_batch): tail grid = CUs / share
-    int tail_whole = 80;           // GAPLAC_TAIL_WHOLE: the whole matrix in the tail when nt <= this (and TAIL_TMAX)
-    int batch_w = 4;               // GAPLAC_BATCH_W: models per tail launch when the whole matrix is in the tail
+    int batch_w = 32;              // GAPLAC_BATCH_W: models per tail launch when the whole matrix is in the tail
+    int batch_lag = -1;            // GAPLAC_BATCH_LAG: tile columns between consecutive models of a tail launch
+                                   // (-1: 3/8 of the matrix's tile columns)
+    int batch_gw = 8, batch_near = 2;  // the batched tail's deep-task width and near distance (A/B: §3.4)
     // the batched-tail workspace (gaplac_logpdf_batch): batch_w matrices
     struct BatchWs {
         double* A = nullptr;
@@ -116,7 +118,7 @@ struct gaplac_ctx {
         size_t ctl_elems = 0;
         uint32_t* tasks = nullptr;
         size_t tasks_elems = 0;
-        int tasks_T = -1, tasks_B = 0, tasks_n = 0;
+        int tasks_T = -1, tasks_B = 0, tasks_n = 0, tasks_lag = -1;
     } bw;
     bool borrowed_inputs = false;  // dX / dv belong to the parent
     // Extra rows below the matrix, factored along (lda = Np + 128 xr_tiles):
@@ -426,10 +428,10 @@ void extra_rows_step(gaplac_ctx* ctx, hipStream_t sm, int64_t lda, int nt, int p
 // serial tail (tail_s > 0, plain logpdf) the list stops at the first boundary with at
 // most tail_s tile columns after it; those columns are factored by serial_tail().
 // The whole matrix in the persistent tail (no super-panels): plain logpdf with at most
-// tail_whole (and TAIL_TMAX) tile columns.
+// tail_s (and TAIL_TMAX) tile columns.
 static bool whole_in_tail(const gaplac_ctx* ctx, int nt) {
     return ctx->xr_mode == 0 && ctx->tailk && ctx->tail_s > 0 && nt <= TAIL_TMAX &&
-           nt <= std::max(ctx->tail_whole, ctx->tail_s);
+           nt <= ctx->tail_s;
 }
 
 static std::vector<int> superpanel_starts(const gaplac_ctx* ctx, int nt) {
@@ -1046,14 +1048,18 @@ int batch_tail_eval(gaplac_ctx* ctx, int64_t N, const std::vector<TermPack>& pac
         HIPCK(ctx, hipHostMalloc(reinterpret_cast<void**>(&w.htp), sizeof(TermPack) * (size_t)B, 0));
         w.host_cap = B;
     }
-    if (w.tasks_T != nt || w.tasks_B != B) {
+    const int lag = ctx->batch_lag >= 0 ? ctx->batch_lag : (3 * nt + 4) / 8;
+    const int lkey = lag * 100 + ctx->batch_gw * 10 + ctx->batch_near;
+    if (w.tasks_T != nt || w.tasks_B != B || w.tasks_lag != lkey) {
         std::vector<uint32_t> one, all;
-        build_tail_tasks(nt, one);
-        interleave_tail_tasks(one, B, all);
+        std::vector<size_t> cs;
+        build_tail_tasks(nt, one, &cs, ctx->batch_gw, ctx->batch_near);
+        interleave_tail_tasks(one, cs, B, lag, all);
         if ((rc = ensure(ctx, &w.tasks, &w.tasks_elems, all.size()))) return rc;
         HIPCK(ctx, hipMemcpy(w.tasks, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         w.tasks_T = nt;
         w.tasks_B = B;
+        w.tasks_lag = lkey;
         w.tasks_n = (int)all.size();
     }
     hipStream_t s = ctx->s_main;
@@ -1113,8 +1119,8 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (ctx->tailk) ctx->tail_s = 80;  // the persistent tail (A/B at N = 16384)
     if (const char* s = std::getenv("GAPLAC_TAIL_S")) ctx->tail_s = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_TAIL_TRACE")) ctx->ttrace_path = s;  // diagnostics
-    if (const char* s = std::getenv("GAPLAC_TAIL_WHOLE")) ctx->tail_whole = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_BATCH_W")) ctx->batch_w = std::max(1, std::min(TAIL_MAX_MODELS, std::atoi(s)));
+    if (const char* s = std::getenv("GAPLAC_BATCH_LAG")) ctx->batch_lag = std::max(0, std::atoi(s));
     auto fail = [&](const char* what, hipError_t e) {
         std::fprintf(stderr, "gaplac_ctx_create: %s: %s\n", what, hipGetErrorString(e));
         gaplac_ctx_destroy(ctx);
@@ -1582,12 +1588,36 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
     {
         // every tail length the library can launch: the task list is a topological order
         static std::string tail_bad = [] {
-            for (int T = 1; T <= TAIL_TMAX; ++T) {
-                std::vector<uint32_t> l;
-                build_tail_tasks(T, l);
-                std::string why;
-                if (!check_tail_tasks(T, l, &why)) return why;
-            }
+            for (int T = 1; T <= TAIL_TMAX; ++T)
+                for (int gw : {4, 8})
+                    for (int near : {2, 3, 4, 8}) {
+                        std::vector<uint32_t> l;
+                        build_tail_tasks(T, l, nullptr, gw, near);
+                        std::string why;
+                        if (!check_tail_tasks(T, l, &why)) return why + " (gw " + std::to_string(gw) + ", near " +
+                                                                  std::to_string(near) + ")";
+                    }
+            // batched launches: each model's tasks, read out of the interleaved list, are
+            // its single list in order (so each is a topological order of its own dataflow)
+            for (int T : {1, 2, 9, 33, 65, 80})
+                for (int B : {1, 3, 32})
+                    for (int lag : {0, 1, 6, 16}) {
+                        std::vector<uint32_t> one, all;
+                        std::vector<size_t> cs;
+                        build_tail_tasks(T, one, &cs);
+                        interleave_tail_tasks(one, cs, B, lag, all);
+                        std::vector<size_t> at((size_t)B, 0);
+                        char b[128];
+                        std::snprintf(b, sizeof b, "interleaved tail list (T = %d, B = %d, lag = %d) breaks a model's order",
+                                      T, B, lag);
+                        if (all.size() != one.size() * (size_t)B) return std::string(b);
+                        for (uint32_t e : all) {
+                            const size_t m = e >> TAIL_MODEL_SHIFT;
+                            if (m >= (size_t)B || at[m] >= one.size() ||
+                                (e & ((1u << TAIL_MODEL_SHIFT) - 1)) != one[at[m]++])
+                                return std::string(b);
+                        }
+                    }
             return std::string();
         }();
         if (!tail_bad.empty()) {

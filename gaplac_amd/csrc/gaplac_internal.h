@@ -110,9 +110,17 @@ struct TailArgs {
 };
 constexpr int TAIL_MODEL_SHIFT = 27;
 constexpr int TAIL_MAX_MODELS = 32;
-void build_tail_tasks(int T, std::vector<uint32_t>& out);
-// B models' task lists interleaved task by task (each model's own order kept)
-void interleave_tail_tasks(const std::vector<uint32_t>& one, int B, std::vector<uint32_t>& out);
+// colstart (optional): index in out where the tasks of tile column g = 0 .. T-2 begin.
+// gw (4 or 8): panel columns per deep update of a far tile; near: tile columns beyond the
+// current block of gw that still get per-column updates.
+void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart = nullptr, int gw = 4,
+                      int near = 4);
+// B models' task lists interleaved (each model's own order kept, so the result is a
+// topological order per model). lag = 0: task by task, all models in step. lag > 0: a
+// software pipeline: model m runs lag * m tile columns behind model 0, and the tasks of the
+// models' current columns are interleaved task by task (colstart from build_tail_tasks).
+void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<size_t>& colstart, int B, int lag,
+                           std::vector<uint32_t>& out);
 // The list is a topological order of the tail's dataflow that applies every update once.
 bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why);
 void launch_tail(hipStream_t s, const TailArgs& a, int grid, KTime* kt);

@@ -1433,10 +1433,10 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
         }                                                                              \
     } while (0)
 
+    const int NCH = kdepth / KB;
     GAPLAC_GLOAD(0);
     GAPLAC_LSTORE(0);
     __syncthreads();
-    const int NCH = kdepth / KB;
     for (int ch = 0; ch < NCH; ++ch) {
         const int buf = ch & 1;
         const bool more = ch + 1 < NCH;
@@ -2183,9 +2183,12 @@ constexpr unsigned TAIL_NQ = 10;  // Q blocks per diagonal tile (= units a diago
 __host__ __device__ __forceinline__ uint32_t tail_enc(int type, int q, int k, int i, int j) {
     return (uint32_t)type | ((uint32_t)q << 2) | ((uint32_t)k << 6) | ((uint32_t)i << 13) | ((uint32_t)j << 20);
 }
-constexpr int TAIL_UD = 5;     // U task q: a whole tile with TAIL_GW columns k .. k+TAIL_GW-1 (K = 512)
-constexpr int TAIL_GW = 4;     // columns per deep update
-constexpr int TAIL_NEAR = 4;   // tile columns j < 4b + 4 + TAIL_NEAR get per-column updates in block b
+constexpr int TAIL_UD = 5;     // U task q: a whole tile with the 4 columns k .. k+3 (K = 512)
+constexpr int TAIL_UD8 = 6;    // U task q: a whole tile with the 8 columns k .. k+7 (K = 1024)
+// panel columns a task applies (deep U tasks 4 or 8, every other update 1)
+__host__ __device__ __forceinline__ int tail_deep_cols(int type, int q) {
+    return type == TK_U ? (q == TAIL_UD ? 4 : q == TAIL_UD8 ? 8 : 1) : 1;
+}
 
 // Stage L_kk's 28 strictly-lower 16x16 blocks and the 8 inverses in LDS for the tail's
 // TRSM: block (b, c), c < b, at p = b(b-1)/2 + c, Ls[p*256 + m*16 + j] = L(16b + j, 16c + m);
@@ -2442,6 +2445,15 @@ __device__ __forceinline__ void tail_update(const Gm<AUX>& gC, const Gm<AUX>& gP
                 gC.st((uint32_t)((int64_t)(c0 + 16 * mj + fr + 4 * rg) * lda + r0 + 16 * mi + fc), acc[mi][mj][rg]);
 }
 
+// The whole-tile update C -= P Q^T over the K = 128 KD columns of tile columns
+// k .. k+KD-1, panels staged in LDS: per chunk of 16 panel columns each wave moves four
+// 1 KB column segments (P rows row0.. by waves 0-3, Q rows qrow0.. by waves 4-7) with
+// LDS-DMA (global_load_lds, 16 B per lane, sc1 like every load of handed-off data), two
+// chunk buffers, the next chunk in flight while the current one is multiplied. Each wave
+// reads its fragments from LDS: one copy of each panel row per workgroup instead of one per
+// wave that uses it (tail_update reads P 4x and Q 2x from L2). The 8 waves, their 4x2
+// blocks of 16x16 and the MFMA sequence per accumulator are tail_update<AUX, 4, 2, KD>'s:
+// bitwise the same result.
 // One 32x32 block of C -= P Q^T, K = 128 (the critical diagonal-tile update, split ten
 // ways): waves 0-3 take one 16x16 sub-block each and load all 32 k-steps of their two
 // fragments before the first MFMA, so the handed-off panel's memory latency is paid once.
@@ -2487,7 +2499,7 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int
             ok = tail_ld(&c->units[i * TAIL_TMAX + k]) >= 4u * k;
         } else {
             const unsigned ups = i == j ? TAIL_NQ : 4u;
-            const int nk = (type == TK_U && q == TAIL_UD) ? TAIL_GW : 1;  // panel columns k .. k+nk-1
+            const int nk = tail_deep_cols(type, q);  // panel columns k .. k+nk-1
             ok = tail_ld(&c->units[i * TAIL_TMAX + j]) >= ups * k;
             for (int c2 = 0; c2 < nk && ok; ++c2)
                 ok = tail_ld(&c->sdone[i * TAIL_TMAX + k + c2]) >= 2u && tail_ld(&c->sdone[j * TAIL_TMAX + k + c2]) >= 2u;
@@ -2536,7 +2548,9 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
             if (type == TK_U && q == 0) {
                 tail_update<GM_SC1, 4, 2>(gC, gP, a.lda, gi * NB, 0, gj * NB);
             } else if (type == TK_U && q == TAIL_UD) {
-                tail_update<GM_SC1, 4, 2, TAIL_GW>(gC, gP, a.lda, gi * NB, 0, gj * NB);
+                tail_update<GM_SC1, 4, 2, 4>(gC, gP, a.lda, gi * NB, 0, gj * NB);
+            } else if (type == TK_U && q == TAIL_UD8) {
+                tail_update<GM_SC1, 4, 2, 8>(gC, gP, a.lda, gi * NB, 0, gj * NB);
             } else if (type == TK_U) {  // quadrant q - 1 of an off-diagonal tile
                 const int qi = (q - 1) >> 1, qj = (q - 1) & 1;
                 tail_update<GM_SC1, 2, 1>(gC, gP, a.lda, gi * NB + 64 * qi, 64 * qj, gj * NB + 64 * qj);
@@ -2556,7 +2570,8 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
                 __hip_atomic_fetch_add(&ctl->sdone[i * TAIL_TMAX + k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 const unsigned whole = i == j ? TAIL_NQ : 4u;
-                const unsigned add = type == TK_Q ? 1u : q == 0 ? whole : q == TAIL_UD ? TAIL_GW * whole : 1u;
+                const int nk = tail_deep_cols(type, q);
+                const unsigned add = type == TK_Q ? 1u : q == 0 ? whole : nk > 1 ? (unsigned)nk * whole : 1u;
                 __hip_atomic_fetch_add(&ctl->units[i * TAIL_TMAX + j], add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             if (a.trace) a.trace[3 * tk + 2] = wall_clock64();
@@ -2566,11 +2581,36 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
     kt_end(kt);
 }
 
-void interleave_tail_tasks(const std::vector<uint32_t>& one, int B, std::vector<uint32_t>& out) {
+void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<size_t>& colstart, int B, int lag,
+                           std::vector<uint32_t>& out) {
     out.clear();
     out.reserve(one.size() * (size_t)B);
-    for (uint32_t e : one)
-        for (int m = 0; m < B; ++m) out.push_back(e | ((uint32_t)m << TAIL_MODEL_SHIFT));
+    auto tag = [](uint32_t e, int m) { return e | ((uint32_t)m << TAIL_MODEL_SHIFT); };
+    if (lag <= 0 || colstart.empty()) {
+        for (uint32_t e : one)
+            for (int m = 0; m < B; ++m) out.push_back(tag(e, m));
+        return;
+    }
+    // column g of the list: [colstart[g], colstart[g+1]) (the last runs to the end)
+    const int ncol = (int)colstart.size();
+    auto col_end = [&](int g) { return g + 1 < ncol ? colstart[(size_t)g + 1] : one.size(); };
+    std::vector<size_t> pos((size_t)B);
+    for (int step = 0; step < ncol + lag * (B - 1); ++step) {
+        // the models whose current column is step - lag * m, their tasks task by task
+        for (int m = 0; m < B; ++m) {
+            const int g = step - lag * m;
+            pos[(size_t)m] = (g >= 0 && g < ncol) ? colstart[(size_t)g] : 0;
+        }
+        for (bool any = true; any;) {
+            any = false;
+            for (int m = 0; m < B; ++m) {
+                const int g = step - lag * m;
+                if (g < 0 || g >= ncol || pos[(size_t)m] >= col_end(g)) continue;
+                out.push_back(tag(one[pos[(size_t)m]++], m));
+                any = true;
+            }
+        }
+    }
 }
 
 // Dequeue order of the tail's tasks (see the block comment above). Every task waits only
@@ -2578,19 +2618,25 @@ void interleave_tail_tasks(const std::vector<uint32_t>& one, int B, std::vector<
 // needs soonest first:
 //   S(g+2,g)  Q(g+1,g+1;g) x10  U(g+2,g+1;g) x4 quadrants  D(g+1)  S(g+2,g+1) (pipelined
 //   behind D(g+1))  Q(g+2,g+2;g) x10  S(g+3,g)  U(g+3,g+1;g) x4  S(i,g) i >= g+4
-//   U(i,g+1;g) x4 i >= g+4  U(i,j;g) for the near tile columns g+2 <= j < 4b+4+TAIL_NEAR
+//   U(i,g+1;g) x4 i >= g+4  U(i,j;g) for the near tile columns g+2 <= j < 4b+4+NEAR
 //   (but (g+2,g+2)), b = g / 4
 // after D(0) and S(1,0): the next tile column's tiles are updated in small (quadrant)
 // tasks early, so each TRSM, the one behind D(g+1) above all, and the next diagonal
 // update find their inputs final instead of queued behind the bulk of column g's updates
 // (a tile's S -> U -> S -> ... chain down the sub-diagonals must keep the chain's pace).
-// Far tiles (j >= 4b+4+TAIL_NEAR) of a complete block b of TAIL_GW columns get the block's
-// four columns in ONE deep task (K = 512: a quarter of the dequeues, waits, tile loads and
-// stores of four K = 128 tasks): those that turn near in block b+1 right after column
-// 4b+3 (before their first per-column update), the rest spread over the lists of columns
-// 4b+4 .. 4b+7, nearest tile column first, behind each column's own tasks.
-void build_tail_tasks(int T, std::vector<uint32_t>& out) {
+// Far tiles (j >= GW b + GW + NEAR) of a complete block b of GW (4 or 8) columns get the
+// block's columns in ONE deep task (K = 128 GW: 1/GW of the dequeues, waits, tile loads and
+// stores of GW K = 128 tasks): those that turn near in block b+1 right after column
+// GW b + GW - 1 (before their first per-column update), the rest spread over the lists of
+// the block's next GW columns, nearest tile column first, behind each column's own tasks.
+// Single evaluations use GW = 4, NEAR = 4 (latency); batched launches fewer per-column
+// updates (throughput).
+void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart, int gw, int near) {
+    // deep width; near distance (>= 2: the next two diagonal tiles take per-column Q tasks)
+    const int GW = gw == 8 ? 8 : 4, NEAR = std::max(2, near);
+    const int qdeep = GW == 8 ? TAIL_UD8 : TAIL_UD;
     out.clear();
+    if (colstart) colstart->clear();
     auto S = [&](int i, int k) {
         if (i < T)
             for (int h = 0; h < 2; ++h) out.push_back(tail_enc(TK_S, h, k, i, 0));  // row halves
@@ -2603,14 +2649,15 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out) {
         if (i < T)
             for (int q = 1; q <= 4; ++q) out.push_back(tail_enc(TK_U, q, k, i, j));
     };
-    // block b of TAIL_GW columns is deep-updated when all its columns update something
-    auto deep_block = [&](int b) { return TAIL_GW * b + TAIL_GW - 1 <= T - 2; };
-    auto far_from = [&](int b) { return TAIL_GW * b + TAIL_GW + TAIL_NEAR; };  // first far tile column
+    // block b of GW columns is deep-updated when all its columns update something
+    auto deep_block = [&](int b) { return GW * b + GW - 1 <= T - 2; };
+    auto far_from = [&](int b) { return GW * b + GW + NEAR; };  // first far tile column
     std::vector<std::vector<uint32_t>> later((size_t)std::max(T, 1));  // spread deep tasks per column
     out.push_back(tail_enc(TK_D, 0, 0, 0, 0));
     S(1, 0);
     for (int g = 0; g + 1 < T; ++g) {
-        const int b = g / TAIL_GW;
+        if (colstart) colstart->push_back(g == 0 ? 0 : out.size());
+        const int b = g / GW;
         const int jfar = deep_block(b) ? far_from(b) : T;  // per-column updates below this tile column
         S(g + 2, g);
         Qs(g + 1, g);
@@ -2626,15 +2673,15 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out) {
             for (int i = j; i < T; ++i)
                 if (i != g + 2 || j != g + 2) out.push_back(tail_enc(TK_U, 0, g, i, j));
         for (uint32_t e : later[(size_t)g]) out.push_back(e);
-        if (deep_block(b) && g == TAIL_GW * b + TAIL_GW - 1) {
+        if (deep_block(b) && g == GW * b + GW - 1) {
             // block b's deep tasks: near in block b+1 -> now; the rest -> columns g+1 .. g+4
-            const int k0 = TAIL_GW * b, jnear = deep_block(b + 1) ? far_from(b + 1) : T;
+            const int k0 = GW * b, jnear = deep_block(b + 1) ? far_from(b + 1) : T;
             std::vector<uint32_t> rest;
             for (int j = jfar; j < T; ++j)
-                for (int i = j; i < T; ++i) (j < jnear ? out : rest).push_back(tail_enc(TK_U, TAIL_UD, k0, i, j));
+                for (int i = j; i < T; ++i) (j < jnear ? out : rest).push_back(tail_enc(TK_U, qdeep, k0, i, j));
             const size_t n = rest.size();
             for (size_t x = 0; x < n; ++x) {
-                const int col = g + 1 + (int)(x * TAIL_GW / std::max<size_t>(n, 1));
+                const int col = g + 1 + (int)(x * GW / std::max<size_t>(n, 1));
                 later[(size_t)std::min(col, T - 2)].push_back(rest[x]);
             }
         }
@@ -2666,15 +2713,15 @@ bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why
             if (!ddone[(size_t)k]) return fail(n, "S before D is dequeued");  // (pipelined behind D)
             sdone[(size_t)i * T + k] += 1;
         } else {
-            const int nk = (type == TK_U && q == TAIL_UD) ? TAIL_GW : 1;
+            const int nk = tail_deep_cols(type, q);
             if (i < j || j <= k + nk - 1) return fail(n, "update of a tile not right of its panel");
             if (units[(size_t)i * T + j] < whole * (unsigned)k) return fail(n, "update before the tile's earlier columns");
             for (int c = 0; c < nk; ++c)
                 if (sdone[(size_t)i * T + k + c] < 2u || sdone[(size_t)j * T + k + c] < 2u)
                     return fail(n, "update before its panel TRSMs");
-            const unsigned add = type == TK_Q ? 1u : q == 0 ? whole : q == TAIL_UD ? TAIL_GW * whole : 1u;
+            const unsigned add = type == TK_Q ? 1u : q == 0 ? whole : nk > 1 ? (unsigned)nk * whole : 1u;
             // a whole-column step must start exactly at column k (no column skipped or repeated)
-            if ((type == TK_U && (q == 0 || q == TAIL_UD)) && units[(size_t)i * T + j] != whole * (unsigned)k)
+            if ((type == TK_U && (q == 0 || nk > 1)) && units[(size_t)i * T + j] != whole * (unsigned)k)
                 return fail(n, "update repeats or skips a column");
             units[(size_t)i * T + j] += add;
         }

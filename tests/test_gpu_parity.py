@@ -227,21 +227,21 @@ def test_large_n_properties(ctx):
 
 
 def test_batch_on_lanes_bitwise_equal_to_single_evals():
-    """Beyond the whole-matrix tail (GAPLAC_TAIL_WHOLE=0, N = 7000: 55 tile columns, super-
+    """Beyond the whole-matrix tail (GAPLAC_TAIL_S=32, N = 7000: 55 tile columns, super-
     panels then the tail) the models run concurrently on batch lanes: again exactly the
     single-eval results."""
     if not gpu_available():
         pytest.skip("no GPU")
     import os
-    old = os.environ.get("GAPLAC_TAIL_WHOLE")
-    os.environ["GAPLAC_TAIL_WHOLE"] = "0"
+    old = os.environ.get("GAPLAC_TAIL_S")
+    os.environ["GAPLAC_TAIL_S"] = "32"
     try:
         c = Context(0)
     finally:
         if old is None:
-            os.environ.pop("GAPLAC_TAIL_WHOLE")
+            os.environ.pop("GAPLAC_TAIL_S")
         else:
-            os.environ["GAPLAC_TAIL_WHOLE"] = old
+            os.environ["GAPLAC_TAIL_S"] = old
     try:
         rng = np.random.default_rng(13)
         N = 7000

@@ -12,7 +12,9 @@ these sizes) and agree with the default schedule.
 * GAPLAC_SERIAL: everything on one stream;
 * GAPLAC_TAILK=0: the serial tail as per-column launches instead of the persistent dataflow
   kernel (tail_kernel, DESIGN.md §3.3);
-* GAPLAC_TAIL_WHOLE: the whole matrix in the persistent tail up to this many tile columns.
+A matrix with at most GAPLAC_TAIL_S tile columns lies whole in the persistent tail (library
+default 80); the schedules here run with 32 unless they say otherwise, so the larger sizes
+go through super-panels and then the tail.
 The settings are read when a context is created (gaplac_ctx_create). A product-group
 formula (PRODUCT_TERMS) runs through the main schedules too.
 """
@@ -43,8 +45,8 @@ SCHEDULES = {
     "tail_launches": {"GAPLAC_TAILK": "0"},
     "tailk_everything": {"GAPLAC_TAIL_S": "1000"},
     "tailk_spw1": {"GAPLAC_SPW": "1", "GAPLAC_TAIL_S": "40"},
-    "whole_tail_80": {"GAPLAC_TAIL_WHOLE": "80"},
-    "whole_tail_128": {"GAPLAC_TAIL_WHOLE": "128"},
+    "whole_tail_80": {"GAPLAC_TAIL_S": "80"},
+    "whole_tail_128": {"GAPLAC_TAIL_S": "128"},
 }
 SIZES = [1, 127, 129, 700, 2049, 3000, 9000]
 TERMS = [(SQEXP, 0, 1.5, 0), (OU, 0, 3.0, 1), (CAT, 1, 0.0, 2), (NOISE, -1, 1.0, 3)]
@@ -59,9 +61,9 @@ def inputs(N):
 
 
 def make_ctx(env):
-    # the super-panel schedules at these sizes: the whole matrix goes to the tail only up to
-    # GAPLAC_TAIL_S tile columns, except where a schedule says otherwise
-    env = {"GAPLAC_TAIL_WHOLE": "0", **env}
+    # the super-panel schedules at these sizes: a 32-column tail, except where a schedule
+    # says otherwise (the library default, 80, puts every size here whole in the tail)
+    env = {"GAPLAC_TAIL_S": "32", **env}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:

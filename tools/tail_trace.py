@@ -33,6 +33,22 @@ def main(path):
         d, w = dur[ty], wait[ty]
         print(f"{NAMES[ty]}: n={len(d):5d} exec mean {sum(d) / len(d):7.2f} us max {max(d):7.2f}  "
               f"wait mean {sum(w) / len(w):7.2f} max {max(w):7.2f}")
+    # U tasks by shape, with their MFMA rate per workgroup (fp64 peak per CU = 78.6/256 TF/s)
+    ushape = defaultdict(list)
+    for (ty, q, k, i, j), (t0, t1, t2) in by.items():
+        if ty == 2:
+            ushape["K=512 tile" if q == 5 else "K=128 tile" if q == 0 else "K=128 quadrant"].append(t2 - t1)
+    flops = {"K=512 tile": 2 * 128 * 128 * 512, "K=128 tile": 2 * 128 * 128 * 128, "K=128 quadrant": 2 * 64 * 64 * 128}
+    for name, d in sorted(ushape.items()):
+        m = sum(d) / len(d)
+        print(f"  U {name:15s} n={len(d):5d} exec mean {m:7.2f} us = {flops[name] / m / 1e6:.3f} TF/s per CU "
+              f"({flops[name] / m / 1e6 / (78.6 / 256):.2f} of peak)")
+    span = (max(r[3] for r in rows) - base) / 100.0
+    ex = sum(sum(d) for d in dur.values())
+    wt = sum(sum(w) for w in wait.values())
+    grid = 256
+    print(f"span {span:.1f} us; over {grid} workgroups: exec {ex / (grid * span):.3f}, wait {wt / (grid * span):.3f}, "
+          f"rest (dequeue, idle) {1 - (ex + wt) / (grid * span):.3f}")
     T = max(k for (_, _, k, _, _) in by) + 2
     print(f"{'k':>3} {'D start':>9} {'D end':>9} {'S start':>9} {'S end':>9} {'Q start':>9} {'Q end':>9} {'D+1 deq':>9}")
     for k in range(T - 1):
