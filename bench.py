@@ -216,6 +216,7 @@ def main():
     two = None
     n4096 = None
     n65536 = None
+    select4 = None
     if full_run and rank == 0:
         models = [terms_for(LENGTHSCALES[i % len(LENGTHSCALES)]) for i in range(8)]
         ctx.logpdf_batch(X, models[:2], CF.NOISE_VAR, v)
@@ -225,6 +226,7 @@ def main():
         two = 16 / (time.perf_counter() - tb)
         n4096 = measure_config1(ctx, torch)
         n65536 = measure_config3_single(local_rank, torch)
+        select4 = measure_config4(local_rank, torch)
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -283,6 +285,7 @@ def main():
         "two_chains_evals_per_s": two,
         "n4096": n4096,
         "n65536": n65536,
+        "select": select4,
         "dist": dist_line,
     }
     if gram_alone:
@@ -405,6 +408,37 @@ def measure_config3_single(local_rank: int, torch, steps: int = 2):
     return {"workload": f"BASELINE configs[3] workload on 1 GPU: SqExp(:x; l=1.5), N={N}, noise 0.1",
             "evals_per_s": 1.0 / dt, "ms_per_eval": dt * 1e3, "steps": steps, "last_logpdf": lp,
             "roofline": {"bound": "mfma", "kernel": "whole evaluation (F = N^3/3 + N^2)", "achieved": round(tf, 3),
+                         "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / PEAK_F64_TFLOPS, 4)}}
+
+
+def measure_config4(local_rank: int, torch, steps: int = 2):
+    """BASELINE configs[4] (select: 64 candidate formulas at N=8192, one gaplac_logpdf_batch
+    call per step, the batched persistent tail of DESIGN.md §3.4) on this GPU, as an extra
+    beside the headline; --mode select runs the same workload on its own. Its own context,
+    freed afterwards."""
+    from gaplac_amd.backend import Context
+    N = CF.N4
+    X, y = CF.config4_inputs(N)
+    models = select_models()
+    c = Context(local_rank)
+    try:
+        c.logpdf_batch(X, models, CF.NOISE_VAR, y)  # warmup: workspaces, task lists
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = None
+        for _ in range(steps):
+            out, _ = c.logpdf_batch(X, models, CF.NOISE_VAR, y)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+    finally:
+        c.close()
+        torch.cuda.empty_cache()
+    flops = len(models) * (N ** 3 / 3.0 + N ** 2)
+    tf = flops / dt / 1e12
+    return {"workload": f"BASELINE configs[4]: {len(models)} candidate formulas, N={N}, noise 0.1 (host inputs)",
+            "evals_per_s": len(models) / dt, "ms_per_step": dt * 1e3, "steps": steps,
+            "n_finite": int(np.isfinite(out).sum()),
+            "roofline": {"bound": "mfma", "kernel": "whole batch (64 x (N^3/3 + N^2))", "achieved": round(tf, 3),
                          "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / PEAK_F64_TFLOPS, 4)}}
 
 

@@ -100,7 +100,11 @@ struct gaplac_ctx {
     int batch_w = 32;              // GAPLAC_BATCH_W: models per tail launch when the whole matrix is in the tail
     int batch_lag = -1;            // GAPLAC_BATCH_LAG: tile columns between consecutive models of a tail launch
                                    // (-1: 3/8 of the matrix's tile columns)
+#ifndef GAPLAC_BATCH_QUADS
+#define GAPLAC_BATCH_QUADS 1
+#endif
     int batch_gw = 8, batch_near = 2;  // the batched tail's deep-task width and near distance (A/B: §3.4)
+    bool batch_quads = GAPLAC_BATCH_QUADS;
     // the batched-tail workspace (gaplac_logpdf_batch): batch_w matrices
     struct BatchWs {
         double* A = nullptr;
@@ -119,7 +123,10 @@ struct gaplac_ctx {
         uint32_t* tasks = nullptr;
         size_t tasks_elems = 0;
         int tasks_T = -1, tasks_B = 0, tasks_n = 0, tasks_lag = -1;
-    } bw;
+        hipEvent_t ev_gram = nullptr, ev_done = nullptr;  // Grams written (s_panel); launch retired (s_main)
+        bool busy = false;                                // a launch on this set is in flight
+        int m0 = 0, B = 0;                                // its models
+    } bw[2];  // two sets: one launch's Grams overlap the previous launch's tail
     bool borrowed_inputs = false;  // dX / dv belong to the parent
     // Extra rows below the matrix, factored along (lda = Np + 128 xr_tiles):
     //   1 = identity rows E = [I 0] -> L^{-T} (gradient, gaplac_logpdf_grad)
@@ -1020,24 +1027,30 @@ int posterior_impl(gaplac_ctx* ctx, int64_t N, int32_t D, const double* X, int64
 
 
 // Batched tail: models m0 .. m0+B-1 of a select batch whose matrix lies
-// whole in the persistent tail, evaluated together: one Gram launch and one reduction per
-// model on s_main, and ONE tail launch whose task list interleaves the B models' lists
-// task by task, so the latency-bound diagonal-block chains of B models run side by side
-// and their far-tile updates fill the chip. Each model's tasks, and so its arithmetic, are
-// those of its single evaluation: the results are bitwise the same.
-int batch_tail_eval(gaplac_ctx* ctx, int64_t N, const std::vector<TermPack>& packs, int m0, int B,
-                    double* out_logpdf, int64_t* out_info) {
+// whole in the persistent tail, evaluated together on workspace set p: the Grams and
+// result records on s_panel (so they run beside the previous launch's tail on s_main),
+// then on s_main ONE tail launch whose task list interleaves the B models' lists as a
+// software pipeline (interleave_tail_tasks), and one reduction per model. Each model's
+// tasks, and so its arithmetic, are those of its single evaluation: the results are
+// bitwise the same. Nothing here waits for the launch; batch_tail_finish collects it.
+static int batch_tail_finish(gaplac_ctx* ctx, int p, double* out_logpdf, int64_t* out_info);
+
+static int batch_tail_enqueue(gaplac_ctx* ctx, int64_t N, const std::vector<TermPack>& packs, int m0, int B, int p,
+                              double* out_logpdf, int64_t* out_info) {
     const int64_t Np = round_up(N + 1, NB);
     const int nt = (int)(Np / NB);
     const int64_t lda = Np;
     const size_t astride = (size_t)Np * (size_t)Np, dstride = (size_t)nt * DINV_PER_BLOCK;
-    gaplac_ctx::BatchWs& w = ctx->bw;
+    gaplac_ctx::BatchWs& w = ctx->bw[p];
     int rc;
+    if (w.busy && (rc = batch_tail_finish(ctx, p, out_logpdf, out_info))) return rc;  // the set's last launch
     if ((rc = ensure(ctx, &w.A, &w.A_elems, astride * (size_t)B))) return rc;
     if ((rc = ensure(ctx, &w.Dinv, &w.Dinv_elems, dstride * (size_t)B))) return rc;
     if ((rc = ensure(ctx, &w.dres, &w.dres_elems, (size_t)B))) return rc;
     if ((rc = ensure(ctx, &w.dtp, &w.dtp_elems, (size_t)B))) return rc;
     if ((rc = ensure(ctx, &w.ctl, &w.ctl_elems, (size_t)B))) return rc;
+    if (!w.ev_gram) HIPCK(ctx, hipEventCreateWithFlags(&w.ev_gram, hipEventDisableTiming));
+    if (!w.ev_done) HIPCK(ctx, hipEventCreateWithFlags(&w.ev_done, hipEventDisableTiming));
     if (w.host_cap < B) {
         if (w.hres) (void)hipHostFree(w.hres);
         if (w.htp) (void)hipHostFree(w.htp);
@@ -1049,11 +1062,11 @@ int batch_tail_eval(gaplac_ctx* ctx, int64_t N, const std::vector<TermPack>& pac
         w.host_cap = B;
     }
     const int lag = ctx->batch_lag >= 0 ? ctx->batch_lag : (3 * nt + 4) / 8;
-    const int lkey = lag * 100 + ctx->batch_gw * 10 + ctx->batch_near;
+    const int lkey = lag * 1000 + ctx->batch_gw * 100 + ctx->batch_near * 10 + (ctx->batch_quads ? 1 : 0);
     if (w.tasks_T != nt || w.tasks_B != B || w.tasks_lag != lkey) {
         std::vector<uint32_t> one, all;
         std::vector<size_t> cs;
-        build_tail_tasks(nt, one, &cs, ctx->batch_gw, ctx->batch_near);
+        build_tail_tasks(nt, one, &cs, ctx->batch_gw, ctx->batch_near, ctx->batch_quads);
         interleave_tail_tasks(one, cs, B, lag, all);
         if ((rc = ensure(ctx, &w.tasks, &w.tasks_elems, all.size()))) return rc;
         HIPCK(ctx, hipMemcpy(w.tasks, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -1062,20 +1075,24 @@ int batch_tail_eval(gaplac_ctx* ctx, int64_t N, const std::vector<TermPack>& pac
         w.tasks_lag = lkey;
         w.tasks_n = (int)all.size();
     }
-    hipStream_t s = ctx->s_main;
+    hipStream_t g = ctx->s_panel, s = ctx->s_main;
     for (int b = 0; b < B; ++b) w.htp[b] = packs[(size_t)(m0 + b)];
-    HIPCK(ctx, hipMemcpyAsync(w.dtp, w.htp, sizeof(TermPack) * (size_t)B, hipMemcpyHostToDevice, s));
-    LaunchGuard g;
-    g.base = w.A;
-    g.elems = (int64_t)(astride * (size_t)B);
+    LaunchGuard guard;
+    guard.base = w.A;
+    guard.elems = (int64_t)(astride * (size_t)B);
     {
-        GuardScope scope(&g);
+        GuardScope scope(&guard);
+        HIPCK(ctx, hipMemcpyAsync(w.dtp, w.htp, sizeof(TermPack) * (size_t)B, hipMemcpyHostToDevice, g));
         for (int b = 0; b < B; ++b) {
-            launch_init_result(s, w.dres + b);
-            launch_gram(s, w.A + astride * (size_t)b, lda, N, nt, ctx->dX, N, ctx->dv, w.dtp + b, 0, 0, nullptr);
+            launch_init_result(g, w.dres + b);
+            launch_gram(g, w.A + astride * (size_t)b, lda, N, nt, ctx->dX, N, ctx->dv, w.dtp + b, 0, 0, nullptr);
         }
+        HIPCK(ctx, hipEventRecord(w.ev_gram, g));
+        HIPCK(ctx, hipStreamWaitEvent(s, w.ev_gram, 0));
         HIPCK(ctx, hipMemsetAsync(w.ctl, 0, sizeof(TailCtl) * (size_t)B, s));
-        TailArgs ta{w.A, lda, N, 0, nt, w.Dinv, w.dres, w.ctl, w.tasks, w.tasks_n, nullptr};
+        const bool trace = !ctx->ttrace_path.empty();  // diagnostics: launches one at a time
+        if (trace && (rc = ensure(ctx, &ctx->ttrace, &ctx->ttrace_elems, 3 * (size_t)w.tasks_n))) return rc;
+        TailArgs ta{w.A, lda, N, 0, nt, w.Dinv, w.dres, w.ctl, w.tasks, w.tasks_n, trace ? ctx->ttrace : nullptr};
         ta.a_stride = (int64_t)astride;
         ta.dinv_stride = (int64_t)dstride;
         ta.nmodels = B;
@@ -1083,14 +1100,38 @@ int batch_tail_eval(gaplac_ctx* ctx, int64_t N, const std::vector<TermPack>& pac
         for (int b = 0; b < B; ++b)
             launch_reduce(s, w.A + astride * (size_t)b, lda, N, (int64_t)nt * NB, ColMap{1, 0, 1}, w.dres + b);
     }
-    if (g.violations) return set_err(ctx, GAPLAC_E_ARG, "batched tail: launch footprint outside the workspace: %s",
-                                     g.first.c_str());
+    if (guard.violations)
+        return set_err(ctx, GAPLAC_E_ARG, "batched tail: launch footprint outside the workspace: %s", guard.first.c_str());
     HIPCK(ctx, hipGetLastError());
     HIPCK(ctx, hipMemcpyAsync(w.hres, w.dres, sizeof(EvalResult) * (size_t)B, hipMemcpyDeviceToHost, s));
-    HIPCK(ctx, hipStreamSynchronize(s));
-    for (int b = 0; b < B; ++b) {
+    HIPCK(ctx, hipEventRecord(w.ev_done, s));
+    w.busy = true;
+    w.m0 = m0;
+    w.B = B;
+    if (!ctx->ttrace_path.empty()) {  // diagnostics: the launch's task timeline
+        if ((rc = batch_tail_finish(ctx, p, out_logpdf, out_info))) return rc;
+        std::vector<unsigned long long> tr(3 * (size_t)w.tasks_n);
+        std::vector<uint32_t> tk((size_t)w.tasks_n);
+        HIPCK(ctx, hipMemcpy(tr.data(), ctx->ttrace, tr.size() * 8, hipMemcpyDeviceToHost));
+        HIPCK(ctx, hipMemcpy(tk.data(), w.tasks, tk.size() * 4, hipMemcpyDeviceToHost));
+        if (FILE* f = std::fopen(ctx->ttrace_path.c_str(), "a")) {
+            std::fprintf(f, "# N=%lld T=%d tasks=%d models=%d (batched)\n", (long long)N, nt, w.tasks_n, B);
+            for (size_t i = 0; i < tk.size(); ++i)
+                std::fprintf(f, "%zu %u %llu %llu %llu\n", i, tk[i], tr[3 * i], tr[3 * i + 1], tr[3 * i + 2]);
+            std::fclose(f);
+        }
+    }
+    return 0;
+}
+
+static int batch_tail_finish(gaplac_ctx* ctx, int p, double* out_logpdf, int64_t* out_info) {
+    gaplac_ctx::BatchWs& w = ctx->bw[p];
+    if (!w.busy) return 0;
+    w.busy = false;
+    HIPCK(ctx, hipEventSynchronize(w.ev_done));
+    for (int b = 0; b < w.B; ++b) {
         if (w.hres[b].err) return set_err(ctx, GAPLAC_E_HIP, "batched tail: in-kernel wait expired (code %u)", w.hres[b].err);
-        out_info[m0 + b] = finish(w.hres[b], &out_logpdf[m0 + b], nullptr, nullptr);
+        out_info[w.m0 + b] = finish(w.hres[b], &out_logpdf[w.m0 + b], nullptr, nullptr);
     }
     return 0;
 }
@@ -1219,14 +1260,18 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     if (ctx->hgp) (void)hipHostFree(ctx->hgp);
     if (ctx->glist) (void)hipFree(ctx->glist);
     if (ctx->tctl) (void)hipFree(ctx->tctl);
-    if (ctx->bw.A) (void)hipFree(ctx->bw.A);
-    if (ctx->bw.Dinv) (void)hipFree(ctx->bw.Dinv);
-    if (ctx->bw.dres) (void)hipFree(ctx->bw.dres);
-    if (ctx->bw.dtp) (void)hipFree(ctx->bw.dtp);
-    if (ctx->bw.hres) (void)hipHostFree(ctx->bw.hres);
-    if (ctx->bw.htp) (void)hipHostFree(ctx->bw.htp);
-    if (ctx->bw.ctl) (void)hipFree(ctx->bw.ctl);
-    if (ctx->bw.tasks) (void)hipFree(ctx->bw.tasks);
+    for (auto& w : ctx->bw) {
+        if (w.A) (void)hipFree(w.A);
+        if (w.Dinv) (void)hipFree(w.Dinv);
+        if (w.dres) (void)hipFree(w.dres);
+        if (w.dtp) (void)hipFree(w.dtp);
+        if (w.hres) (void)hipHostFree(w.hres);
+        if (w.htp) (void)hipHostFree(w.htp);
+        if (w.ctl) (void)hipFree(w.ctl);
+        if (w.tasks) (void)hipFree(w.tasks);
+        if (w.ev_gram) (void)hipEventDestroy(w.ev_gram);
+        if (w.ev_done) (void)hipEventDestroy(w.ev_done);
+    }
     if (ctx->ttasks) (void)hipFree(ctx->ttasks);
     if (ctx->ttrace) (void)hipFree(ctx->ttrace);
     if (ctx->dres) (void)hipFree(ctx->dres);
@@ -1312,12 +1357,19 @@ int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D, 
         if (nmodels >= 2 && whole_in_tail(ctx, nt)) {  // batched tail
             for (gaplac_ctx* c : ctx->lanes) HIPCK(ctx, hipStreamSynchronize(c->s_main));
             if ((rc = upload(ctx, N, D, X, ldx, v))) return rc;
+            HIPCK(ctx, hipStreamSynchronize(ctx->s_main));  // the Grams read X / v on s_panel
             for (int m = 0; m < nmodels; ++m) packs[(size_t)m].noise = noise;
-            for (int m0 = 0; m0 < nmodels; m0 += ctx->batch_w) {
+            int p = 0;
+            for (int m0 = 0; m0 < nmodels; m0 += ctx->batch_w, p ^= 1) {
                 const int B = std::min(ctx->batch_w, nmodels - m0);
-                if ((rc = batch_tail_eval(ctx, N, packs, m0, B, out_logpdf, out_info))) return rc;
+                if ((rc = batch_tail_enqueue(ctx, N, packs, m0, B, p, out_logpdf, out_info))) break;
             }
-            return 0;
+            // collect both sets (also after a failure: nothing of this call stays in flight)
+            for (int q = 0; q < 2; ++q) {
+                const int r2 = batch_tail_finish(ctx, q, out_logpdf, out_info);
+                if (!rc) rc = r2;
+            }
+            return rc;
         }
     }
     // the lanes borrow dX / dv: nothing of an earlier call may still read them
@@ -1590,9 +1642,10 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
         static std::string tail_bad = [] {
             for (int T = 1; T <= TAIL_TMAX; ++T)
                 for (int gw : {4, 8})
-                    for (int near : {2, 3, 4, 8}) {
+                    for (int near : {2, 3, 4, 8})
+                    for (bool quads : {true, false}) {
                         std::vector<uint32_t> l;
-                        build_tail_tasks(T, l, nullptr, gw, near);
+                        build_tail_tasks(T, l, nullptr, gw, near, quads);
                         std::string why;
                         if (!check_tail_tasks(T, l, &why)) return why + " (gw " + std::to_string(gw) + ", near " +
                                                                   std::to_string(near) + ")";

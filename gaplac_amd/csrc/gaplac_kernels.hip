@@ -2631,7 +2631,8 @@ void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<s
 // the block's next GW columns, nearest tile column first, behind each column's own tasks.
 // Single evaluations use GW = 4, NEAR = 4 (latency); batched launches fewer per-column
 // updates (throughput).
-void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart, int gw, int near) {
+void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart, int gw, int near,
+                      bool quads) {
     // deep width; near distance (>= 2: the next two diagonal tiles take per-column Q tasks)
     const int GW = gw == 8 ? 8 : 4, NEAR = std::max(2, near);
     const int qdeep = GW == 8 ? TAIL_UD8 : TAIL_UD;
@@ -2645,9 +2646,13 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
         if (i < T)
             for (int q = 0; q < (int)TAIL_NQ; ++q) out.push_back(tail_enc(TK_Q, q, k, i, i));
     };
-    auto Uq = [&](int i, int j, int k) {  // quadrants of off-diagonal tile (i, j)
-        if (i < T)
-            for (int q = 1; q <= 4; ++q) out.push_back(tail_enc(TK_U, q, k, i, j));
+    auto Uq = [&](int i, int j, int k) {  // quadrants of off-diagonal tile (i, j) (or the whole tile)
+        if (i < T) {
+            if (!quads)
+                out.push_back(tail_enc(TK_U, 0, k, i, j));
+            else
+                for (int q = 1; q <= 4; ++q) out.push_back(tail_enc(TK_U, q, k, i, j));
+        }
     };
     // block b of GW columns is deep-updated when all its columns update something
     auto deep_block = [&](int b) { return GW * b + GW - 1 <= T - 2; };

@@ -255,3 +255,44 @@ def test_batch_on_lanes_bitwise_equal_to_single_evals():
         assert abs(out[3] - ref) <= 1e-9 * abs(ref)
     finally:
         c.close()
+
+
+def test_batched_tail_sets_reused_bitwise_equal_to_single_evals():
+    """The batched tail with 3 models per launch over 11 models: four launches
+    alternate between the two workspace sets (each launch's Grams on s_panel beside the
+    previous launch's tail), so every set is reused while the other is in flight; a
+    non-positive-definite model sits in the middle. Every result is exactly the single
+    evaluation's."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import os
+    old = {k: os.environ.get(k) for k in ("GAPLAC_BATCH_W", "GAPLAC_BATCH_LAG")}
+    os.environ.update({"GAPLAC_BATCH_W": "3", "GAPLAC_BATCH_LAG": "5"})
+    try:
+        c = Context(0)
+    finally:
+        for k, val in old.items():
+            if val is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = val
+    try:
+        rng = np.random.default_rng(29)
+        N = 1500
+        X = np.column_stack([rng.uniform(0, 10, N), rng.integers(0, 400, N).astype(float)])
+        v = rng.standard_normal(N)
+        models = [[(SQEXP, 0, 0.5 + 0.25 * i, 0), (CAT, 1, 0.0, 1), (NOISE, -1, 0.1, 2)] for i in range(10)]
+        models.insert(5, [(CAT, 1, 0.0, 0)])  # noise 0 below: singular
+        for rep in range(2):
+            out, info = c.logpdf_batch(X, models, 0.0, v)
+            for i, m in enumerate(models):
+                if i == 5:
+                    with pytest.raises(PosDefException) as e:
+                        c.logpdf(X, m, 0.0, v)
+                    assert info[i] == e.value.info and np.isnan(out[i])
+                else:
+                    assert info[i] == 0 and out[i] == c.logpdf(X, m, 0.0, v), (rep, i)
+        ref = R.logpdf(X, models[7], 0.0, v)[0]
+        assert rel(out[7], ref) <= RTOL
+    finally:
+        c.close()

@@ -26,19 +26,23 @@ def main(path):
     by = {}
     for e, t0, t1, t2 in rows:
         ty, q, k, i, j = e & 3, (e >> 2) & 15, (e >> 6) & 127, (e >> 13) & 127, (e >> 20) & 127
+        m = e >> 27  # model (batched launches)
         dur[ty].append((t2 - t1) / 100.0)
         wait[ty].append((t1 - t0) / 100.0)
-        by[(ty, q, k, i, j)] = (us(t0), us(t1), us(t2))
+        by[(ty, q, k, i, j) if m == 0 else (ty, q, k, i, j, m)] = (us(t0), us(t1), us(t2))
     for ty in sorted(dur):
         d, w = dur[ty], wait[ty]
         print(f"{NAMES[ty]}: n={len(d):5d} exec mean {sum(d) / len(d):7.2f} us max {max(d):7.2f}  "
               f"wait mean {sum(w) / len(w):7.2f} max {max(w):7.2f}")
     # U tasks by shape, with their MFMA rate per workgroup (fp64 peak per CU = 78.6/256 TF/s)
     ushape = defaultdict(list)
-    for (ty, q, k, i, j), (t0, t1, t2) in by.items():
+    for key, (t0, t1, t2) in by.items():
+        ty, q = key[0], key[1]
         if ty == 2:
-            ushape["K=512 tile" if q == 5 else "K=128 tile" if q == 0 else "K=128 quadrant"].append(t2 - t1)
-    flops = {"K=512 tile": 2 * 128 * 128 * 512, "K=128 tile": 2 * 128 * 128 * 128, "K=128 quadrant": 2 * 64 * 64 * 128}
+            ushape["K=1024 tile" if q == 6 else "K=512 tile" if q == 5 else "K=128 tile" if q == 0
+                   else "K=128 quadrant"].append(t2 - t1)
+    flops = {"K=1024 tile": 2 * 128 * 128 * 1024, "K=512 tile": 2 * 128 * 128 * 512, "K=128 tile": 2 * 128 * 128 * 128,
+             "K=128 quadrant": 2 * 64 * 64 * 128}
     for name, d in sorted(ushape.items()):
         m = sum(d) / len(d)
         print(f"  U {name:15s} n={len(d):5d} exec mean {m:7.2f} us = {flops[name] / m / 1e6:.3f} TF/s per CU "
@@ -49,7 +53,7 @@ def main(path):
     grid = 256
     print(f"span {span:.1f} us; over {grid} workgroups: exec {ex / (grid * span):.3f}, wait {wt / (grid * span):.3f}, "
           f"rest (dequeue, idle) {1 - (ex + wt) / (grid * span):.3f}")
-    T = max(k for (_, _, k, _, _) in by) + 2
+    T = max(key[2] for key in by) + 2
     print(f"{'k':>3} {'D start':>9} {'D end':>9} {'S start':>9} {'S end':>9} {'Q start':>9} {'Q end':>9} {'D+1 deq':>9}")
     for k in range(T - 1):
         d = by.get((0, 0, k, 0, 0))
