@@ -100,11 +100,12 @@ struct gaplac_ctx {
     int batch_w = 32;              // GAPLAC_BATCH_W: models per tail launch when the whole matrix is in the tail
     int batch_lag = -1;            // GAPLAC_BATCH_LAG: tile columns between consecutive models of a tail launch
                                    // (-1: 3/8 of the matrix's tile columns)
-#ifndef GAPLAC_BATCH_QUADS
-#define GAPLAC_BATCH_QUADS 1
+#ifndef GAPLAC_QUAD_LAST
+#define GAPLAC_QUAD_LAST 24
 #endif
     int batch_gw = 8, batch_near = 2;  // the batched tail's deep-task width and near distance (A/B: §3.4)
-    bool batch_quads = GAPLAC_BATCH_QUADS;
+    // single evaluations: quadrant next-column updates in the last 24 tail columns (the
+    // latency-bound end); batched lists: whole tiles throughout (select: 258 -> 265 evals/s)
     // the batched-tail workspace (gaplac_logpdf_batch): batch_w matrices
     struct BatchWs {
         double* A = nullptr;
@@ -603,13 +604,13 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             // the tail as one persistent dataflow launch
             if (ctx->dry) {  // gaplac_plan_check: the task list's dependency order
                 std::vector<uint32_t> host;
-                build_tail_tasks(T, host);
+                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST);
                 std::string why;
                 if (!check_tail_tasks(T, host, &why)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
             }
             if (ctx->ttasks_T != T && !ctx->dry) {
                 std::vector<uint32_t> host;
-                build_tail_tasks(T, host);
+                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST);
                 int rc;
                 if ((rc = ensure(ctx, &ctx->ttasks, &ctx->ttasks_elems, host.size()))) return rc;
                 HIPCK(ctx, hipMemcpy(ctx->ttasks, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -1062,11 +1063,11 @@ static int batch_tail_enqueue(gaplac_ctx* ctx, int64_t N, const std::vector<Term
         w.host_cap = B;
     }
     const int lag = ctx->batch_lag >= 0 ? ctx->batch_lag : (3 * nt + 4) / 8;
-    const int lkey = lag * 1000 + ctx->batch_gw * 100 + ctx->batch_near * 10 + (ctx->batch_quads ? 1 : 0);
+    const int lkey = lag * 100 + ctx->batch_gw * 10 + ctx->batch_near;
     if (w.tasks_T != nt || w.tasks_B != B || w.tasks_lag != lkey) {
         std::vector<uint32_t> one, all;
         std::vector<size_t> cs;
-        build_tail_tasks(nt, one, &cs, ctx->batch_gw, ctx->batch_near, ctx->batch_quads);
+        build_tail_tasks(nt, one, &cs, ctx->batch_gw, ctx->batch_near, 0);
         interleave_tail_tasks(one, cs, B, lag, all);
         if ((rc = ensure(ctx, &w.tasks, &w.tasks_elems, all.size()))) return rc;
         HIPCK(ctx, hipMemcpy(w.tasks, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -1643,9 +1644,9 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
             for (int T = 1; T <= TAIL_TMAX; ++T)
                 for (int gw : {4, 8})
                     for (int near : {2, 3, 4, 8})
-                    for (bool quads : {true, false}) {
+                    for (int ql : {0, 7, 40, TAIL_TMAX}) {
                         std::vector<uint32_t> l;
-                        build_tail_tasks(T, l, nullptr, gw, near, quads);
+                        build_tail_tasks(T, l, nullptr, gw, near, ql);
                         std::string why;
                         if (!check_tail_tasks(T, l, &why)) return why + " (gw " + std::to_string(gw) + ", near " +
                                                                   std::to_string(near) + ")";

@@ -2632,7 +2632,7 @@ void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<s
 // Single evaluations use GW = 4, NEAR = 4 (latency); batched launches fewer per-column
 // updates (throughput).
 void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart, int gw, int near,
-                      bool quads) {
+                      int quad_last) {
     // deep width; near distance (>= 2: the next two diagonal tiles take per-column Q tasks)
     const int GW = gw == 8 ? 8 : 4, NEAR = std::max(2, near);
     const int qdeep = GW == 8 ? TAIL_UD8 : TAIL_UD;
@@ -2648,7 +2648,7 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
     };
     auto Uq = [&](int i, int j, int k) {  // quadrants of off-diagonal tile (i, j) (or the whole tile)
         if (i < T) {
-            if (!quads)
+            if (k < T - quad_last)
                 out.push_back(tail_enc(TK_U, 0, k, i, j));
             else
                 for (int q = 1; q <= 4; ++q) out.push_back(tail_enc(TK_U, q, k, i, j));
