@@ -105,7 +105,8 @@ struct gaplac_ctx {
 #endif
     int batch_gw = 8, batch_near = 2;  // the batched tail's deep-task width and near distance (A/B: §3.4)
     // single evaluations: quadrant next-column updates in the last 24 tail columns (the
-    // latency-bound end); batched lists: whole tiles throughout (select: 258 -> 265 evals/s)
+    // latency-bound end) and pipelined half-tile TRSMs; batched lists: whole tiles and
+    // whole-tile TRSMs throughout (select: 258 -> 267 evals/s)
     // the batched-tail workspace (gaplac_logpdf_batch): batch_w matrices
     struct BatchWs {
         double* A = nullptr;
@@ -1067,7 +1068,7 @@ static int batch_tail_enqueue(gaplac_ctx* ctx, int64_t N, const std::vector<Term
     if (w.tasks_T != nt || w.tasks_B != B || w.tasks_lag != lkey) {
         std::vector<uint32_t> one, all;
         std::vector<size_t> cs;
-        build_tail_tasks(nt, one, &cs, ctx->batch_gw, ctx->batch_near, 0);
+        build_tail_tasks(nt, one, &cs, ctx->batch_gw, ctx->batch_near, 0, true);
         interleave_tail_tasks(one, cs, B, lag, all);
         if ((rc = ensure(ctx, &w.tasks, &w.tasks_elems, all.size()))) return rc;
         HIPCK(ctx, hipMemcpy(w.tasks, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -1644,9 +1645,10 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
             for (int T = 1; T <= TAIL_TMAX; ++T)
                 for (int gw : {4, 8})
                     for (int near : {2, 3, 4, 8})
-                    for (int ql : {0, 7, 40, TAIL_TMAX}) {
+                    for (int ql : {0, 7, 40, TAIL_TMAX})
+                    for (bool wt : {false, true}) {
                         std::vector<uint32_t> l;
-                        build_tail_tasks(T, l, nullptr, gw, near, ql);
+                        build_tail_tasks(T, l, nullptr, gw, near, ql, wt);
                         std::string why;
                         if (!check_tail_tasks(T, l, &why)) return why + " (gw " + std::to_string(gw) + ", near " +
                                                                   std::to_string(near) + ")";

@@ -2177,6 +2177,7 @@ __global__ __launch_bounds__(256) void lower_mv_reduce_kernel(const double* __re
 // bounded (0.2 s); an expired wait sets TailCtl::err, which the host turns into GAPLAC_E_HIP.
 // =================================================================================
 enum { TK_D = 0, TK_S = 1, TK_U = 2, TK_Q = 3 };
+constexpr int TAIL_S_WHOLE = 2;  // S task q: the whole 128-row tile, after D(k) (else q = row half)
 constexpr unsigned TAIL_NQ = 10;  // Q blocks per diagonal tile (= units a diagonal U adds)
 
 // task word: type (2 bits) | q (4) | k (7) | i (7) | j (7), tile indices relative to ts
@@ -2233,9 +2234,12 @@ __device__ __forceinline__ void tail_trsm(double* smem, double* Acol, int64_t ld
     const int fr = lane >> 4, fc = lane & 15;
     const int64_t k0 = (int64_t)k * NB;
     const Gm<AUX> gA(Acol), gD(Dk);
-    const uint32_t rowb = (uint32_t)((int64_t)bi * NB + 64 * h + 16 * (wave & 3));
+    // h = 0, 1: rows 64h .. 64h+63 on waves 0-3; h = 2 (TAIL_S_WHOLE): the whole tile, 16
+    // rows per wave on all eight (two independent substitution chains per SIMD)
+    const bool whole = h == 2;
+    const uint32_t rowb = (uint32_t)((int64_t)bi * NB + (whole ? 16 * wave : 64 * h + 16 * (wave & 3)));
     d4 Bt[NDB];
-    if (wave < 4) {
+    if (wave < 4 || whole) {
 #pragma unroll
         for (int b = 0; b < NDB; ++b)
 #pragma unroll
@@ -2243,7 +2247,7 @@ __device__ __forceinline__ void tail_trsm(double* smem, double* Acol, int64_t ld
     }
     tail_trsm_stage(Ls, gA, gD, lda, k0, tid);
     __syncthreads();
-    if (wave >= 4) return;
+    if (wave >= 4 && !whole) return;
     d4 Y[NDB];
 #pragma unroll
     for (int b = 0; b < NDB; ++b) {
@@ -2497,6 +2501,7 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int
             ok = tail_ld(&c->units[k * TAIL_TMAX + k]) >= TAIL_NQ * k;
         } else if (type == TK_S) {  // the block itself; D(k)'s progress inside tail_trsm_pipe
             ok = tail_ld(&c->units[i * TAIL_TMAX + k]) >= 4u * k;
+            if (q == TAIL_S_WHOLE && ok) ok = tail_ld(&c->ddone[k]) != 0u;  // not pipelined: D(k) done
         } else {
             const unsigned ups = i == j ? TAIL_NQ : 4u;
             const int nk = tail_deep_cols(type, q);  // panel columns k .. k+nk-1
@@ -2539,6 +2544,8 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
             if ((int64_t)gk * NB < a.N)
                 potrf_diag2_body<GM_SC1>(smem, colk + (int64_t)gk * NB, a.lda, a.N, (int64_t)gk * NB,
                                          Dinv + (size_t)gk * DINV_PER_BLOCK, res, nullptr, &ctl->dprog[k]);
+        } else if (type == TK_S && q == TAIL_S_WHOLE) {
+            tail_trsm<GM_SC1>(smem, colk, a.lda, gk, a.ts + i, q, Dinv + (size_t)gk * DINV_PER_BLOCK);
         } else if (type == TK_S) {
             tail_trsm_pipe<GM_SC1>(smem, s_rowf, colk, a.lda, gk, a.ts + i, q, Dinv + (size_t)gk * DINV_PER_BLOCK,
                                    &ctl->dprog[k], &ctl->ddone[k], &ctl->err);
@@ -2566,8 +2573,9 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         if (threadIdx.x == 0) {
             if (type == TK_D) {
                 __hip_atomic_fetch_add(&ctl->ddone[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else if (type == TK_S) {  // two halves per tile: done at 2
-                __hip_atomic_fetch_add(&ctl->sdone[i * TAIL_TMAX + k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (type == TK_S) {  // two halves per tile (or one whole-tile task): done at 2
+                __hip_atomic_fetch_add(&ctl->sdone[i * TAIL_TMAX + k], q == TAIL_S_WHOLE ? 2u : 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 const unsigned whole = i == j ? TAIL_NQ : 4u;
                 const int nk = tail_deep_cols(type, q);
@@ -2632,7 +2640,7 @@ void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<s
 // Single evaluations use GW = 4, NEAR = 4 (latency); batched launches fewer per-column
 // updates (throughput).
 void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart, int gw, int near,
-                      int quad_last) {
+                      int quad_last, bool whole_trsm) {
     // deep width; near distance (>= 2: the next two diagonal tiles take per-column Q tasks)
     const int GW = gw == 8 ? 8 : 4, NEAR = std::max(2, near);
     const int qdeep = GW == 8 ? TAIL_UD8 : TAIL_UD;
@@ -2640,7 +2648,12 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
     if (colstart) colstart->clear();
     auto S = [&](int i, int k) {
         if (i < T)
-            for (int h = 0; h < 2; ++h) out.push_back(tail_enc(TK_S, h, k, i, 0));  // row halves
+        {
+            if (whole_trsm && k < T - quad_last)
+                out.push_back(tail_enc(TK_S, TAIL_S_WHOLE, k, i, 0));  // the whole tile (throughput)
+            else
+                for (int h = 0; h < 2; ++h) out.push_back(tail_enc(TK_S, h, k, i, 0));  // row halves
+        }
     };
     auto Qs = [&](int i, int k) {  // the ten 32x32 blocks of diagonal tile i
         if (i < T)
@@ -2716,7 +2729,7 @@ bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why
         } else if (type == TK_S) {
             if (units[(size_t)i * T + k] != 4u * (unsigned)k || i <= k) return fail(n, "S before its tile is updated");
             if (!ddone[(size_t)k]) return fail(n, "S before D is dequeued");  // (pipelined behind D)
-            sdone[(size_t)i * T + k] += 1;
+            sdone[(size_t)i * T + k] += q == TAIL_S_WHOLE ? 2u : 1u;
         } else {
             const int nk = tail_deep_cols(type, q);
             if (i < j || j <= k + nk - 1) return fail(n, "update of a tile not right of its panel");
