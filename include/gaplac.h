@@ -110,7 +110,8 @@ int gaplac_logpdf_device(gaplac_ctx* ctx, int64_t N, int32_t D, const double* dX
  * `logpdf(pr_k, y_k)` calls of CLI/src/select.jl:49-50. out_logpdf / out_info have
  * nmodels entries; the return value is 0 when the batch ran (per-model PD failures are
  * reported in out_info[m] > 0 with out_logpdf[m] = NaN) and <0 on argument/runtime
- * errors. */
+ * errors. Each result is bitwise that model's gaplac_logpdf. Device memory: up to two
+ * workspace sets of GAPLAC_BATCH_W (32) matrices of (N+1 rounded up to 128)^2 doubles. */
 int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D,
                         const double* X, int64_t ldx, const int32_t* term_offset,
                         const gaplac_term* terms, double noise, const double* v,
