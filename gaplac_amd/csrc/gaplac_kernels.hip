@@ -2186,9 +2186,10 @@ __host__ __device__ __forceinline__ uint32_t tail_enc(int type, int q, int k, in
 }
 constexpr int TAIL_UD = 5;     // U task q: a whole tile with the 4 columns k .. k+3 (K = 512)
 constexpr int TAIL_UD8 = 6;    // U task q: a whole tile with the 8 columns k .. k+7 (K = 1024)
-// panel columns a task applies (deep U tasks 4 or 8, every other update 1)
+constexpr int TAIL_UD2 = 7;    // U task q: a whole tile with the 2 columns k, k+1 (K = 256)
+// panel columns a task applies (deep U tasks 2, 4 or 8, every other update 1)
 __host__ __device__ __forceinline__ int tail_deep_cols(int type, int q) {
-    return type == TK_U ? (q == TAIL_UD ? 4 : q == TAIL_UD8 ? 8 : 1) : 1;
+    return type == TK_U ? (q == TAIL_UD ? 4 : q == TAIL_UD8 ? 8 : q == TAIL_UD2 ? 2 : 1) : 1;
 }
 
 // Stage L_kk's 28 strictly-lower 16x16 blocks and the 8 inverses in LDS for the tail's
@@ -2558,6 +2559,8 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
                 tail_update<GM_SC1, 4, 2, 4>(gC, gP, a.lda, gi * NB, 0, gj * NB);
             } else if (type == TK_U && q == TAIL_UD8) {
                 tail_update<GM_SC1, 4, 2, 8>(gC, gP, a.lda, gi * NB, 0, gj * NB);
+            } else if (type == TK_U && q == TAIL_UD2) {
+                tail_update<GM_SC1, 4, 2, 2>(gC, gP, a.lda, gi * NB, 0, gj * NB);
             } else if (type == TK_U) {  // quadrant q - 1 of an off-diagonal tile
                 const int qi = (q - 1) >> 1, qj = (q - 1) & 1;
                 tail_update<GM_SC1, 2, 1>(gC, gP, a.lda, gi * NB + 64 * qi, 64 * qj, gj * NB + 64 * qj);
@@ -2640,7 +2643,7 @@ void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<s
 // Single evaluations use GW = 4, NEAR = 4 (latency); batched launches fewer per-column
 // updates (throughput).
 void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart, int gw, int near,
-                      int quad_last, bool whole_trsm) {
+                      int quad_last, bool whole_trsm, bool pairs) {
     // deep width; near distance (>= 2: the next two diagonal tiles take per-column Q tasks)
     const int GW = gw == 8 ? 8 : 4, NEAR = std::max(2, near);
     const int qdeep = GW == 8 ? TAIL_UD8 : TAIL_UD;
@@ -2687,9 +2690,22 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
         Uq(g + 3, g + 1, g);
         for (int i = g + 4; i < T; ++i) S(i, g);
         for (int i = g + 4; i < T; ++i) Uq(i, g + 1, g);
+        // near tiles: column g's update, or with pairs (throughput lists) two columns in one
+        // K = 256 task: at even g the tiles j >= g+3 (but the diagonal tile g+3, which takes
+        // Q tasks at column g+1) wait for column g+1, whose list applies g and g+1 together
+        // (pairs only before the last quad_last columns: the latency-shaped end keeps them single)
+        const bool even = (g & 1) == 0;
+        const bool defer = pairs && even && g + 1 < T - 1 && g + 1 < T - quad_last;
+        const bool paired = pairs && !even && g < T - quad_last;
         for (int j = g + 2; j < std::min(jfar, T); ++j)
-            for (int i = j; i < T; ++i)
-                if (i != g + 2 || j != g + 2) out.push_back(tail_enc(TK_U, 0, g, i, j));
+            for (int i = j; i < T; ++i) {
+                if (i == g + 2 && j == g + 2) continue;  // the Q tasks above
+                if (defer && j >= g + 3 && !(i == g + 3 && j == g + 3)) continue;
+                if (paired)
+                    out.push_back(tail_enc(TK_U, TAIL_UD2, g - 1, i, j));  // columns g-1, g
+                else
+                    out.push_back(tail_enc(TK_U, 0, g, i, j));
+            }
         for (uint32_t e : later[(size_t)g]) out.push_back(e);
         if (deep_block(b) && g == GW * b + GW - 1) {
             // block b's deep tasks: near in block b+1 -> now; the rest -> columns g+1 .. g+4

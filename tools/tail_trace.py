@@ -39,9 +39,10 @@ def main(path):
     for key, (t0, t1, t2) in by.items():
         ty, q = key[0], key[1]
         if ty == 2:
-            ushape["K=1024 tile" if q == 6 else "K=512 tile" if q == 5 else "K=128 tile" if q == 0
-                   else "K=128 quadrant"].append(t2 - t1)
-    flops = {"K=1024 tile": 2 * 128 * 128 * 1024, "K=512 tile": 2 * 128 * 128 * 512, "K=128 tile": 2 * 128 * 128 * 128,
+            ushape["K=1024 tile" if q == 6 else "K=512 tile" if q == 5 else "K=256 tile" if q == 7
+                   else "K=128 tile" if q == 0 else "K=128 quadrant"].append(t2 - t1)
+    flops = {"K=1024 tile": 2 * 128 * 128 * 1024, "K=512 tile": 2 * 128 * 128 * 512, "K=256 tile": 2 * 128 * 128 * 256,
+             "K=128 tile": 2 * 128 * 128 * 128,
              "K=128 quadrant": 2 * 64 * 64 * 128}
     for name, d in sorted(ushape.items()):
         m = sum(d) / len(d)
