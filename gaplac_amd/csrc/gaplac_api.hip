@@ -100,8 +100,11 @@ struct gaplac_ctx {
     int batch_w = 32;              // GAPLAC_BATCH_W: models per tail launch when the whole matrix is in the tail
     int batch_lag = -1;            // GAPLAC_BATCH_LAG: tile columns between consecutive models of a tail launch
                                    // (-1: 3/8 of the matrix's tile columns)
-#ifndef GAPLAC_SINGLE_PAIRS
-#define GAPLAC_SINGLE_PAIRS 1
+#ifndef GAPLAC_SINGLE_GROUP
+#define GAPLAC_SINGLE_GROUP 2
+#endif
+#ifndef GAPLAC_BATCH_GROUP
+#define GAPLAC_BATCH_GROUP 2
 #endif
 #ifndef GAPLAC_QUAD_LAST
 #define GAPLAC_QUAD_LAST 24
@@ -608,13 +611,13 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             // the tail as one persistent dataflow launch
             if (ctx->dry) {  // gaplac_plan_check: the task list's dependency order
                 std::vector<uint32_t> host;
-                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_PAIRS);
+                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP);
                 std::string why;
                 if (!check_tail_tasks(T, host, &why)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
             }
             if (ctx->ttasks_T != T && !ctx->dry) {
                 std::vector<uint32_t> host;
-                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_PAIRS);
+                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP);
                 int rc;
                 if ((rc = ensure(ctx, &ctx->ttasks, &ctx->ttasks_elems, host.size()))) return rc;
                 HIPCK(ctx, hipMemcpy(ctx->ttasks, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -1071,7 +1074,7 @@ static int batch_tail_enqueue(gaplac_ctx* ctx, int64_t N, const std::vector<Term
     if (w.tasks_T != nt || w.tasks_B != B || w.tasks_lag != lkey) {
         std::vector<uint32_t> one, all;
         std::vector<size_t> cs;
-        build_tail_tasks(nt, one, &cs, ctx->batch_gw, ctx->batch_near, 0, true, true);
+        build_tail_tasks(nt, one, &cs, ctx->batch_gw, ctx->batch_near, 0, true, GAPLAC_BATCH_GROUP);
         interleave_tail_tasks(one, cs, B, lag, all);
         if ((rc = ensure(ctx, &w.tasks, &w.tasks_elems, all.size()))) return rc;
         HIPCK(ctx, hipMemcpy(w.tasks, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -1649,9 +1652,9 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
                 for (int gw : {4, 8})
                     for (int near : {2, 3, 4, 8})
                     for (int ql : {0, 7, 40, TAIL_TMAX})
-                    for (int wp : {0, 1, 2, 3}) {
+                    for (int wp : {0, 1, 2, 3, 4, 5}) {
                         std::vector<uint32_t> l;
-                        build_tail_tasks(T, l, nullptr, gw, near, ql, (wp & 1) != 0, (wp & 2) != 0);
+                        build_tail_tasks(T, l, nullptr, gw, near, ql, (wp & 1) != 0, 1 << (wp >> 1));
                         std::string why;
                         if (!check_tail_tasks(T, l, &why)) return why + " (gw " + std::to_string(gw) + ", near " +
                                                                   std::to_string(near) + ")";

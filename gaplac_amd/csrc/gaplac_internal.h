@@ -116,10 +116,10 @@ constexpr int TAIL_MAX_MODELS = 32;
 // columns take latency-shaped tasks (the next tile column's tiles updated as four 64x64
 // quadrant tasks), the columns before them whole tiles; whole_trsm: before the last
 // quad_last columns the TRSMs are whole-tile tasks after the diagonal block, not two row
-// halves pipelined behind it; pairs: near tiles take two columns per K = 256 task where
-// the chain allows.
+// halves pipelined behind it; group (1, 2 or 4): near tiles take that many columns per
+// task (K = 128 group) where the chain allows.
 void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart = nullptr, int gw = 4,
-                      int near = 4, int quad_last = TAIL_TMAX, bool whole_trsm = false, bool pairs = false);
+                      int near = 4, int quad_last = TAIL_TMAX, bool whole_trsm = false, int group = 1);
 // B models' task lists interleaved (each model's own order kept, so the result is a
 // topological order per model). lag = 0: task by task, all models in step. lag > 0: a
 // software pipeline: model m runs lag * m tile columns behind model 0, and the tasks of the

@@ -2643,7 +2643,8 @@ void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<s
 // Single evaluations use GW = 4, NEAR = 4 (latency); batched launches fewer per-column
 // updates (throughput).
 void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart, int gw, int near,
-                      int quad_last, bool whole_trsm, bool pairs) {
+                      int quad_last, bool whole_trsm, int group) {
+    group = group >= 4 ? 4 : group >= 2 ? 2 : 1;  // divides the deep width (4 or 8): groups stay in a block
     // deep width; near distance (>= 2: the next two diagonal tiles take per-column Q tasks)
     const int GW = gw == 8 ? 8 : 4, NEAR = std::max(2, near);
     const int qdeep = GW == 8 ? TAIL_UD8 : TAIL_UD;
@@ -2690,21 +2691,21 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
         Uq(g + 3, g + 1, g);
         for (int i = g + 4; i < T; ++i) S(i, g);
         for (int i = g + 4; i < T; ++i) Uq(i, g + 1, g);
-        // near tiles: column g's update, or with pairs (throughput lists) two columns in one
-        // K = 256 task: at even g the tiles j >= g+3 (but the diagonal tile g+3, which takes
-        // Q tasks at column g+1) wait for column g+1, whose list applies g and g+1 together
-        // (pairs only before the last quad_last columns: the latency-shaped end keeps them single)
-        const bool even = (g & 1) == 0;
-        const bool defer = pairs && even && g + 1 < T - 1 && g + 1 < T - quad_last;
-        const bool paired = pairs && !even && g < T - quad_last;
+        // near tiles: column g's update, or (group = 2 / 4 columns, before the latency-shaped
+        // end) the group's columns g0 .. g1 in ONE task at g1 for the tiles the chain does not
+        // need before then: off the diagonal j >= g1 + 2 (tile column j is next at column
+        // j - 1), on it j >= g1 + 3 (it takes Q tasks from column j - 2 on)
+        const int r = g % group, g0 = g - r, g1 = g0 + group - 1;
+        const bool grouped = group > 1 && g1 <= T - 2 && g1 < T - quad_last;
+        const int qgroup = group == 2 ? TAIL_UD2 : group == 4 ? TAIL_UD : TAIL_UD8;
         for (int j = g + 2; j < std::min(jfar, T); ++j)
             for (int i = j; i < T; ++i) {
                 if (i == g + 2 && j == g + 2) continue;  // the Q tasks above
-                if (defer && j >= g + 3 && !(i == g + 3 && j == g + 3)) continue;
-                if (paired)
-                    out.push_back(tail_enc(TK_U, TAIL_UD2, g - 1, i, j));  // columns g-1, g
-                else
-                    out.push_back(tail_enc(TK_U, 0, g, i, j));
+                if (grouped && (i == j ? j >= g1 + 3 : j >= g1 + 2)) {
+                    if (g == g1) out.push_back(tail_enc(TK_U, qgroup, g0, i, j));
+                    continue;
+                }
+                out.push_back(tail_enc(TK_U, 0, g, i, j));
             }
         for (uint32_t e : later[(size_t)g]) out.push_back(e);
         if (deep_block(b) && g == GW * b + GW - 1) {
