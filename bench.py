@@ -9,9 +9,24 @@ triangular solve, logdet -> scalar) through the C-ABI entry gaplac_logpdf_device
 and v already resident in HBM. The SqExp lengthscale changes every step (an MCMC chain
 proposing new hyperparameters), so nothing can be cached between steps.
 
-Multi-GPU (--gpus N, launched by torch.distributed.run): each rank runs its own
-independent evaluations (replicas: hyperparameter points / chains / select candidates,
-SURVEY.md §8e), no data-path collective; value = evals of all ranks / max wall time.
+Multi-GPU (--gpus N): each rank runs its own independent evaluations (replicas:
+hyperparameter points / chains / select candidates), no data-path
+collective; value = evals of all ranks / max wall time. Two ways to start it:
+
+* under torch.distributed.run (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in the env):
+  this process is one rank, and WORLD_SIZE must equal --gpus;
+* as plain `python bench.py --gpus N` (no WORLD_SIZE in the env): this process is only a
+  launcher. It checks that N devices are visible (torch.cuda.device_count() does not
+  initialise the GPU), starts N child processes of this script with the rank variables
+  set (rendezvous on 127.0.0.1), never touches the GPU itself and never execs, and exits
+  with the first failing child's status (the other ranks are then terminated).
+Every rank asserts world size == --gpus and that its device exists; on a 1-GPU box
+`--gpus 2` fails with a message instead of reporting n_gpus: 1.
+
+With --gpus > 1 rank 0 also measures BASELINE configs[3] (N=65536) spread over all ranks
+(extra.dist) and checks its logpdf against the single-GPU evaluation of the same input in
+the same run (extra.dist.parity_vs_single, bar 1e-9 relative); a failed or non-matching
+dist line makes the process exit non-zero after the JSON line is printed.
 
 Prints ONE JSON line (rank 0).
 """
@@ -22,6 +37,8 @@ import datetime
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -104,6 +121,100 @@ def load_traffic(name=TRAFFIC_FILE):
         return None, None
 
 
+DIST_PARITY_BAR = 1e-9  # relative, north_star's fp64 bar
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv, need_gpus: bool = True, poll_s: float = 0.2) -> int:
+    """Start n ranks of this script as child processes and wait for them.
+
+    The parent never touches the GPU (device_count() only counts devices on this image)
+    and never execs; each child gets RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* and the
+    same argv. Returns 0 if every rank exited 0, otherwise the first failure's status
+    (a signal maps to 128 + signo), after terminating the ranks still running."""
+    if need_gpus:
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench: --gpus {n} needs {n} visible GPUs, this node shows {have}", file=sys.stderr, flush=True)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    pending = set(range(n))
+    while pending:
+        for r in sorted(pending):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            pending.discard(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"bench: rank {r} exited with status {c}; stopping the other ranks", file=sys.stderr, flush=True)
+                for q in pending:
+                    procs[q].terminate()
+        if pending:
+            time.sleep(poll_s)
+    return rc
+
+
+def rank_env(args):
+    """(rank, world, local_rank) from the launcher's env, checked against --gpus."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+                         f"(torch.distributed.run --nproc-per-node {args.gpus}, or plain python bench.py --gpus N)")
+    return rank, world, local_rank
+
+
+def init_rank(args):
+    """Select this rank's GPU and join the job's process group (nccl = RCCL)."""
+    rank, world, local_rank = rank_env(args)
+    import torch
+    import torch.distributed as dist
+    have = torch.cuda.device_count()
+    if local_rank >= have:
+        raise SystemExit(f"bench: rank {rank} wants GPU {local_rank} but only {have} are visible")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank),
+                                timeout=datetime.timedelta(seconds=600))
+        assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
+    return rank, world, local_rank, torch, dist
+
+
+def main_launcher_check(args):
+    """--mode launcher-check: the rank side of the launcher without a GPU (gloo). Every
+    rank checks its env against --gpus, all-reduces its rank, and rank 0 prints one JSON
+    line; --fail-rank r makes rank r exit 3 (tests the launcher's failure path)."""
+    rank, world, _ = rank_env(args)
+    import torch
+    import torch.distributed as dist
+    if rank == args.fail_rank:
+        raise SystemExit(3)
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=60))
+    assert dist.get_world_size() == world
+    t = torch.tensor([float(rank)], dtype=torch.float64)
+    dist.all_reduce(t)
+    ranks = [None] * world
+    dist.all_gather_object(ranks, {"rank": rank, "pid": os.getpid()})
+    if rank == 0:
+        print(json.dumps({"metric": "launcher-check", "n_gpus": world, "rank_sum": float(t.item()),
+                          "pids": [r["pid"] for r in ranks]}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -113,21 +224,31 @@ def main():
     ap.add_argument("--skip-cpu", action="store_true", help="skip the CPU baseline leg (profiling runs)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event pass")
     ap.add_argument("--profile-steps", type=int, default=2, help="eager steps timed per kernel after the timed region")
-    ap.add_argument("--mode", choices=("replicas", "dist", "single", "select", "grad", "posterior", "rand"),
+    ap.add_argument("--mode", choices=("replicas", "dist", "single", "select", "grad", "posterior", "rand",
+                                       "launcher-check"),
                     default="replicas",
                     help="replicas (default, the headline metric): independent evals per GPU; dist: one "
                          "evaluation spread over all ranks (BASELINE configs[3], N=65536); single: the "
                          "single-GPU path at --n (comparison line for dist); select: BASELINE configs[4], "
                          "64 candidate formulas x N=8192 through gaplac_logpdf_batch, sharded over ranks; "
                          "grad: logpdf + gradient (gaplac_logpdf_grad, the mcmc/NUTS step) on the configs[2] workload; "
-                         "posterior: mean_and_var(posterior(fx, y), xs) at --m test points; rand: one FiniteGP draw")
+                         "posterior: mean_and_var(posterior(fx, y), xs) at --m test points; rand: one FiniteGP draw; "
+                         "launcher-check: the multi-rank launcher on gloo without a GPU (tests)")
     ap.add_argument("--m", type=int, default=1024, help="posterior mode: test points")
     ap.add_argument("--loopback", type=int, default=0,
                     help="dist mode on ONE GPU: emulate this many ranks in-process (schedule timing only)")
     ap.add_argument("--spw", type=int, default=4, help="dist mode: super-panel width in 128-column tiles")
     ap.add_argument("--no-dist", action="store_true",
                     help="replicas mode with --gpus > 1: skip the configs[3] distributed extra line")
-    args = ap.parse_args()
+    ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # launcher-check only
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus, argv, need_gpus=args.mode != "launcher-check")
+    if args.mode == "launcher-check":
+        return main_launcher_check(args)
     if args.mode in ("dist", "single"):
         return main_dist(args)
     if args.mode == "select":
@@ -137,17 +258,7 @@ def main():
     if args.mode in ("posterior", "rand"):
         return main_post(args)
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-
-    import torch
-    import torch.distributed as dist
-
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank),
-                                timeout=datetime.timedelta(seconds=300))
+    rank, world, local_rank, torch, dist = init_rank(args)
 
     from gaplac_amd.backend import Context
 
@@ -238,7 +349,8 @@ def main():
     dist_line = None
     if world > 1 and not args.no_dist:
         ctx.close()  # free the N=16384 workspace before the 65536 one
-        dist_line = measure_config3_dist(rank, world, local_rank, torch, dist)
+        single_lp = n65536["last_logpdf"] if n65536 else None
+        dist_line = measure_config3_dist(rank, world, local_rank, torch, dist, single_lp=single_lp)
 
     total_evals = args.steps * world
     value = total_evals / elapsed
@@ -338,14 +450,19 @@ def main():
         "cpu_baseline": cpu,
         "extra": extra,
     }
+    rc = 0
     if dist_line is not None:
-        # a failed configs[3] line must not hide behind a good replicas headline
-        out["dist_ok"] = "error" not in dist_line
+        # a failed or non-matching configs[3] line must not hide behind a good replicas
+        # headline: the line is printed, then the process exits non-zero
+        out["dist_ok"] = "error" not in dist_line and bool(dist_line.get("parity_ok"))
         if not out["dist_ok"]:
-            print(f"bench: configs[3] distributed line FAILED: {dist_line['error']}", file=sys.stderr, flush=True)
+            why = dist_line.get("error") or f"parity_vs_single {dist_line.get('parity_vs_single')} > {DIST_PARITY_BAR}"
+            print(f"bench: configs[3] distributed line FAILED: {why}", file=sys.stderr, flush=True)
+            rc = 4
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return rc
 
 
 def measure_config1(ctx, torch, steps: int = 8):
@@ -442,49 +559,67 @@ def measure_config4(local_rank: int, torch, steps: int = 2):
                          "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / PEAK_F64_TFLOPS, 4)}}
 
 
-def measure_config3_dist(rank: int, world: int, local_rank: int, torch, dist, steps: int = 3):
+def measure_config3_dist(rank: int, world: int, local_rank: int, torch, dist, steps: int = 3,
+                         single_lp: float | None = None):
     """BASELINE configs[3]: SqExp(:x; l=1.5), N=65536, one evaluation over all ranks of the
     job (1-D block-column cyclic Cholesky, panel broadcasts with RCCL over xGMI,
-    gaplac_amd/distributed.py). Strong scaling: the work per evaluation is fixed."""
+    gaplac_amd/distributed.py). Strong scaling: the work per evaluation is fixed.
+
+    Rank 0 checks the distributed logpdf against the single-GPU evaluation of the same
+    input (single_lp, or one evaluated here): parity_vs_single, bar DIST_PARITY_BAR.
+    A failure on another rank raises (the launcher then stops the job, non-zero)."""
+    try:
+        line = _config3_dist(rank, world, local_rank, torch, dist, steps)
+    except Exception as e:
+        if rank != 0:
+            raise
+        return {"error": repr(e)[:400]}
+    if rank == 0:
+        if single_lp is None:
+            single_lp = measure_config3_single(local_rank, torch, steps=1)["last_logpdf"]
+        rel = abs(line["last_logpdf"] - single_lp) / abs(single_lp)
+        line.update(single_gpu_logpdf=single_lp, parity_vs_single=rel, parity_bar=DIST_PARITY_BAR,
+                    parity_ok=bool(rel <= DIST_PARITY_BAR))
+    return line
+
+
+def _config3_dist(rank: int, world: int, local_rank: int, torch, dist, steps: int):
     from gaplac_amd import distributed as DI
     x, v = CF.config3_inputs()
     N = x.shape[0]
-    try:
-        dx = torch.from_numpy(x).to("cuda")
-        dvv = torch.from_numpy(v).to("cuda")
-        r = DI.DistRank(local_rank, world, rank, spw=DI.DEFAULT_SPW)
-        tr = DI.TorchTransport(device=torch.device("cuda", local_rank), timing=True)
+    dx = torch.from_numpy(x).to("cuda")
+    dvv = torch.from_numpy(v).to("cuda")
+    r = DI.DistRank(local_rank, world, rank, spw=DI.DEFAULT_SPW)
+    tr = DI.TorchTransport(device=torch.device("cuda", local_rank), timing=True)
 
-        def one():
-            return DI.logpdf_dist_device([r], tr, N, 1, dx.data_ptr(), N, CF.CONFIG3_TERMS, CF.NOISE_VAR,
-                                         dvv.data_ptr())
+    def one():
+        return DI.logpdf_dist_device([r], tr, N, 1, dx.data_ptr(), N, CF.CONFIG3_TERMS, CF.NOISE_VAR,
+                                     dvv.data_ptr())
 
-        one()  # warmup (workspace, lists, RCCL communicator)
-        tr.reset_timing()
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        lp = None
-        for _ in range(steps):
-            lp = one()
-        torch.cuda.synchronize()
-        dist.barrier()
-        el = time.perf_counter() - t0
-        t = torch.tensor([el, tr.bcast_ms() / steps], dtype=torch.float64, device="cuda")
-        allt = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(allt, t)
-        r.close()
-        el = max(float(a[0].item()) for a in allt)
-        bc = [round(float(a[1].item()), 3) for a in allt]
-        flops = N ** 3 / 3.0 + N ** 2
-        tf = flops * steps / el / 1e12 / world
-        return {"workload": f"BASELINE configs[3]: SqExp(:x; l=1.5), N={N}, noise 0.1, one evaluation over {world} GPUs",
-                "value": steps / el, "unit": "evals/s", "ms_per_eval": el / steps * 1e3, "scaling": "strong",
-                "ranks_seen": len(allt), "bcast_ms_per_eval_per_rank": bc, "last_logpdf": lp,
-                "achieved_tflops_per_gpu": round(tf, 3), "frac_of_fp64_peak": round(tf / PEAK_F64_TFLOPS, 4),
-                "transport": "torch.distributed nccl (RCCL) broadcast on the library's comm stream"}
-    except Exception as e:  # the replicas headline stands on its own; report the failure
-        return {"error": repr(e)[:400]}
+    one()  # warmup (workspace, lists, RCCL communicator)
+    tr.reset_timing()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lp = None
+    for _ in range(steps):
+        lp = one()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el, tr.bcast_ms() / steps], dtype=torch.float64, device="cuda")
+    allt = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(allt, t)
+    r.close()
+    el = max(float(a[0].item()) for a in allt)
+    bc = [round(float(a[1].item()), 3) for a in allt]
+    flops = N ** 3 / 3.0 + N ** 2
+    tf = flops * steps / el / 1e12 / world
+    return {"workload": f"BASELINE configs[3]: SqExp(:x; l=1.5), N={N}, noise 0.1, one evaluation over {world} GPUs",
+            "value": steps / el, "unit": "evals/s", "ms_per_eval": el / steps * 1e3, "scaling": "strong",
+            "ranks_seen": len(allt), "bcast_ms_per_eval_per_rank": bc, "last_logpdf": lp,
+            "achieved_tflops_per_gpu": round(tf, 3), "frac_of_fp64_peak": round(tf / PEAK_F64_TFLOPS, 4),
+            "transport": "torch.distributed nccl (RCCL) broadcast on the library's comm stream"}
 
 
 def cpu_grad_baseline(N: int):
@@ -509,16 +644,9 @@ def cpu_grad_baseline(N: int):
 
 def main_grad(args):
     """logpdf + gradient evals/s (the mcmc NUTS step: gaplac_logpdf_grad_device), replicas."""
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    import torch.distributed as dist
+    rank, world, local_rank, torch, dist = init_rank(args)
     from gaplac_amd.backend import Context
 
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     N = args.n
     X, v = make_inputs(N)
     dX = torch.from_numpy(np.ascontiguousarray(X.T)).to("cuda")
@@ -617,16 +745,9 @@ def main_post(args):
     """posterior: mean_and_var(posterior(FiniteGP(X, 0.1), y), xs) over M test points
     (gaplac_posterior_mean_var; src/plotting.jl:8-12); rand: rand(FiniteGP(X, 0.1)) = L z
     (gaplac_rand; CLI/src/sample.jl:25). configs[2] kernel and inputs; replicas over ranks."""
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    import torch.distributed as dist
+    rank, world, local_rank, torch, dist = init_rank(args)
     from gaplac_amd.backend import Context
 
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     N, M = args.n, args.m
     X, v = make_inputs(N)
     rng = np.random.default_rng(5)
@@ -701,17 +822,10 @@ select_models = CF.select_models
 def main_select(args):
     """Batched select over 64 formulas (one gaplac_logpdf_batch call per rank; candidates
     sharded round-robin over ranks, results all-gathered: gaplac_amd/replicas.py)."""
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    import torch.distributed as dist
+    rank, world, local_rank, torch, dist = init_rank(args)
     from gaplac_amd import replicas
     from gaplac_amd.backend import Context
 
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     N = args.n if args.n != N_DEFAULT else CF.N4
     X, y = CF.config4_inputs(N)
     models = select_models()
@@ -759,17 +873,10 @@ def main_select(args):
 
 def main_dist(args):
     """One evaluation spread over the ranks of the job (strong scaling: total work fixed)."""
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    import torch.distributed as dist
+    rank, world, local_rank, torch, dist = init_rank(args)
     from gaplac_amd import distributed as DI
     from gaplac_amd.backend import Context
 
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     N = args.n if args.n != N_DEFAULT else CF.N3
     x, v = make_inputs_dist(N)
     dX = torch.from_numpy(x).to("cuda")
@@ -828,4 +935,4 @@ def main_dist(args):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -24,6 +24,7 @@ EXPORTED = (
     "gaplac_last_error",
     "gaplac_ctx_create",
     "gaplac_ctx_destroy",
+    "gaplac_ctx_release",
     "gaplac_logpdf",
     "gaplac_logpdf_device",
     "gaplac_logpdf_batch",
@@ -110,6 +111,7 @@ def load() -> ctypes.CDLL:
     lib.gaplac_last_error.argtypes = [c_void_p]
     lib.gaplac_ctx_create.argtypes = [c_int, POINTER(c_void_p)]
     lib.gaplac_ctx_destroy.argtypes = [c_void_p]
+    lib.gaplac_ctx_release.argtypes = [c_void_p]
     common = [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, POINTER(Term), c_double, c_void_p]
     lib.gaplac_logpdf.argtypes = common + [_DP, _DP, _DP]
     lib.gaplac_logpdf_device.argtypes = common + [_DP, _DP, _DP]

@@ -56,6 +56,10 @@ class Context:
             self.lib.gaplac_ctx_destroy(self.h)
             self.h = None
 
+    def release(self):
+        """Free the large device workspaces (gaplac_ctx_release); the next call re-allocates."""
+        self._check(self.lib.gaplac_ctx_release(self.h))
+
     def __del__(self):
         try:
             self.close()

@@ -79,6 +79,7 @@ struct gaplac_ctx {
     size_t ttasks_elems = 0;
     int ttasks_T = -1, ttasks_n = 0;
     std::string ttrace_path;     // GAPLAC_TAIL_TRACE: append per-task times of every tail launch here
+    int tail_fault = -1;         // GAPLAC_TAIL_FAULT (tests only): skip this tail column's diagonal block
     unsigned long long* ttrace = nullptr;
     size_t ttrace_elems = 0;
     gaplac_stats stats{};
@@ -634,6 +635,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             }
             TailArgs ta{ctx->A, lda, N, ts, T, ctx->Dinv, ctx->dres, ctx->tctl, ctx->ttasks, nts,
                         ctx->ttrace_path.empty() ? nullptr : ctx->ttrace};
+            ta.fault = ctx->tail_fault;
             // batch lanes run their tails side by side: each persistent grid takes its share
             // of the CUs (one tail workgroup fills a CU's LDS), so no tail waits for another
             launch_tail(sm, ta, std::min(std::max(1, ctx->ncu / std::max(1, ctx->tail_share)), nts), slot(ctx, 10, 0));
@@ -1083,36 +1085,52 @@ static int batch_tail_enqueue(gaplac_ctx* ctx, int64_t N, const std::vector<Term
         w.tasks_lag = lkey;
         w.tasks_n = (int)all.size();
     }
+    const bool trace = !ctx->ttrace_path.empty();  // diagnostics: launches one at a time
+    if (trace && (rc = ensure(ctx, &ctx->ttrace, &ctx->ttrace_elems, 3 * (size_t)w.tasks_n))) return rc;
     hipStream_t g = ctx->s_panel, s = ctx->s_main;
     for (int b = 0; b < B; ++b) w.htp[b] = packs[(size_t)(m0 + b)];
+    // From the first enqueue on, a failure must not leave this call's work in flight (the
+    // Grams read dX / dv, which the next call's upload overwrites): drain both streams first.
+    auto bail = [&](int code) {
+        (void)hipStreamSynchronize(g);
+        (void)hipStreamSynchronize(s);
+        return code;
+    };
+#define BATCHCK(call)                                                                                    \
+    do {                                                                                                 \
+        hipError_t e_ = (call);                                                                          \
+        if (e_ != hipSuccess)                                                                            \
+            return bail(set_err(ctx, GAPLAC_E_HIP, "%s failed: %s", #call, hipGetErrorString(e_)));      \
+    } while (0)
     LaunchGuard guard;
     guard.base = w.A;
     guard.elems = (int64_t)(astride * (size_t)B);
     {
         GuardScope scope(&guard);
-        HIPCK(ctx, hipMemcpyAsync(w.dtp, w.htp, sizeof(TermPack) * (size_t)B, hipMemcpyHostToDevice, g));
+        BATCHCK(hipMemcpyAsync(w.dtp, w.htp, sizeof(TermPack) * (size_t)B, hipMemcpyHostToDevice, g));
         for (int b = 0; b < B; ++b) {
             launch_init_result(g, w.dres + b);
             launch_gram(g, w.A + astride * (size_t)b, lda, N, nt, ctx->dX, N, ctx->dv, w.dtp + b, 0, 0, nullptr);
         }
-        HIPCK(ctx, hipEventRecord(w.ev_gram, g));
-        HIPCK(ctx, hipStreamWaitEvent(s, w.ev_gram, 0));
-        HIPCK(ctx, hipMemsetAsync(w.ctl, 0, sizeof(TailCtl) * (size_t)B, s));
-        const bool trace = !ctx->ttrace_path.empty();  // diagnostics: launches one at a time
-        if (trace && (rc = ensure(ctx, &ctx->ttrace, &ctx->ttrace_elems, 3 * (size_t)w.tasks_n))) return rc;
+        BATCHCK(hipEventRecord(w.ev_gram, g));
+        BATCHCK(hipStreamWaitEvent(s, w.ev_gram, 0));
+        BATCHCK(hipMemsetAsync(w.ctl, 0, sizeof(TailCtl) * (size_t)B, s));
         TailArgs ta{w.A, lda, N, 0, nt, w.Dinv, w.dres, w.ctl, w.tasks, w.tasks_n, trace ? ctx->ttrace : nullptr};
         ta.a_stride = (int64_t)astride;
         ta.dinv_stride = (int64_t)dstride;
         ta.nmodels = B;
-        launch_tail(s, ta, std::min(ctx->ncu, w.tasks_n), nullptr);
+        ta.fault = ctx->tail_fault;
+        if (!guard.violations) launch_tail(s, ta, std::min(ctx->ncu, w.tasks_n), nullptr);
         for (int b = 0; b < B; ++b)
             launch_reduce(s, w.A + astride * (size_t)b, lda, N, (int64_t)nt * NB, ColMap{1, 0, 1}, w.dres + b);
     }
     if (guard.violations)
-        return set_err(ctx, GAPLAC_E_ARG, "batched tail: launch footprint outside the workspace: %s", guard.first.c_str());
-    HIPCK(ctx, hipGetLastError());
-    HIPCK(ctx, hipMemcpyAsync(w.hres, w.dres, sizeof(EvalResult) * (size_t)B, hipMemcpyDeviceToHost, s));
-    HIPCK(ctx, hipEventRecord(w.ev_done, s));
+        return bail(set_err(ctx, GAPLAC_E_ARG, "batched tail: launch footprint outside the workspace: %s",
+                            guard.first.c_str()));
+    BATCHCK(hipGetLastError());
+    BATCHCK(hipMemcpyAsync(w.hres, w.dres, sizeof(EvalResult) * (size_t)B, hipMemcpyDeviceToHost, s));
+    BATCHCK(hipEventRecord(w.ev_done, s));
+#undef BATCHCK
     w.busy = true;
     w.m0 = m0;
     w.B = B;
@@ -1168,6 +1186,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (ctx->tailk) ctx->tail_s = 80;  // the persistent tail (A/B at N = 16384)
     if (const char* s = std::getenv("GAPLAC_TAIL_S")) ctx->tail_s = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_TAIL_TRACE")) ctx->ttrace_path = s;  // diagnostics
+    if (const char* s = std::getenv("GAPLAC_TAIL_FAULT")) ctx->tail_fault = std::atoi(s);  // tests: forced expiry
     if (const char* s = std::getenv("GAPLAC_BATCH_W")) ctx->batch_w = std::max(1, std::min(TAIL_MAX_MODELS, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BATCH_LAG")) ctx->batch_lag = std::max(0, std::atoi(s));
     auto fail = [&](const char* what, hipError_t e) {
@@ -1293,6 +1312,30 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     return 0;
 }
 
+int gaplac_ctx_release(gaplac_ctx* ctx) {
+    if (!ctx) return GAPLAC_E_ARG;
+    HIPCK(ctx, hipSetDevice(ctx->device));
+    HIPCK(ctx, hipStreamSynchronize(ctx->s_main));
+    HIPCK(ctx, hipStreamSynchronize(ctx->s_panel));
+    if (ctx->s_extra) HIPCK(ctx, hipStreamSynchronize(ctx->s_extra));
+    for (gaplac_ctx* c : ctx->lanes) gaplac_ctx_destroy(c);
+    ctx->lanes.clear();
+    auto drop = [](double*& p, size_t& n) {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    };
+    drop(ctx->A, ctx->A_elems);
+    drop(ctx->Dinv, ctx->Dinv_elems);
+    for (auto& w : ctx->bw) {
+        if (w.busy) HIPCK(ctx, hipEventSynchronize(w.ev_done));
+        w.busy = false;
+        drop(w.A, w.A_elems);
+        drop(w.Dinv, w.Dinv_elems);
+    }
+    return 0;
+}
+
 int gaplac_logpdf_device(gaplac_ctx* ctx, int64_t N, int32_t D, const double* dX, int64_t ldx,
                          int32_t T, const gaplac_term* terms, double noise, const double* dv,
                          double* out_logpdf, double* out_logdet, double* out_quad) {
@@ -1362,14 +1405,31 @@ int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D, 
     HIPCK(ctx, hipSetDevice(ctx->device));
     {
         const int nt = (int)(round_up(N + 1, NB) / NB);
-        if (nmodels >= 2 && whole_in_tail(ctx, nt)) {  // batched tail
+        // Models per batched launch, capped by the free device memory: two workspace sets of
+        // bw matrices must fit beside everything else on the device (what the sets already
+        // hold is reusable). Below two models per set the lane path runs instead.
+        int bwid = std::min(ctx->batch_w, std::max(nmodels, 1));
+        if (nmodels >= 2 && whole_in_tail(ctx, nt)) {
+            const int64_t Np = (int64_t)nt * NB;
+            const size_t per = ((size_t)Np * (size_t)Np + (size_t)nt * DINV_PER_BLOCK) * sizeof(double) +
+                               sizeof(TailCtl) + sizeof(EvalResult) + sizeof(TermPack);
+            size_t freeb = 0, totalb = 0;
+            if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
+                size_t held = 0;
+                for (const auto& w : ctx->bw) held += (w.A_elems + w.Dinv_elems) * sizeof(double);
+                const size_t margin = (size_t)2 << 30;  // 2 GiB for everything else
+                const size_t budget = freeb + held > margin ? freeb + held - margin : 0;
+                bwid = (int)std::min<size_t>((size_t)bwid, budget / (2 * per));
+            }
+        }
+        if (nmodels >= 2 && bwid >= 2 && whole_in_tail(ctx, nt)) {  // batched tail
             for (gaplac_ctx* c : ctx->lanes) HIPCK(ctx, hipStreamSynchronize(c->s_main));
             if ((rc = upload(ctx, N, D, X, ldx, v))) return rc;
             HIPCK(ctx, hipStreamSynchronize(ctx->s_main));  // the Grams read X / v on s_panel
             for (int m = 0; m < nmodels; ++m) packs[(size_t)m].noise = noise;
             int p = 0;
-            for (int m0 = 0; m0 < nmodels; m0 += ctx->batch_w, p ^= 1) {
-                const int B = std::min(ctx->batch_w, nmodels - m0);
+            for (int m0 = 0; m0 < nmodels; m0 += bwid, p ^= 1) {
+                const int B = std::min(bwid, nmodels - m0);
                 if ((rc = batch_tail_enqueue(ctx, N, packs, m0, B, p, out_logpdf, out_info))) break;
             }
             // collect both sets (also after a failure: nothing of this call stays in flight)

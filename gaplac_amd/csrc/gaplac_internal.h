@@ -107,6 +107,10 @@ struct TailArgs {
     // counters ctl + m (ctl[0].head is the one dequeue counter)
     int64_t a_stride = 0, dinv_stride = 0;
     int nmodels = 1;
+    // debug (GAPLAC_TAIL_FAULT, tests only): the diagonal-block task of relative tile column
+    // fault is skipped, never publishing, so every wait behind it expires and the evaluation
+    // must come back as GAPLAC_E_HIP; -1 = off
+    int fault = -1;
 };
 constexpr int TAIL_MODEL_SHIFT = 27;
 constexpr int TAIL_MAX_MODELS = 32;

@@ -2177,6 +2177,11 @@ __global__ __launch_bounds__(256) void lower_mv_reduce_kernel(const double* __re
 // bounded (0.2 s); an expired wait sets TailCtl::err, which the host turns into GAPLAC_E_HIP.
 // =================================================================================
 enum { TK_D = 0, TK_S = 1, TK_U = 2, TK_Q = 3 };
+constexpr unsigned long long TAIL_WAIT_TICKS = 20000000ull;  // 0.2 s of the 100 MHz wall clock
+
+__device__ __forceinline__ unsigned tail_ld(const unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 constexpr int TAIL_S_WHOLE = 2;  // S task q: the whole 128-row tile, after D(k) (else q = row half)
 constexpr unsigned TAIL_NQ = 10;  // Q blocks per diagonal tile (= units a diagonal U adds)
 
@@ -2287,7 +2292,7 @@ __device__ __forceinline__ void tail_trsm(double* smem, double* Acol, int64_t ld
 template <int AUX>
 __device__ __forceinline__ void tail_trsm_pipe(double* smem, unsigned* rowf, double* Acol, int64_t lda, int k, int bi,
                                                int h, const double* Dk, const unsigned* prog, const unsigned* ddone,
-                                               unsigned* err) {
+                                               unsigned* err, unsigned* rerr) {
     double* Ls = smem;  // (TRSM_LBLK + NDB) x 256, as tail_trsm_stage lays it out
     const int tid = otid(), wave = tid >> 6, lane = tid & 63;
     const int fr = lane >> 4, fc = lane & 15;
@@ -2313,8 +2318,9 @@ __device__ __forceinline__ void tail_trsm_pipe(double* smem, unsigned* rowf, dou
                         avail = pr < NDB - 1 ? pr : NDB - 1;
                     }
                     if (avail > next) break;
-                    if (wall_clock64() - t0 > 20000000ull) {
-                        avail = NDB;  // expired: stage what is there, flag the error
+                    // expired (or another task already failed): stage what is there, flag it
+                    if (wall_clock64() - t0 > TAIL_WAIT_TICKS || tail_ld(err) != 0u) {
+                        avail = NDB;
                         timeout = true;
                         break;
                     }
@@ -2343,7 +2349,10 @@ __device__ __forceinline__ void tail_trsm_pipe(double* smem, unsigned* rowf, dou
                     __hip_atomic_fetch_add(&rowf[b], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             next = avail;
         }
-        if (timeout && lane == 0) atomicOr(err, 1u);
+        if (timeout && lane == 0) {
+            atomicOr(err, 1u);
+            atomicOr(rerr, 2u);  // straight into the result record (no exit-time read needed)
+        }
         return;
     }
     const uint32_t rowb = (uint32_t)((int64_t)bi * NB + 64 * h + 16 * wave);
@@ -2355,12 +2364,21 @@ __device__ __forceinline__ void tail_trsm_pipe(double* smem, unsigned* rowf, dou
     d4 Y[NDB];
 #pragma unroll
     for (int b = 0; b < NDB; ++b) {
-        // row b staged by all four staging waves (bounded: they always get there, a
-        // timed-out wait above stages stale data and flags the error)
-        for (int it = 0; it < (1 << 22); ++it) {
-            if (__hip_atomic_load(&rowf[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= 4u) break;
-            __builtin_amdgcn_s_sleep(1);
+        // row b staged by all four staging waves. Bounded on the wall clock at twice the
+        // staging waves' own bound (they always get here, a timed-out wait above stages stale
+        // data and flags it); an expiry here flags the evaluation too, never a silent result.
+        if (lane == 0) {
+            const unsigned long long t0 = wall_clock64();
+            while (__hip_atomic_load(&rowf[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4u) {
+                if (wall_clock64() - t0 > 2 * TAIL_WAIT_TICKS) {
+                    atomicOr(err, 1u);
+                    atomicOr(rerr, 2u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
         }
+        __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         d4 s0 = Bt[b], s1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -2489,11 +2507,9 @@ __device__ __forceinline__ void tail_q32(const Gm<AUX>& gC, const Gm<AUX>& gP, i
     for (int rg = 0; rg < 4; ++rg) gC.st((uint32_t)((int64_t)(c0 + fr + 4 * rg) * lda + r0 + fc), acc[rg]);
 }
 
-__device__ __forceinline__ unsigned tail_ld(const unsigned* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // Lane 0: wait until the task's inputs are final (bounded: 0.2 s of the 100 MHz clock).
+// Returns false when the bound expires or another task has already failed (TailCtl::err
+// set: then every later wait returns at once and the launch drains quickly).
 __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int k, int i, int j) {
     const unsigned long long t0 = wall_clock64();
     for (;;) {
@@ -2511,7 +2527,7 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int
                 ok = tail_ld(&c->sdone[i * TAIL_TMAX + k + c2]) >= 2u && tail_ld(&c->sdone[j * TAIL_TMAX + k + c2]) >= 2u;
         }
         if (ok) return true;
-        if (wall_clock64() - t0 > 20000000ull) return false;  // 0.2 s
+        if (wall_clock64() - t0 > TAIL_WAIT_TICKS || tail_ld(&c->err) != 0u) return false;
         __builtin_amdgcn_s_sleep(2);
     }
 }
@@ -2536,12 +2552,16 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         double* const Dinv = a.Dinv + m * a.dinv_stride;
         EvalResult* const res = a.res + m;
         if (a.trace && threadIdx.x == 0) a.trace[3 * tk] = wall_clock64();
-        if (threadIdx.x == 0 && !tail_wait(ctl, type, q, k, i, j)) atomicOr(&ctl->err, 1u);
+        if (threadIdx.x == 0 && !tail_wait(ctl, type, q, k, i, j)) {
+            atomicOr(&ctl->err, 1u);
+            atomicOr(&res->err, 2u);  // the result record itself: the host sees it whatever the exit order
+        }
         __syncthreads();
         if (a.trace && threadIdx.x == 0) a.trace[3 * tk + 1] = wall_clock64();
         const int gk = a.ts + k;
         double* colk = A + (int64_t)gk * NB * a.lda;
         if (type == TK_D) {
+            if (k == a.fault) continue;  // debug (GAPLAC_TAIL_FAULT): D(k) never runs nor publishes
             if ((int64_t)gk * NB < a.N)
                 potrf_diag2_body<GM_SC1>(smem, colk + (int64_t)gk * NB, a.lda, a.N, (int64_t)gk * NB,
                                          Dinv + (size_t)gk * DINV_PER_BLOCK, res, nullptr, &ctl->dprog[k]);
@@ -2549,7 +2569,7 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
             tail_trsm<GM_SC1>(smem, colk, a.lda, gk, a.ts + i, q, Dinv + (size_t)gk * DINV_PER_BLOCK);
         } else if (type == TK_S) {
             tail_trsm_pipe<GM_SC1>(smem, s_rowf, colk, a.lda, gk, a.ts + i, q, Dinv + (size_t)gk * DINV_PER_BLOCK,
-                                   &ctl->dprog[k], &ctl->ddone[k], &ctl->err);
+                                   &ctl->dprog[k], &ctl->ddone[k], &ctl->err, &res->err);
         } else {
             const int gi = a.ts + i, gj = a.ts + j;
             const Gm<GM_SC1> gC(A + (int64_t)gj * NB * a.lda), gP(colk);
@@ -2588,7 +2608,7 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
             if (a.trace) a.trace[3 * tk + 2] = wall_clock64();
         }
     }
-    if (threadIdx.x < a.nmodels && a.ctl[threadIdx.x].err) atomicOr(&a.res[threadIdx.x].err, 2u);
+    if (threadIdx.x < a.nmodels && tail_ld(&a.ctl[threadIdx.x].err) != 0u) atomicOr(&a.res[threadIdx.x].err, 2u);
     kt_end(kt);
 }
 

@@ -84,6 +84,11 @@ typedef struct gaplac_ctx gaplac_ctx;
  * logpdf); needed so repeated MCMC evaluations do not re-allocate. */
 int  gaplac_ctx_create(int device, gaplac_ctx** out);
 int  gaplac_ctx_destroy(gaplac_ctx* ctx);
+/* Free the context's large device workspaces (the evaluation matrix, the batched-select
+ * workspace sets, the batch lanes) after waiting for its work; the next call allocates
+ * again. For callers that share a device between several contexts or processes.
+ * Replaces: nothing (the reference frees its temporaries per call). */
+int  gaplac_ctx_release(gaplac_ctx* ctx);
 const char* gaplac_last_error(const gaplac_ctx* ctx);
 int  gaplac_abi_version(void);
 
@@ -111,7 +116,9 @@ int gaplac_logpdf_device(gaplac_ctx* ctx, int64_t N, int32_t D, const double* dX
  * nmodels entries; the return value is 0 when the batch ran (per-model PD failures are
  * reported in out_info[m] > 0 with out_logpdf[m] = NaN) and <0 on argument/runtime
  * errors. Each result is bitwise that model's gaplac_logpdf. Device memory: up to two
- * workspace sets of GAPLAC_BATCH_W (32) matrices of (N+1 rounded up to 128)^2 doubles. */
+ * workspace sets of GAPLAC_BATCH_W (32) matrices of (N+1 rounded up to 128)^2 doubles,
+ * fewer models per set when the free device memory (hipMemGetInfo, 2 GiB kept free) does
+ * not hold them, and the two-lane path below two; gaplac_ctx_release frees them. */
 int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D,
                         const double* X, int64_t ldx, const int32_t* term_offset,
                         const gaplac_term* terms, double noise, const double* v,

@@ -1,0 +1,67 @@
+"""bench.py's multi-rank launcher (CPU, gloo): `python bench.py --gpus N` with no WORLD_SIZE
+in the env starts N ranks of itself, every rank checks WORLD_SIZE == --gpus, and a failing
+rank's status ends the job. The driver's 8-GPU scaling run goes through exactly this path
+(or through torch.distributed.run, which sets the same variables)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(kw)
+    return env
+
+
+def _run(args, env=None, timeout=180):
+    return subprocess.run([sys.executable, BENCH, *args], env=env or _env(), capture_output=True, text=True,
+                          timeout=timeout, cwd=ROOT)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_launcher_starts_n_ranks(n):
+    p = _run(["--gpus", str(n), "--mode", "launcher-check"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(s) for s in p.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    d = lines[0]
+    assert d["n_gpus"] == n
+    assert d["rank_sum"] == n * (n - 1) / 2
+    assert len(set(d["pids"])) == n  # n separate processes
+
+
+def test_launcher_propagates_a_failing_rank():
+    p = _run(["--gpus", "2", "--mode", "launcher-check", "--fail-rank", "1"])
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    assert "rank 1 exited with status 3" in p.stderr
+
+
+def test_launcher_refuses_more_ranks_than_gpus():
+    # this container has no GPU: a GPU mode with --gpus 2 must fail before starting ranks
+    p = _run(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+    assert p.returncode == 2, (p.returncode, p.stderr[-2000:])
+    assert "needs 2 visible GPUs" in p.stderr
+    assert not any(s.startswith("{") for s in p.stdout.splitlines())
+
+
+def test_rank_checks_world_against_gpus():
+    # launched as one rank of a job whose size differs from --gpus (a mis-sized torchrun)
+    env = _env(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT="29555")
+    p = _run(["--gpus", "2", "--mode", "launcher-check"], env=env)
+    assert p.returncode != 0
+    assert "--gpus 2 but WORLD_SIZE=1" in p.stderr
+
+
+def test_launch_ranks_return_codes(monkeypatch):
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.launch_ranks(2, ["--gpus", "2", "--mode", "launcher-check"], need_gpus=False) == 0
+    assert bench.launch_ranks(2, ["--gpus", "2", "--mode", "launcher-check", "--fail-rank", "0"],
+                              need_gpus=False) == 3
