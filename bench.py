@@ -221,7 +221,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=N_DEFAULT)
-    ap.add_argument("--skip-cpu", action="store_true", help="skip the CPU baseline leg (profiling runs)")
+    ap.add_argument("--skip-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the extra size legs (N=4096, N=65536, select, two chains): profiling runs")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event pass")
     ap.add_argument("--profile-steps", type=int, default=2, help="eager steps timed per kernel after the timed region")
     ap.add_argument("--mode", choices=("replicas", "dist", "single", "select", "grad", "posterior", "rand",
@@ -320,7 +322,7 @@ def main():
     if not args.no_profile and rank == 0:
         gram_alone = ctx.gram_time(X, terms_for(LENGTHSCALES[0]), CF.NOISE_VAR, v, reps=5)
 
-    full_run = not args.no_profile and not args.skip_cpu  # profiled runs keep to the timed schedule
+    full_run = not args.no_profile and not args.no_extra  # profiled runs keep to the timed schedule
     # Throughput with two chains per GPU (extra, not the headline): independent evaluations
     # in flight on two lanes (gaplac_logpdf_batch), filling the latency-bound tail of one
     # evaluation's panel chain with the other's bulk updates.
