@@ -36,21 +36,29 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_library(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build_library(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:
+    """The in-tree library (default), or an A/B variant: out = another path, defines =
+    extra -D switches (e.g. ("GAPLAC_EARLY_DEQ=0",)), loaded with GAPLAC_LIB_PATH."""
+    target = out or OUT
+    if out is None and not defines and not force and not _stale():
         return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    tmp = OUT + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+    os.makedirs(os.path.dirname(os.path.abspath(target)), exist_ok=True)
+    tmp = target + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall"]
+    cmd += [f"-D{d}" for d in defines]
+    cmd += ["-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-4000:]}")
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, target)
+    return target
 
 
 if __name__ == "__main__":
-    print(build_library(force="--force" in sys.argv, verbose=True))
+    # python -m gaplac_amd.build [--force] [--out PATH] [-DNAME=VALUE ...]
+    a = sys.argv[1:]
+    out = a[a.index("--out") + 1] if "--out" in a else None
+    print(build_library(force="--force" in a, verbose=True, out=out,
+                        defines=[x[2:] for x in a if x.startswith("-D")]))

@@ -77,9 +77,11 @@ struct gaplac_ctx {
     TailCtl* tctl = nullptr;     // its completion counters (zeroed per launch)
     uint32_t* ttasks = nullptr;  // its task list for ttasks_T tile columns
     size_t ttasks_elems = 0;
-    int ttasks_T = -1, ttasks_n = 0;
+    int ttasks_T = -1, ttasks_n = 0, ttasks_gw = 0;
     std::string ttrace_path;     // GAPLAC_TAIL_TRACE: append per-task times of every tail launch here
     int tail_fault = -1;         // GAPLAC_TAIL_FAULT (tests only): skip this tail column's diagonal block
+    int single_gw = 0;           // GAPLAC_SINGLE_GW: deep-task width of single-evaluation tails (0: by length)
+    int single_gw8_t = 1000;     // GAPLAC_SINGLE_GW8_T: tails of at least this many columns use width 8
     unsigned long long* ttrace = nullptr;
     size_t ttrace_elems = 0;
     gaplac_stats stats{};
@@ -153,6 +155,8 @@ struct gaplac_ctx {
     size_t galpha_elems = 0;
     double* gdv = nullptr;
     size_t gdv_elems = 0;
+    double* gz = nullptr;  // z (row N of the factor), contiguous: alpha's input beside cinv
+    size_t gz_elems = 0;
     double* gpart = nullptr;
     size_t gpart_elems = 0;
     double* gout = nullptr;   // device: T+1 results
@@ -450,6 +454,14 @@ static bool whole_in_tail(const gaplac_ctx* ctx, int nt) {
            nt <= ctx->tail_s;
 }
 
+// Deep-task width of a single evaluation's tail list: far tiles take GW tile columns per
+// task (K = 128 GW). GAPLAC_SINGLE_GW = 4 or 8 for every tail; 0 (default): 8 for tails of
+// at least single_gw8_t tile columns (throughput-bound early columns), 4 below.
+static int single_gw(const gaplac_ctx* ctx, int T) {
+    if (ctx->single_gw == 4 || ctx->single_gw == 8) return ctx->single_gw;
+    return T >= ctx->single_gw8_t ? 8 : 4;
+}
+
 static std::vector<int> superpanel_starts(const gaplac_ctx* ctx, int nt) {
     std::vector<int> sp{0};
     // a matrix the persistent tail covers whole (plain logpdf, at most TAIL_TMAX tile
@@ -612,17 +624,18 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             // the tail as one persistent dataflow launch
             if (ctx->dry) {  // gaplac_plan_check: the task list's dependency order
                 std::vector<uint32_t> host;
-                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP);
+                build_tail_tasks(T, host, nullptr, single_gw(ctx, T), 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP);
                 std::string why;
                 if (!check_tail_tasks(T, host, &why)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
             }
-            if (ctx->ttasks_T != T && !ctx->dry) {
+            if ((ctx->ttasks_T != T || ctx->ttasks_gw != single_gw(ctx, T)) && !ctx->dry) {
                 std::vector<uint32_t> host;
-                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP);
+                build_tail_tasks(T, host, nullptr, single_gw(ctx, T), 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP);
                 int rc;
                 if ((rc = ensure(ctx, &ctx->ttasks, &ctx->ttasks_elems, host.size()))) return rc;
                 HIPCK(ctx, hipMemcpy(ctx->ttasks, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
                 ctx->ttasks_T = T;
+                ctx->ttasks_gw = single_gw(ctx, T);
                 ctx->ttasks_n = (int)host.size();
             }
             if (!ctx->tctl && !ctx->dry)
@@ -715,10 +728,19 @@ int enqueue_eval_body(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt)
         launch_posterior(ctx->s_main, ctx->A, lda, Np, N, ctx->xr_M, ctx->dXs, ctx->xr_M, ctx->dtp, ctx->gpart,
                          ctx->pmean, ctx->pvar);
     if (ctx->xr_mode == 1) {
-        // alpha = Y z, then M = -C^{-1} over the factor storage, contraction, reduction
+        // alpha = Y z on s_extra beside M = -C^{-1} over the factor storage on s_main (both only
+        // read Y; z is copied out first, cinv may overwrite row N), then the contraction and
+        // the reduction on s_main once alpha is in
         hipStream_t sm = ctx->s_main;
+        hipStream_t sx = ctx->serial ? sm : ctx->s_extra;
         launch_zero_tail_cols(sm, ctx->A, lda, Np, N);
-        launch_alpha(sm, ctx->A, lda, Np, N, ctx->gpart, ctx->galpha, ctx->gdv);
+        launch_copy_z(sm, ctx->A, lda, N, ctx->gz);
+        if (sx != sm) {
+            HIPQ(ctx, hipEventRecord(ctx->ev_xinit, sm));
+            HIPQ(ctx, hipStreamWaitEvent(sx, ctx->ev_xinit, 0));
+        }
+        launch_alpha(sx, ctx->A, lda, Np, N, ctx->gz, ctx->gpart, ctx->galpha, ctx->gdv);
+        if (sx != sm) HIPQ(ctx, hipEventRecord(ctx->ev_xdone, sx));
         size_t e0 = 0;
         const bool ev = ctx->prof_mode == 2;
         if (ev) {
@@ -736,6 +758,7 @@ int enqueue_eval_body(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt)
             HIPQ(ctx, hipEventRecord(ctx->evpool[e0 + 1], sm));
             ctx->evpairs.push_back({e0, 0.0, 0.0, 8});
         }
+        if (sx != sm) HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_xdone, 0));
         launch_grad_contract(sm, ctx->A, lda, N, ctx->dX, N, ctx->galpha, ctx->dtp, ctx->dgp, ctx->gpart,
                              slot(ctx, 9, 0));
         const int m = (int)((N + NB - 1) / NB);
@@ -804,6 +827,7 @@ int ensure_workspace(gaplac_ctx* ctx, int64_t N) {
         const size_t part = std::max(nk * (size_t)N, (size_t)m * (m + 1) / 2 * (GAPLAC_MAX_TERMS + 1));
         if ((rc = ensure(ctx, &ctx->galpha, &ctx->galpha_elems, (size_t)N))) return rc;
         if ((rc = ensure(ctx, &ctx->gdv, &ctx->gdv_elems, (size_t)N))) return rc;
+        if ((rc = ensure(ctx, &ctx->gz, &ctx->gz_elems, (size_t)N))) return rc;
         if ((rc = ensure(ctx, &ctx->gpart, &ctx->gpart_elems, part))) return rc;
         if (ctx->glist_m != m) {
             std::vector<uint32_t> host;
@@ -1187,6 +1211,8 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_TAIL_S")) ctx->tail_s = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_TAIL_TRACE")) ctx->ttrace_path = s;  // diagnostics
     if (const char* s = std::getenv("GAPLAC_TAIL_FAULT")) ctx->tail_fault = std::atoi(s);  // tests: forced expiry
+    if (const char* s = std::getenv("GAPLAC_SINGLE_GW")) ctx->single_gw = std::atoi(s);
+    if (const char* s = std::getenv("GAPLAC_SINGLE_GW8_T")) ctx->single_gw8_t = std::max(1, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_BATCH_W")) ctx->batch_w = std::max(1, std::min(TAIL_MAX_MODELS, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BATCH_LAG")) ctx->batch_lag = std::max(0, std::atoi(s));
     auto fail = [&](const char* what, hipError_t e) {
@@ -1280,6 +1306,7 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     if (ctx->pmean) (void)hipFree(ctx->pmean);
     if (ctx->pvar) (void)hipFree(ctx->pvar);
     if (ctx->gdv) (void)hipFree(ctx->gdv);
+    if (ctx->gz) (void)hipFree(ctx->gz);
     if (ctx->gpart) (void)hipFree(ctx->gpart);
     if (ctx->gout) (void)hipFree(ctx->gout);
     if (ctx->hgout) (void)hipHostFree(ctx->hgout);
@@ -1711,7 +1738,7 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
             for (int T = 1; T <= TAIL_TMAX; ++T)
                 for (int gw : {4, 8})
                     for (int near : {2, 3, 4, 8})
-                    for (int ql : {0, 7, 40, TAIL_TMAX})
+                    for (int ql : {0, 7, 24, 40, TAIL_TMAX})
                     for (int wp : {0, 1, 2, 3, 4, 5}) {
                         std::vector<uint32_t> l;
                         build_tail_tasks(T, l, nullptr, gw, near, ql, (wp & 1) != 0, 1 << (wp >> 1));

@@ -217,10 +217,13 @@ void launch_init_result(hipStream_t s, EvalResult* res);
 void launch_init_identity_rows(hipStream_t s, double* A, int64_t lda, int64_t Np, int nt, int W);
 // Zero Y[:, N .. Np) (the columns of the padding / v row).
 void launch_zero_tail_cols(hipStream_t s, double* A, int64_t lda, int64_t Np, int64_t N);
-// alpha = Y z (= C^{-1} v), z = row N of the factor: partial sums per 512-column chunk,
-// then a fixed-order sum; also writes dv = -alpha.
-void launch_alpha(hipStream_t s, const double* A, int64_t lda, int64_t Np, int64_t N, double* partial,
-                  double* alpha, double* dv);
+// z = row N of the factor into a contiguous buffer (N doubles).
+void launch_copy_z(hipStream_t s, const double* A, int64_t lda, int64_t N, double* z);
+// alpha = Y z (= C^{-1} v), z from launch_copy_z: partial sums per 512-column chunk, then a
+// fixed-order sum; also writes dv = -alpha. Reads only the identity rows and z, so it runs
+// beside cinv_tile_kernel (which overwrites the factor storage).
+void launch_alpha(hipStream_t s, const double* A, int64_t lda, int64_t Np, int64_t N, const double* z,
+                  double* partial, double* alpha, double* dv);
 // Product-group bounds per term (the gradient of a term inside a product group carries
 // the group's other terms).
 struct GradTermPack {

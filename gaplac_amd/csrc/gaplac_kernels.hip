@@ -1762,14 +1762,23 @@ __global__ __launch_bounds__(256) void zero_tail_cols_kernel(double* __restrict_
     if (col < Np && r < Np) A[col * lda + Np + r] = 0.0;
 }
 
+// z = row N of the factor (z_k = A[k * lda + N]) into a contiguous buffer: alpha reads it
+// from there while cinv_tile_kernel, which may overwrite row N, runs beside it.
+__global__ __launch_bounds__(256) void copy_z_kernel(const double* __restrict__ A, int64_t lda, int64_t N,
+                                                     double* __restrict__ z) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k < N) z[k] = A[k * lda + N];
+}
+
 // alpha partial sums: block (x, y) = rows 256x .. 256x+255, columns 512y .. 512y+511.
 __global__ __launch_bounds__(256) void alpha_partial_kernel(const double* __restrict__ A, int64_t lda,
-                                                            int64_t Np, int64_t N, double* __restrict__ partial) {
+                                                            int64_t Np, int64_t N, const double* __restrict__ z,
+                                                            double* __restrict__ partial) {
     __shared__ double zs[512];
     const int tid = threadIdx.x;
     const int64_t k0 = (int64_t)blockIdx.y * 512;
     const int64_t i = (int64_t)blockIdx.x * 256 + tid;
-    for (int t = tid; t < 512; t += 256) zs[t] = (k0 + t < N) ? A[(k0 + t) * lda + N] : 0.0;
+    for (int t = tid; t < 512; t += 256) zs[t] = (k0 + t < N) ? z[k0 + t] : 0.0;
     __syncthreads();
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
     // Y is upper triangular: only columns k >= i are read (the tiles below the identity
@@ -2532,14 +2541,24 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int
     }
 }
 
+#ifndef GAPLAC_EARLY_DEQ
+#define GAPLAC_EARLY_DEQ 1  // 0: dequeue at the top of the loop (round 3)
+#endif
 __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict__ kt) {
     __shared__ double smem[DIAG2_SMEM];
     __shared__ unsigned s_task;
     __shared__ unsigned s_rowf[NDB];
     kt_begin(kt);
+    // Dequeue: the next task's index is fetched while the current task's stores drain (the
+    // atomic is issued just before the publish step's vmcnt(0) wait, so its round trip hides
+    // behind the store acknowledgements), and the workgroup holds it for only that long. The
+    // order of dequeues, and with it the no-deadlock argument above, is unchanged: a task
+    // still waits only for tasks dequeued before it.
+    unsigned next_tk = 0;
+    if (GAPLAC_EARLY_DEQ && threadIdx.x == 0) next_tk = atomicAdd(&a.ctl->head, 1u);
     for (;;) {
         __syncthreads();
-        if (threadIdx.x == 0) s_task = atomicAdd(&a.ctl->head, 1u);
+        if (threadIdx.x == 0) s_task = GAPLAC_EARLY_DEQ ? next_tk : atomicAdd(&a.ctl->head, 1u);
         __syncthreads();
         const unsigned tk = s_task;
         if (tk >= (unsigned)a.ntasks) break;
@@ -2560,8 +2579,9 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         if (a.trace && threadIdx.x == 0) a.trace[3 * tk + 1] = wall_clock64();
         const int gk = a.ts + k;
         double* colk = A + (int64_t)gk * NB * a.lda;
-        if (type == TK_D) {
-            if (k == a.fault) continue;  // debug (GAPLAC_TAIL_FAULT): D(k) never runs nor publishes
+        const bool faulted = type == TK_D && k == a.fault;  // debug (GAPLAC_TAIL_FAULT): never runs nor publishes
+        if (faulted) {
+        } else if (type == TK_D) {
             if ((int64_t)gk * NB < a.N)
                 potrf_diag2_body<GM_SC1>(smem, colk + (int64_t)gk * NB, a.lda, a.N, (int64_t)gk * NB,
                                          Dinv + (size_t)gk * DINV_PER_BLOCK, res, nullptr, &ctl->dprog[k]);
@@ -2591,9 +2611,10 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
             }
         }
         // publish: every wave's stores complete, then one lane bumps the counter
+        if (GAPLAC_EARLY_DEQ && threadIdx.x == 0) next_tk = atomicAdd(&a.ctl->head, 1u);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (threadIdx.x == 0 && !faulted) {
             if (type == TK_D) {
                 __hip_atomic_fetch_add(&ctl->ddone[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else if (type == TK_S) {  // two halves per tile (or one whole-tile task): done at 2
@@ -2989,12 +3010,18 @@ void launch_zero_tail_cols(hipStream_t s, double* A, int64_t lda, int64_t Np, in
     zero_tail_cols_kernel<<<dim3((unsigned)((Np + 255) / 256), (unsigned)(Np - N)), dim3(256), 0, s>>>(A, lda, Np, N);
 }
 
-void launch_alpha(hipStream_t s, const double* A, int64_t lda, int64_t Np, int64_t N, double* partial,
-                  double* alpha, double* dv) {
+void launch_copy_z(hipStream_t s, const double* A, int64_t lda, int64_t N, double* z) {
+    if (N <= 0) return;
+    if (!guard_launch("copy_z_kernel", A, 0, (N - 1) * lda + N + 1)) return;
+    copy_z_kernel<<<dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s>>>(A, lda, N, z);
+}
+
+void launch_alpha(hipStream_t s, const double* A, int64_t lda, int64_t Np, int64_t N, const double* z,
+                  double* partial, double* alpha, double* dv) {
     if (N <= 0) return;
     if (!guard_launch("alpha_partial_kernel", A, 0, (N - 1) * lda + Np + N)) return;
     const int nk = (int)((N + 511) / 512);
-    alpha_partial_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nk), dim3(256), 0, s>>>(A, lda, Np, N,
+    alpha_partial_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nk), dim3(256), 0, s>>>(A, lda, Np, N, z,
                                                                                              partial);
     alpha_reduce_kernel<<<dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s>>>(partial, N, nk, alpha, dv);
 }

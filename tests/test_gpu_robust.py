@@ -15,8 +15,17 @@ import pytest
 from gaplac_amd import _native
 from gaplac_amd.backend import Context, GaplacError
 from oracle import restatement as R
+from tests.conftest import gpu_available
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    # the torch probe first, before this module loads the library (like the other GPU files)
+    if not gpu_available():
+        pytest.skip("no GPU")
+
 
 TERMS = [(_native.SQEXP, 0, 1.5, 0)]
 

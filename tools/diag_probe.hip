@@ -17,10 +17,6 @@ __global__ __launch_bounds__(512) void diag_v2(double* Ag, int64_t lda, int64_t 
   __shared__ double smem[DIAG2_SMEM];
   potrf_diag2_body<0>(smem, Ag, lda, N, g0, Dinv, res);
 }
-__global__ __launch_bounds__(512) void diag_v3(double* Ag, int64_t lda, int64_t N, int64_t g0, double* Dinv, EvalResult* res) {
-  __shared__ double smem[DIAG2_SMEM];
-  potrf_diag2_body<0, 1>(smem, Ag, lda, N, g0, Dinv, res);
-}
 
 int main() {
   const int nt = 4, Np = nt * NB;
@@ -55,15 +51,14 @@ int main() {
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
     if (v == 1) diag_v1<<<1, 256>>>(A, Np, N, 0, Dinv, res);
-    else if (v == 2) diag_v2<<<1, 512>>>(A, Np, N, 0, Dinv, res);
-    else diag_v3<<<1, 512>>>(A, Np, N, 0, Dinv, res);
+    else diag_v2<<<1, 512>>>(A, Np, N, 0, Dinv, res);
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(ms, e0, e1));
     CK(hipMemcpy(out.data(), A, out.size() * 8, hipMemcpyDeviceToHost));
     CK(hipMemcpy(dinv.data(), Dinv, dinv.size() * 8, hipMemcpyDeviceToHost));
     return 0;
   };
-  for (int v = 1; v <= 3; ++v) {
+  for (int v = 1; v <= 2; ++v) {
     for (int rep = 0; rep < 4; ++rep) {
       float ms;
       if (run(v, h, 1 << 30, &ms)) return 1;
