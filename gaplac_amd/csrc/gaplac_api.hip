@@ -77,11 +77,9 @@ struct gaplac_ctx {
     TailCtl* tctl = nullptr;     // its completion counters (zeroed per launch)
     uint32_t* ttasks = nullptr;  // its task list for ttasks_T tile columns
     size_t ttasks_elems = 0;
-    int ttasks_T = -1, ttasks_n = 0, ttasks_gw = 0;
+    int ttasks_T = -1, ttasks_n = 0;
     std::string ttrace_path;     // GAPLAC_TAIL_TRACE: append per-task times of every tail launch here
     int tail_fault = -1;         // GAPLAC_TAIL_FAULT (tests only): skip this tail column's diagonal block
-    int single_gw = 0;           // GAPLAC_SINGLE_GW: deep-task width of single-evaluation tails (0: by length)
-    int single_gw8_t = 1000;     // GAPLAC_SINGLE_GW8_T: tails of at least this many columns use width 8
     unsigned long long* ttrace = nullptr;
     size_t ttrace_elems = 0;
     gaplac_stats stats{};
@@ -454,14 +452,6 @@ static bool whole_in_tail(const gaplac_ctx* ctx, int nt) {
            nt <= ctx->tail_s;
 }
 
-// Deep-task width of a single evaluation's tail list: far tiles take GW tile columns per
-// task (K = 128 GW). GAPLAC_SINGLE_GW = 4 or 8 for every tail; 0 (default): 8 for tails of
-// at least single_gw8_t tile columns (throughput-bound early columns), 4 below.
-static int single_gw(const gaplac_ctx* ctx, int T) {
-    if (ctx->single_gw == 4 || ctx->single_gw == 8) return ctx->single_gw;
-    return T >= ctx->single_gw8_t ? 8 : 4;
-}
-
 static std::vector<int> superpanel_starts(const gaplac_ctx* ctx, int nt) {
     std::vector<int> sp{0};
     // a matrix the persistent tail covers whole (plain logpdf, at most TAIL_TMAX tile
@@ -624,18 +614,17 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             // the tail as one persistent dataflow launch
             if (ctx->dry) {  // gaplac_plan_check: the task list's dependency order
                 std::vector<uint32_t> host;
-                build_tail_tasks(T, host, nullptr, single_gw(ctx, T), 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP);
+                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP);
                 std::string why;
                 if (!check_tail_tasks(T, host, &why)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
             }
-            if ((ctx->ttasks_T != T || ctx->ttasks_gw != single_gw(ctx, T)) && !ctx->dry) {
+            if (ctx->ttasks_T != T && !ctx->dry) {
                 std::vector<uint32_t> host;
-                build_tail_tasks(T, host, nullptr, single_gw(ctx, T), 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP);
+                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP);
                 int rc;
                 if ((rc = ensure(ctx, &ctx->ttasks, &ctx->ttasks_elems, host.size()))) return rc;
                 HIPCK(ctx, hipMemcpy(ctx->ttasks, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
                 ctx->ttasks_T = T;
-                ctx->ttasks_gw = single_gw(ctx, T);
                 ctx->ttasks_n = (int)host.size();
             }
             if (!ctx->tctl && !ctx->dry)
@@ -1211,8 +1200,6 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_TAIL_S")) ctx->tail_s = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_TAIL_TRACE")) ctx->ttrace_path = s;  // diagnostics
     if (const char* s = std::getenv("GAPLAC_TAIL_FAULT")) ctx->tail_fault = std::atoi(s);  // tests: forced expiry
-    if (const char* s = std::getenv("GAPLAC_SINGLE_GW")) ctx->single_gw = std::atoi(s);
-    if (const char* s = std::getenv("GAPLAC_SINGLE_GW8_T")) ctx->single_gw8_t = std::max(1, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_BATCH_W")) ctx->batch_w = std::max(1, std::min(TAIL_MAX_MODELS, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BATCH_LAG")) ctx->batch_lag = std::max(0, std::atoi(s));
     auto fail = [&](const char* what, hipError_t e) {

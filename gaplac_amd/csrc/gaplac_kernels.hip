@@ -2541,24 +2541,14 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int
     }
 }
 
-#ifndef GAPLAC_EARLY_DEQ
-#define GAPLAC_EARLY_DEQ 1  // 0: dequeue at the top of the loop (round 3)
-#endif
 __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict__ kt) {
     __shared__ double smem[DIAG2_SMEM];
     __shared__ unsigned s_task;
     __shared__ unsigned s_rowf[NDB];
     kt_begin(kt);
-    // Dequeue: the next task's index is fetched while the current task's stores drain (the
-    // atomic is issued just before the publish step's vmcnt(0) wait, so its round trip hides
-    // behind the store acknowledgements), and the workgroup holds it for only that long. The
-    // order of dequeues, and with it the no-deadlock argument above, is unchanged: a task
-    // still waits only for tasks dequeued before it.
-    unsigned next_tk = 0;
-    if (GAPLAC_EARLY_DEQ && threadIdx.x == 0) next_tk = atomicAdd(&a.ctl->head, 1u);
     for (;;) {
         __syncthreads();
-        if (threadIdx.x == 0) s_task = GAPLAC_EARLY_DEQ ? next_tk : atomicAdd(&a.ctl->head, 1u);
+        if (threadIdx.x == 0) s_task = atomicAdd(&a.ctl->head, 1u);
         __syncthreads();
         const unsigned tk = s_task;
         if (tk >= (unsigned)a.ntasks) break;
@@ -2611,7 +2601,6 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
             }
         }
         // publish: every wave's stores complete, then one lane bumps the counter
-        if (GAPLAC_EARLY_DEQ && threadIdx.x == 0) next_tk = atomicAdd(&a.ctl->head, 1u);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0 && !faulted) {

@@ -37,8 +37,6 @@ SCHEDULES = {
     "spw3_serial8": {"GAPLAC_SPW": "3", "GAPLAC_TAIL_S": "8"},
     "spw1_no_tail": {"GAPLAC_SPW": "1", "GAPLAC_TAIL_S": "0"},
     "pair_all": {"GAPLAC_PAIR_M": "1"},
-    "tail_deep8": {"GAPLAC_SINGLE_GW": "8"},
-    "tail_deep8_by_len": {"GAPLAC_SINGLE_GW8_T": "20"},
     "pair_band_whole_tiles": {"GAPLAC_PAIR_M": "1", "GAPLAC_BAND_TILES_M": "1"},
     "no_pair": {"GAPLAC_PAIR_M": "0"},
     "pair_spw3_whole": {"GAPLAC_PAIR_M": "1", "GAPLAC_SPW": "3", "GAPLAC_BAND_TILES_M": "1"},
