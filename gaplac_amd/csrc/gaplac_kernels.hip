@@ -878,7 +878,10 @@ struct Gm {
 // ---------------------------------------------------------------------------------
 // LDS: the small buffers first (their addresses fit the 16-bit DS offset), then the block.
 constexpr int DIAG2_COLBUF = 16 * 64;  // colbuf[c * 64 + lane]: column c's record (diag2_sweep_a)
-constexpr int DIAG2_SMEM = DIAG2_COLBUF + NB + NPK * 256;  // colbuf, rdiag, Ab (doubles)
+constexpr int DIAG2_SMEM = DIAG2_COLBUF + NB + NPK * 256 + 8;  // colbuf, rdiag, Ab, v3's 16 flags (doubles)
+#ifndef GAPLAC_DIAG_FW
+#define GAPLAC_DIAG_FW 1  // diagonal block sweep: 1 = v3 (fill wave F beside the chain), 0 = v2
+#endif
 
 #define SB() __builtin_amdgcn_sched_barrier(0)
 #define PIN(x) asm volatile("" : "+v"(x))
@@ -1030,6 +1033,182 @@ __device__ __forceinline__ void diag2_sweep_b(double* Ab, double* colbuf, int s,
     }
 }
 
+
+// ---------------------------------------------------------------------------------
+// Diagonal block v3 sweep (GAPLAC_DIAG_FW = 1): the panel's fill updates move off the pivot
+// chain's wave. Measured on v2 (tools/diag_probe.hip): wave A's sweep is issue-bound at
+// ~290 cycles per column against a ~115-cycle dependent chain, because besides the chain it
+// applies every finished column to the panel's later columns (the fills, ~7.5 FMAs and ~7
+// LDS multiplier reads per column). Here a fill wave F holds the same 64 rows, applies
+// every finished column k to the columns j >= k + 4 and hands column k + 4 over to A
+// through LDS (colF, flag fflag[k + 4]); A keeps only the chain and the last three updates
+// of the next column (k-2, k-1, k), so its next column arrives with columns 0 .. c-3
+// applied. Each column still receives the finished columns in order 0, 1, 2, ... by the
+// same fused multiply-adds, so the factor is bitwise that of v2.
+// Records: A writes each finished column straight into the block column in Ab (lanes <= c
+// of the diagonal block as the final zeros / pivot) and rd_c into rdiag[16 s + c], which
+// doubles as the column's flag (rdiag starts at -1 for every column; rd is never -1).
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ bool lds_wait_ne(const double* p, double sentinel) {
+    for (int it = 0; it < (1 << 20); ++it) {
+        if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != sentinel) return true;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+
+__device__ __forceinline__ void diag3_sweep_a(double* Ab, const double* colF, const unsigned* fflag, double* rdiag,
+                                              int s, int lane, int64_t gcol0, int64_t N, EvalResult* res) {
+    asm volatile("" : "+v"(lane));
+    const int R0 = 16 * s;
+    const int row = R0 + lane;
+    const bool live = row < NB;
+    double* blk = Ab + bidx(live ? (row >> 4) : s, s) * 256;
+    const double* Ld = Ab + bidx(s, s) * 256;  // L(R0 + r, R0 + c) at Ld[c * 16 + r] once column c is recorded
+    const int rr = row & 15;
+    double v[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = blk[c * 16 + rr];  // columns 4 .. 15 come from F
+    const int64_t npiv64 = N - (gcol0 + R0);  // columns >= npiv are padding (unit pivots)
+    const int npiv = (int)(npiv64 < 0 ? 0 : (npiv64 > 16 ? 16 : npiv64));
+    const unsigned padmask = (0xffffu << npiv) & 0xffffu;
+    const bool padlane = lane < 16 && ((padmask >> lane) & 1u);
+    double k375 = 0.375;  // kept in a VGPR (not an inline constant)
+    PIN(k375);
+    double m1[17], m2[17];  // m1[c] = L(R0 + c + 1, c - 1), m2[c] = L(R0 + c + 1, c - 2): uniform
+#pragma unroll
+    for (int c = 0; c < 17; ++c) m1[c] = m2[c] = 0.0;
+    double mypiv = 1.0;
+    bool timeout = false;
+    double piv = readlane_d(v[0], 0);
+    SB();
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const bool pad = (padmask >> c) & 1u;
+        const double p = pad ? 1.0 : piv;
+        const double y = __builtin_amdgcn_rsq(p);
+        mypiv = lane == c ? v[c] : mypiv;  // the non-PD test runs after the sweep
+        // column c+1: from F (columns 0 .. c-3 applied) for c + 1 >= 4, then c-2 and c-1 here
+        if (c + 1 < 16) {
+            if (c + 1 >= 4) {
+                int it = 0;
+                while (__hip_atomic_load(&fflag[c + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+                    if (++it > (1 << 20)) {
+                        timeout = true;
+                        break;
+                    }
+                }
+                v[c + 1] = colF[(c + 1) * 64 + lane];
+            }
+            if (c >= 2) v[c + 1] = fma(-v[c - 2], m2[c], v[c + 1]);
+            if (c >= 1) v[c + 1] = fma(-v[c - 1], m1[c], v[c + 1]);
+        }
+        SB();
+        const double t = p * y;
+        const double e = fma(-t, y, 1.0);
+        const double cc = fma(e, k375, 0.5);
+        const double ye = y * e;
+        const double rd = fma(ye, cc, y);  // 1/sqrt(p), <= 1 ulp
+        // the diagonal lane's own value is its pivot, so it becomes p * rd = sqrt(p)
+        v[c] = v[c] * rd;
+        SB();
+        double ln = 0.0;
+        if (c + 1 < 16) ln = readlane_d(v[c], c + 1);
+        // the record: column c's final values into the block column, then rd (the flag)
+        if (live) blk[c * 16 + rr] = lane > c ? v[c] : (lane == c ? (padlane ? 1.0 : v[c]) : 0.0);
+        if (lane == 0) rdiag[R0 + c] = rd;
+        // this column's multipliers of the next two columns, read back from the record
+        if (c + 2 < 16) m1[c + 1] = Ld[c * 16 + c + 2];
+        if (c + 3 < 16) m2[c + 2] = Ld[c * 16 + c + 3];
+        SB();
+        if (c + 1 < 16) v[c + 1] = fma(-v[c], ln, v[c + 1]);
+        SB();
+        if (c + 1 < 16) piv = readlane_d(v[c + 1], c + 1);
+        SB();
+    }
+    // OpenBLAS potf2 (the reference's dpotrf, 0.3.20) tests ajj <= 0 only: a NaN pivot is
+    // not reported and propagates to a NaN logpdf, as in the reference
+    const unsigned long long badm = __ballot(lane < 16 && !((padmask >> lane) & 1u) && mypiv <= 0.0);
+    if (badm && lane == 0) atomicMin(&res->info, (unsigned long long)(gcol0 + R0 + __builtin_ctzll(badm) + 1));
+    if (timeout && lane == 0) atomicOr(&res->err, 1u);
+}
+
+// F: rows 16 s + lane (A's rows), columns 4 .. 15 of panel s. Record k is applied to every
+// column j >= k + 4, column k + 4 first; that column then has columns 0 .. k applied and
+// goes to A.
+__device__ __forceinline__ void diag3_sweep_f(const double* Ab, double* colF, unsigned* fflag, const double* rdiag,
+                                              int s, int lane, EvalResult* res) {
+    asm volatile("" : "+v"(lane));
+    const int R0 = 16 * s;
+    const int row = R0 + lane;
+    const bool live = row < NB;
+    const double* blk = Ab + bidx(live ? (row >> 4) : s, s) * 256;
+    const double* Ld = Ab + bidx(s, s) * 256;
+    const int rr = row & 15;
+    double v[16];
+#pragma unroll
+    for (int j = 4; j < 16; ++j) v[j] = blk[j * 16 + rr];
+    bool timeout = false;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        if (!lds_wait_ne(&rdiag[R0 + k], -1.0)) timeout = true;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the record after its flag
+        const double rec = blk[k * 16 + rr];  // L(row, R0 + k)
+        double m[16];
+#pragma unroll
+        for (int j = k + 4; j < 16; ++j) m[j] = Ld[k * 16 + j];
+        v[k + 4] = fma(-rec, m[k + 4], v[k + 4]);
+        colF[(k + 4) * 64 + lane] = v[k + 4];
+        if (lane == 0)
+            __hip_atomic_store(&fflag[k + 4], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+        for (int j = k + 5; j < 16; ++j) v[j] = fma(-rec, m[j], v[j]);
+    }
+    if (timeout && lane == 0) atomicOr(&res->err, 1u);
+}
+
+// B (rows 16 s + 64 + lane, s < 4) in v3: diag2_sweep_b's arithmetic with the flag in
+// rdiag and the multipliers read from A's records in the diagonal block.
+__device__ __forceinline__ void diag3_sweep_b(double* Ab, const double* rdiag, int s, int lane, EvalResult* res) {
+    asm volatile("" : "+v"(lane));
+    const int row = 16 * s + 64 + lane;
+    const bool live = row < NB;
+    double* blk = Ab + bidx(live ? (row >> 4) : NDB - 1, s) * 256;
+    const double* Ld = Ab + bidx(s, s) * 256;
+    const int rr = row & 15;
+    double v[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v[c] = blk[c * 16 + rr];
+    bool timeout = false;
+    double fl = __hip_atomic_load(&rdiag[16 * s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        for (int it = 0; fl == -1.0 && it < (1 << 20); ++it) {
+            __builtin_amdgcn_s_sleep(1);
+            fl = __hip_atomic_load(&rdiag[16 * s + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (fl == -1.0) {
+            timeout = true;
+            fl = __builtin_nan("");
+        }
+        const double rd = fl;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the record's values after its flag
+        double lc[16];
+#pragma unroll
+        for (int c2 = c + 1; c2 < 16; ++c2) lc[c2] = Ld[c * 16 + c2];
+        if (c + 1 < 16) fl = __hip_atomic_load(&rdiag[16 * s + c + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const double l = v[c] * rd;
+        v[c] = l;
+#pragma unroll
+        for (int c2 = c + 1; c2 < 16; ++c2) v[c2] = fma(-l, lc[c2], v[c2]);
+    }
+    if (timeout && lane == 0) atomicOr(&res->err, 1u);
+    if (live) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) blk[c * 16 + rr] = v[c];
+    }
+}
+
 // Dinv_s = L_ss^{-1} (column-major 16x16 into global): lane j < 16 solves L x = e_j
 // right-looking (x[m] final, then every later row updated with it).
 template <int AUX>
@@ -1114,13 +1293,14 @@ __device__ __forceinline__ void diag2_store_column(const double* Ab, double* Ag,
 // 512 threads: wave 0 = A (the pivot chain), wave 1 = B (rows 64+ of panels 0-3), waves 2-7
 // the trailing updates, the stores of finished block columns and (wave 7) the inverses.
 // Waves w and w + 4 share a SIMD, so every SIMD's matrix pipe takes trailing work.
-template <int AUX>
+template <int AUX, int FW = GAPLAC_DIAG_FW>
 __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restrict__ Ag, int64_t lda, int64_t N,
                                                  int64_t g0, double* __restrict__ Dinv, EvalResult* __restrict__ res,
                                                  double* Dl = nullptr, unsigned* prog = nullptr) {
-    double* colbuf = smem;
+    double* colbuf = smem;  // v2: the column records; v3: F's hand-over columns (colF)
     double* rdiag = colbuf + DIAG2_COLBUF;
     double* Ab = rdiag + NB;
+    unsigned* fflag = reinterpret_cast<unsigned*>(Ab + NPK * 256);  // v3: column j handed over by F
     const int t = otid(), wave = t >> 6, lane = t & 63;
     // the chain first (wave-uniform branches: s_setprio takes an immediate)
     if (wave == 0) __builtin_amdgcn_s_setprio(3);
@@ -1160,7 +1340,15 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
             }
         }
     }
-    if (wave == 3 && lane < 16) colbuf[lane * 64 + lane] = -1.0;  // the records' flags
+    if (FW) {
+        if (wave == 3) {  // every column's flag (rdiag) and F's hand-over flags
+            rdiag[lane] = -1.0;
+            rdiag[64 + lane] = -1.0;
+            if (lane < 16) fflag[lane] = 0u;
+        }
+    } else if (wave == 3 && lane < 16) {
+        colbuf[lane * 64 + lane] = -1.0;  // the records' flags
+    }
     // a barrier that does not wait for the other blocks' loads (__syncthreads would)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1169,7 +1357,9 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
         if (s >= 1) {
             // phase 1: panel s-1 into block column s (the diagonal block first, on wave 0)
             for (int I = s + wave; I < NDB; I += 8) dblk_update(Ab, I, s, s - 1, lane);
-            if (wave == 3 && lane < 16) {
+            if (FW) {
+                if (wave == 3 && lane < 16) fflag[lane] = 0u;  // F's hand-over flags of panel s
+            } else if (wave == 3 && lane < 16) {
                 rdiag[16 * (s - 1) + lane] = colbuf[lane * 64 + lane];  // rd of panel s-1's columns
                 colbuf[lane * 64 + lane] = -1.0;                        // the records' flags
             }
@@ -1183,9 +1373,28 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
         if (prog && s >= 2 && wave == 3 && lane == 0)  // columns and inverses 0 .. s-2 final
             __hip_atomic_store(prog, (unsigned)(s - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (wave == 0) {
-            diag2_sweep_a(Ab, colbuf, s, lane, g0, N, res);
+            if (FW)
+                diag3_sweep_a(Ab, colbuf, fflag, rdiag, s, lane, g0, N, res);
+            else
+                diag2_sweep_a(Ab, colbuf, s, lane, g0, N, res);
         } else if (wave == 1 && s < 4) {
-            diag2_sweep_b(Ab, colbuf, s, lane, res);
+            if (FW)
+                diag3_sweep_b(Ab, rdiag, s, lane, res);
+            else
+                diag2_sweep_b(Ab, colbuf, s, lane, res);
+        } else if (FW && wave == 7) {
+            diag3_sweep_f(Ab, colbuf, fflag, rdiag, s, lane, res);
+            if (s == 0) {  // wave 7's share of the rest of the block
+#pragma unroll
+                for (int i = 0; i < 10; ++i) {
+                    const int q = tt + 384 * i;
+                    if (q < 28 * 128) {
+                        int I, J;
+                        diag2_block_of(q >> 7, I, J);
+                        *reinterpret_cast<double2*>(&Ab[bidx(I, J) * 256 + 2 * (q & 127)]) = rest[i];
+                    }
+                }
+            }
         } else {
             if (s == 0 && wave >= 2) {  // the rest of the block into LDS
 #pragma unroll
@@ -1201,9 +1410,13 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
             if (s >= 1) {
                 // wave 4 shares wave A's SIMD: it only stores and inverts (light), the
                 // trailing blocks go to waves 2, 3, 5, 6, 7 (and 1 from panel 4 on)
-                if (wave >= 2) diag2_store_column<AUX>(Ab, Ag, lda, s - 1, t - 128, 384);
+                if (wave >= 2) diag2_store_column<AUX>(Ab, Ag, lda, s - 1, t - 128, FW ? 320 : 384);
+                STAMPT(128, 40 + s);  // wave 2: after its share of the stores
                 if (wave == 4) {
                     diag2_dinv<AUX>(Ab, Dinv, rdiag, s - 1, lane, Dl);
+                } else if (FW) {  // waves 2, 3, 5, 6 (and 1 from panel 4 on)
+                    const int w = wave == 1 ? 0 : (s < 4 ? 0 : 1) + (wave < 4 ? wave - 2 : wave - 3);
+                    diag2_trailing(Ab, s, w, s < 4 ? 4 : 5, lane);
                 } else {
                     const int w = wave == 1 ? 0 : (s < 4 ? 0 : 1) + (wave < 4 ? wave - 2 : wave - 3);
                     diag2_trailing(Ab, s, w, s < 4 ? 5 : 6, lane);
@@ -1213,9 +1426,14 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
         if (wave == 0) STAMP(2 + 2 * s);
         STAMPT(64, 29 + s);
         STAMPT(128, 21 + s);
+        STAMPT(192, 48 + s);
+        STAMPT(256, 80 + s);
+        STAMPT(320, 56 + s);
+        STAMPT(384, 64 + s);
+        STAMPT(448, 72 + s);
         __syncthreads();
     }
-    if (wave == 3 && lane < 16) rdiag[16 * (NDB - 1) + lane] = colbuf[lane * 64 + lane];
+    if (!FW && wave == 3 && lane < 16) rdiag[16 * (NDB - 1) + lane] = colbuf[lane * 64 + lane];
     if (prog && wave >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (prog && wave == 3 && lane == 0)  // columns and inverses 0 .. 6 final
