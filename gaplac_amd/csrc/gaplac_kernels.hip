@@ -1081,6 +1081,11 @@ __device__ __forceinline__ void diag3_sweep_a(double* Ab, const double* colF, co
     double mypiv = 1.0;
     bool timeout = false;
     double piv = readlane_d(v[0], 0);
+    // F's column c + 2 and its flag are read one iteration ahead (issued together: the flag
+    // read executes first in this wave's LDS order, so when it shows the flag set the column
+    // read after it returns the handed-over values; otherwise both are read again)
+    unsigned fnext = 0u;
+    double cnext = 0.0;
     SB();
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
@@ -1091,14 +1096,31 @@ __device__ __forceinline__ void diag3_sweep_a(double* Ab, const double* colF, co
         // column c+1: from F (columns 0 .. c-3 applied) for c + 1 >= 4, then c-2 and c-1 here
         if (c + 1 < 16) {
             if (c + 1 >= 4) {
-                int it = 0;
-                while (__hip_atomic_load(&fflag[c + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
-                    if (++it > (1 << 20)) {
-                        timeout = true;
-                        break;
+                if (c + 1 > 4) {
+                    int it = 0;
+                    while (fnext == 0u && it < (1 << 20)) {
+                        ++it;
+                        fnext = __hip_atomic_load(&fflag[c + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        asm volatile("" ::: "memory");  // the column read stays after the flag read
+                        cnext = colF[(c + 1) * 64 + lane];
                     }
+                    if (fnext == 0u) timeout = true;
+                    v[c + 1] = cnext;
+                } else {
+                    int it = 0;
+                    while (__hip_atomic_load(&fflag[c + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+                        if (++it > (1 << 20)) {
+                            timeout = true;
+                            break;
+                        }
+                    }
+                    v[c + 1] = colF[(c + 1) * 64 + lane];
                 }
-                v[c + 1] = colF[(c + 1) * 64 + lane];
+            }
+            if (c + 2 < 16 && c + 2 > 4) {  // next iteration's column, speculatively
+                fnext = __hip_atomic_load(&fflag[c + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                asm volatile("" ::: "memory");  // the column read stays after the flag read
+                cnext = colF[(c + 2) * 64 + lane];
             }
             if (c >= 2) v[c + 1] = fma(-v[c - 2], m2[c], v[c + 1]);
             if (c >= 1) v[c + 1] = fma(-v[c - 1], m1[c], v[c + 1]);
@@ -1149,20 +1171,34 @@ __device__ __forceinline__ void diag3_sweep_f(const double* Ab, double* colF, un
 #pragma unroll
     for (int j = 4; j < 16; ++j) v[j] = blk[j * 16 + rr];
     bool timeout = false;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        if (!lds_wait_ne(&rdiag[R0 + k], -1.0)) timeout = true;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the record after its flag
-        const double rec = blk[k * 16 + rr];  // L(row, R0 + k)
-        double m[16];
+    // record k's flag, row value and multipliers are read together (the flag first in this
+    // wave's LDS order: when it shows rd, the reads after it see the record A wrote before
+    // it), the next record's right after column k + 4 is handed over, so their latency runs
+    // beside the rest of record k's updates
+    double fl = 0.0, rec = 0.0, m[16];
+    auto issue = [&](int k) {
+        fl = __hip_atomic_load(&rdiag[R0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        asm volatile("" ::: "memory");  // the record reads stay after the flag read
+        rec = blk[k * 16 + rr];  // L(row, R0 + k)
 #pragma unroll
         for (int j = k + 4; j < 16; ++j) m[j] = Ld[k * 16 + j];
-        v[k + 4] = fma(-rec, m[k + 4], v[k + 4]);
-        colF[(k + 4) * 64 + lane] = v[k + 4];
-        if (lane == 0)
-            __hip_atomic_store(&fflag[k + 4], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    issue(0);
 #pragma unroll
-        for (int j = k + 5; j < 16; ++j) v[j] = fma(-rec, m[j], v[j]);
+    for (int k = 0; k < 12; ++k) {
+        for (int it = 0; fl == -1.0 && it < (1 << 22); ++it) issue(k);
+        if (fl == -1.0) timeout = true;
+        const double rk = rec;
+        double mk[16];
+#pragma unroll
+        for (int j = k + 4; j < 16; ++j) mk[j] = m[j];
+        v[k + 4] = fma(-rk, mk[k + 4], v[k + 4]);
+        colF[(k + 4) * 64 + lane] = v[k + 4];
+        asm volatile("" ::: "memory");
+        if (lane == 0) fflag[k + 4] = 1u;  // after the column in this wave's LDS order
+        if (k + 1 < 12) issue(k + 1);
+#pragma unroll
+        for (int j = k + 5; j < 16; ++j) v[j] = fma(-rk, mk[j], v[j]);
     }
     if (timeout && lane == 0) atomicOr(&res->err, 1u);
 }
