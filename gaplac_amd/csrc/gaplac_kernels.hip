@@ -1184,6 +1184,7 @@ __device__ __forceinline__ void diag3_sweep_f(const double* Ab, double* colF, un
         for (int j = k + 4; j < 16; ++j) m[j] = Ld[k * 16 + j];
     };
     issue(0);
+    SB();
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
         for (int it = 0; fl == -1.0 && it < (1 << 22); ++it) issue(k);
@@ -1192,13 +1193,20 @@ __device__ __forceinline__ void diag3_sweep_f(const double* Ab, double* colF, un
         double mk[16];
 #pragma unroll
         for (int j = k + 4; j < 16; ++j) mk[j] = m[j];
+        // column k + 4 first: it has every earlier record applied (pinned in place below)
         v[k + 4] = fma(-rk, mk[k + 4], v[k + 4]);
         colF[(k + 4) * 64 + lane] = v[k + 4];
         asm volatile("" ::: "memory");
         if (lane == 0) fflag[k + 4] = 1u;  // after the column in this wave's LDS order
-        if (k + 1 < 12) issue(k + 1);
+        SB();
+        if (k + 1 < 12) issue(k + 1);  // next record's reads in flight under this record's updates
+        SB();
 #pragma unroll
-        for (int j = k + 5; j < 16; ++j) v[j] = fma(-rk, mk[j], v[j]);
+        for (int j = k + 5; j < 16; ++j) {
+            v[j] = fma(-rk, mk[j], v[j]);
+            PIN(v[j]);  // applied now, not sunk into the hand-over of column j
+        }
+        SB();
     }
     if (timeout && lane == 0) atomicOr(&res->err, 1u);
 }
