@@ -1064,7 +1064,7 @@ __device__ __forceinline__ void diag3_sweep_a(double* Ab, const double* colF, co
     const int row = R0 + lane;
     const bool live = row < NB;
     double* blk = Ab + bidx(live ? (row >> 4) : s, s) * 256;
-    const double* Ld = Ab + bidx(s, s) * 256;  // L(R0 + r, R0 + c) at Ld[c * 16 + r] once column c is recorded
+    double* wblk = live ? blk : const_cast<double*>(colF);  // record target (colF[0, 256) is unused)
     const int rr = row & 15;
     double v[16];
 #pragma unroll
@@ -1080,73 +1080,85 @@ __device__ __forceinline__ void diag3_sweep_a(double* Ab, const double* colF, co
     for (int c = 0; c < 17; ++c) m1[c] = m2[c] = 0.0;
     double mypiv = 1.0;
     bool timeout = false;
+    // F's column j and its flag are read two iterations ahead, together (the flag read
+    // executes first in this wave's LDS order, so when it shows the flag set the column read
+    // after it returns the handed-over values; otherwise both are read again)
+    unsigned fl[16];
+    double cf[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        fl[j] = 1u;
+        cf[j] = 0.0;
+    }
+    auto fetch = [&](int j) {
+        fl[j] = __hip_atomic_load(&fflag[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        asm volatile("" ::: "memory");  // the column read stays after the flag read
+        cf[j] = colF[j * 64 + lane];
+    };
+    fetch(4);
     double piv = readlane_d(v[0], 0);
-    // F's column c + 2 and its flag are read one iteration ahead (issued together: the flag
-    // read executes first in this wave's LDS order, so when it shows the flag set the column
-    // read after it returns the handed-over values; otherwise both are read again)
-    unsigned fnext = 0u;
-    double cnext = 0.0;
+    double p = ((padmask & 1u) != 0u) ? 1.0 : piv;
+    double y = __builtin_amdgcn_rsq(p);
     SB();
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
-        const bool pad = (padmask >> c) & 1u;
-        const double p = pad ? 1.0 : piv;
-        const double y = __builtin_amdgcn_rsq(p);
         mypiv = lane == c ? v[c] : mypiv;  // the non-PD test runs after the sweep
-        // column c+1: from F (columns 0 .. c-3 applied) for c + 1 >= 4, then c-2 and c-1 here
-        if (c + 1 < 16) {
-            if (c + 1 >= 4) {
-                if (c + 1 > 4) {
-                    int it = 0;
-                    while (fnext == 0u && it < (1 << 20)) {
-                        ++it;
-                        fnext = __hip_atomic_load(&fflag[c + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        asm volatile("" ::: "memory");  // the column read stays after the flag read
-                        cnext = colF[(c + 1) * 64 + lane];
-                    }
-                    if (fnext == 0u) timeout = true;
-                    v[c + 1] = cnext;
-                } else {
-                    int it = 0;
-                    while (__hip_atomic_load(&fflag[c + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
-                        if (++it > (1 << 20)) {
-                            timeout = true;
-                            break;
-                        }
-                    }
-                    v[c + 1] = colF[(c + 1) * 64 + lane];
-                }
-            }
-            if (c + 2 < 16 && c + 2 > 4) {  // next iteration's column, speculatively
-                fnext = __hip_atomic_load(&fflag[c + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                asm volatile("" ::: "memory");  // the column read stays after the flag read
-                cnext = colF[(c + 2) * 64 + lane];
-            }
-            if (c >= 2) v[c + 1] = fma(-v[c - 2], m2[c], v[c + 1]);
-            if (c >= 1) v[c + 1] = fma(-v[c - 1], m1[c], v[c + 1]);
-        }
-        SB();
         const double t = p * y;
+        SB();
         const double e = fma(-t, y, 1.0);
+        SB();
+        // column c+1 gets columns c-2 and c-1 in the chain's shadow (F applied 0 .. c-3;
+        // columns 1 .. 3 come raw from the block); placed here, ~2 dependent steps after
+        // the previous iteration's last LDS operations, which their wait covers
+        if (c + 1 < 16) {
+            if (c + 1 >= 4) v[c + 1] = cf[c + 1];
+            if (c >= 2) {
+                v[c + 1] = fma(-v[c - 2], m2[c], v[c + 1]);
+                PIN(v[c + 1]);
+            }
+            if (c >= 1) {
+                v[c + 1] = fma(-v[c - 1], m1[c], v[c + 1]);
+                PIN(v[c + 1]);
+            }
+        }
         const double cc = fma(e, k375, 0.5);
         const double ye = y * e;
+        SB();
         const double rd = fma(ye, cc, y);  // 1/sqrt(p), <= 1 ulp
+        SB();
         // the diagonal lane's own value is its pivot, so it becomes p * rd = sqrt(p)
         v[c] = v[c] * rd;
         SB();
         double ln = 0.0;
         if (c + 1 < 16) ln = readlane_d(v[c], c + 1);
-        // the record: column c's final values into the block column, then rd (the flag)
-        if (live) blk[c * 16 + rr] = lane > c ? v[c] : (lane == c ? (padlane ? 1.0 : v[c]) : 0.0);
-        if (lane == 0) rdiag[R0 + c] = rd;
-        // this column's multipliers of the next two columns, read back from the record
-        if (c + 2 < 16) m1[c + 1] = Ld[c * 16 + c + 2];
-        if (c + 3 < 16) m2[c + 2] = Ld[c * 16 + c + 3];
         SB();
         if (c + 1 < 16) v[c + 1] = fma(-v[c], ln, v[c + 1]);
+        // this column's multipliers of the next two columns (off the chain)
+        if (c + 2 < 16) m1[c + 1] = readlane_d(v[c], c + 2);
+        if (c + 3 < 16) m2[c + 2] = readlane_d(v[c], c + 3);
         SB();
         if (c + 1 < 16) piv = readlane_d(v[c + 1], c + 1);
+        // the record: column c's final values into the block column, then rd (the flag);
+        // F's column c + 3 requested
+        // (unmasked stores: the compiler keeps exact LDS counts and waits only for what is
+        // used; lanes past the last row write to colF's unused first four columns)
+        wblk[c * 16 + rr] = lane > c ? v[c] : (lane == c ? (padlane ? 1.0 : v[c]) : 0.0);
+        rdiag[R0 + c] = rd;  // every lane, the same value
+        if (c + 3 < 16 && c + 3 >= 5) fetch(c + 3);
         SB();
+        if (c + 1 < 16) {  // the next pivot's rsq, issued before the hand-over check
+            p = ((padmask >> (c + 1)) & 1u) ? 1.0 : piv;
+            y = __builtin_amdgcn_rsq(p);
+        }
+        SB();
+        if (c + 2 < 16 && c + 2 >= 4) {  // F's column c + 2 (fetched an iteration ago) is final
+            int it = 0;
+            while (fl[c + 2] == 0u && it < (1 << 20)) {
+                ++it;
+                fetch(c + 2);
+            }
+            if (fl[c + 2] == 0u) timeout = true;
+        }
     }
     // OpenBLAS potf2 (the reference's dpotrf, 0.3.20) tests ajj <= 0 only: a NaN pivot is
     // not reported and propagates to a NaN logpdf, as in the reference
