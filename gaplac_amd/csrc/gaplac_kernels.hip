@@ -1103,15 +1103,24 @@ __device__ __forceinline__ void diag3_sweep_a(double* Ab, const double* colF, co
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         mypiv = lane == c ? v[c] : mypiv;  // the non-PD test runs after the sweep
-        const double t = p * y;
+        double t = p * y;
+        PIN(t);  // (the pins keep the chain's steps above the hand-over check's branch)
         SB();
-        const double e = fma(-t, y, 1.0);
+        double e = fma(-t, y, 1.0);
+        PIN(e);
         SB();
-        // column c+1 gets columns c-2 and c-1 in the chain's shadow (F applied 0 .. c-3;
-        // columns 1 .. 3 come raw from the block); placed here, ~2 dependent steps after
-        // the previous iteration's last LDS operations, which their wait covers
+        // column c+1 (F's, fetched two iterations ago; columns 1 .. 3 raw from the block)
+        // gets columns c-2 and c-1 in the chain's shadow
         if (c + 1 < 16) {
-            if (c + 1 >= 4) v[c + 1] = cf[c + 1];
+            if (c + 1 >= 4) {
+                int it = 0;
+                while (fl[c + 1] == 0u && it < (1 << 20)) {
+                    ++it;
+                    fetch(c + 1);
+                }
+                if (fl[c + 1] == 0u) timeout = true;
+                v[c + 1] = cf[c + 1];
+            }
             if (c >= 2) {
                 v[c + 1] = fma(-v[c - 2], m2[c], v[c + 1]);
                 PIN(v[c + 1]);
@@ -1129,36 +1138,29 @@ __device__ __forceinline__ void diag3_sweep_a(double* Ab, const double* colF, co
         // the diagonal lane's own value is its pivot, so it becomes p * rd = sqrt(p)
         v[c] = v[c] * rd;
         SB();
+        // the record (column c's final values into the block column, then rd: the flag) and
+        // F's column c + 3, early: the next LDS wait (above) then finds them done. Unmasked
+        // stores keep the compiler's LDS counts exact; lanes past the last row write to
+        // colF's unused first four columns
+        wblk[c * 16 + rr] = lane > c ? v[c] : (lane == c ? (padlane ? 1.0 : v[c]) : 0.0);
+        rdiag[R0 + c] = rd;  // every lane, the same value
+        if (c + 3 < 16 && c + 3 >= 5) fetch(c + 3);
         double ln = 0.0;
         if (c + 1 < 16) ln = readlane_d(v[c], c + 1);
         SB();
         if (c + 1 < 16) v[c + 1] = fma(-v[c], ln, v[c + 1]);
+        SB();
+        if (c + 1 < 16) {
+            piv = readlane_d(v[c + 1], c + 1);
+            p = ((padmask >> (c + 1)) & 1u) ? 1.0 : piv;
+            y = __builtin_amdgcn_rsq(p);  // the next pivot's
+            PIN(y);
+        }
+        SB();
         // this column's multipliers of the next two columns (off the chain)
         if (c + 2 < 16) m1[c + 1] = readlane_d(v[c], c + 2);
         if (c + 3 < 16) m2[c + 2] = readlane_d(v[c], c + 3);
         SB();
-        if (c + 1 < 16) piv = readlane_d(v[c + 1], c + 1);
-        // the record: column c's final values into the block column, then rd (the flag);
-        // F's column c + 3 requested
-        // (unmasked stores: the compiler keeps exact LDS counts and waits only for what is
-        // used; lanes past the last row write to colF's unused first four columns)
-        wblk[c * 16 + rr] = lane > c ? v[c] : (lane == c ? (padlane ? 1.0 : v[c]) : 0.0);
-        rdiag[R0 + c] = rd;  // every lane, the same value
-        if (c + 3 < 16 && c + 3 >= 5) fetch(c + 3);
-        SB();
-        if (c + 1 < 16) {  // the next pivot's rsq, issued before the hand-over check
-            p = ((padmask >> (c + 1)) & 1u) ? 1.0 : piv;
-            y = __builtin_amdgcn_rsq(p);
-        }
-        SB();
-        if (c + 2 < 16 && c + 2 >= 4) {  // F's column c + 2 (fetched an iteration ago) is final
-            int it = 0;
-            while (fl[c + 2] == 0u && it < (1 << 20)) {
-                ++it;
-                fetch(c + 2);
-            }
-            if (fl[c + 2] == 0u) timeout = true;
-        }
     }
     // OpenBLAS potf2 (the reference's dpotrf, 0.3.20) tests ajj <= 0 only: a NaN pivot is
     // not reported and propagates to a NaN logpdf, as in the reference
