@@ -1065,6 +1065,7 @@ __device__ __forceinline__ void diag3_sweep_a(double* Ab, const double* colF, co
     const bool live = row < NB;
     double* blk = Ab + bidx(live ? (row >> 4) : s, s) * 256;
     double* wblk = live ? blk : const_cast<double*>(colF);  // record target (colF[0, 256) is unused)
+    const double* Ld = Ab + bidx(s, s) * 256;  // L(R0 + r, R0 + c) at Ld[c * 16 + r] once column c is recorded
     const int rr = row & 15;
     double v[16];
 #pragma unroll
@@ -1102,6 +1103,9 @@ __device__ __forceinline__ void diag3_sweep_a(double* Ab, const double* colF, co
     SB();
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
+#ifdef GAPLAC_STAMPS
+        if (s == 5) STAMP(90 + c);
+#endif
         mypiv = lane == c ? v[c] : mypiv;  // the non-PD test runs after the sweep
         double t = p * y;
         PIN(t);  // (the pins keep the chain's steps above the hand-over check's branch)
@@ -1157,9 +1161,10 @@ __device__ __forceinline__ void diag3_sweep_a(double* Ab, const double* colF, co
             PIN(y);
         }
         SB();
-        // this column's multipliers of the next two columns (off the chain)
-        if (c + 2 < 16) m1[c + 1] = readlane_d(v[c], c + 2);
-        if (c + 3 < 16) m2[c + 2] = readlane_d(v[c], c + 3);
+        // this column's multipliers of the next two columns, read back from the record
+        // (LDS broadcast reads: a v_readlane pair costs ~16 issue cycles)
+        if (c + 2 < 16) m1[c + 1] = Ld[c * 16 + c + 2];
+        if (c + 3 < 16) m2[c + 2] = Ld[c * 16 + c + 3];
         SB();
     }
     // OpenBLAS potf2 (the reference's dpotrf, 0.3.20) tests ajj <= 0 only: a NaN pivot is
@@ -1351,7 +1356,10 @@ __device__ __forceinline__ void diag2_store_column(const double* Ab, double* Ag,
 // 512 threads: wave 0 = A (the pivot chain), wave 1 = B (rows 64+ of panels 0-3), waves 2-7
 // the trailing updates, the stores of finished block columns and (wave 7) the inverses.
 // Waves w and w + 4 share a SIMD, so every SIMD's matrix pipe takes trailing work.
-template <int AUX, int FW = GAPLAC_DIAG_FW>
+#ifndef GAPLAC_DINV_WAVE
+#define GAPLAC_DINV_WAVE 6  // the diagonal kernel's inverse wave: 6 (SIMD 2); 4 shares wave A's SIMD
+#endif
+template <int AUX, int FW = GAPLAC_DIAG_FW, int DINV_WAVE = GAPLAC_DINV_WAVE>
 __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restrict__ Ag, int64_t lda, int64_t N,
                                                  int64_t g0, double* __restrict__ Dinv, EvalResult* __restrict__ res,
                                                  double* Dl = nullptr, unsigned* prog = nullptr) {
@@ -1466,18 +1474,20 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
                 }
             }
             if (s >= 1) {
-                // wave 4 shares wave A's SIMD: it only stores and inverts (light), the
-                // trailing blocks go to waves 2, 3, 5, 6, 7 (and 1 from panel 4 on)
+                // the inverse's wave (VALU work) sits off wave A's SIMD (waves w and w + 4 share
+                // one: round 3 had it on wave 4, beside A); the trailing blocks (MFMA) go to the
+                // other waves 2 .. 7 but F
                 if (wave >= 2) diag2_store_column<AUX>(Ab, Ag, lda, s - 1, t - 128, FW ? 320 : 384);
                 STAMPT(128, 40 + s);  // wave 2: after its share of the stores
-                if (wave == 4) {
+                if (wave == DINV_WAVE) {
                     diag2_dinv<AUX>(Ab, Dinv, rdiag, s - 1, lane, Dl);
-                } else if (FW) {  // waves 2, 3, 5, 6 (and 1 from panel 4 on)
-                    const int w = wave == 1 ? 0 : (s < 4 ? 0 : 1) + (wave < 4 ? wave - 2 : wave - 3);
-                    diag2_trailing(Ab, s, w, s < 4 ? 4 : 5, lane);
                 } else {
-                    const int w = wave == 1 ? 0 : (s < 4 ? 0 : 1) + (wave < 4 ? wave - 2 : wave - 3);
-                    diag2_trailing(Ab, s, w, s < 4 ? 5 : 6, lane);
+                    // trailing waves: 2 .. 7 without the inverse's wave (and F's, wave 7, in v3),
+                    // numbered 0 ..; wave 1 joins from panel 4 on
+                    const int wi = wave - 2 - (wave > DINV_WAVE ? 1 : 0);
+                    const int nw = FW ? 4 : 5;
+                    const int w = wave == 1 ? 0 : (s < 4 ? 0 : 1) + wi;
+                    diag2_trailing(Ab, s, w, s < 4 ? nw : nw + 1, lane);
                 }
             }
         }
@@ -1497,9 +1507,9 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
     if (prog && wave == 3 && lane == 0)  // columns and inverses 0 .. 6 final
         __hip_atomic_store(prog, (unsigned)(NDB - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     STAMP(17);
-    if (wave == 4) diag2_dinv<AUX>(Ab, Dinv, rdiag, NDB - 1, lane, Dl);
+    if (wave == DINV_WAVE) diag2_dinv<AUX>(Ab, Dinv, rdiag, NDB - 1, lane, Dl);
     STAMP(18);
-    if (wave != 4) diag2_store_column<AUX>(Ab, Ag, lda, NDB - 1, wave < 4 ? t : t - 64, 448);
+    if (wave != DINV_WAVE) diag2_store_column<AUX>(Ab, Ag, lda, NDB - 1, wave < DINV_WAVE ? t : t - 64, 448);
     STAMP(19);
 }
 #undef SB
