@@ -878,10 +878,7 @@ struct Gm {
 // ---------------------------------------------------------------------------------
 // LDS: the small buffers first (their addresses fit the 16-bit DS offset), then the block.
 constexpr int DIAG2_COLBUF = 16 * 64;  // colbuf[c * 64 + lane]: column c's record (diag2_sweep_a)
-constexpr int DIAG2_SMEM = DIAG2_COLBUF + NB + NPK * 256 + 8;  // colbuf, rdiag, Ab, v3's 16 flags (doubles)
-#ifndef GAPLAC_DIAG_FW
-#define GAPLAC_DIAG_FW 1  // diagonal block sweep: 1 = v3 (fill wave F beside the chain), 0 = v2
-#endif
+constexpr int DIAG2_SMEM = DIAG2_COLBUF + NB + NPK * 256;  // colbuf, rdiag, Ab (doubles)
 
 #define SB() __builtin_amdgcn_sched_barrier(0)
 #define PIN(x) asm volatile("" : "+v"(x))
@@ -1033,245 +1030,6 @@ __device__ __forceinline__ void diag2_sweep_b(double* Ab, double* colbuf, int s,
     }
 }
 
-
-// ---------------------------------------------------------------------------------
-// Diagonal block v3 sweep (GAPLAC_DIAG_FW = 1): the panel's fill updates move off the pivot
-// chain's wave. Measured on v2 (tools/diag_probe.hip): wave A's sweep is issue-bound at
-// ~290 cycles per column against a ~115-cycle dependent chain, because besides the chain it
-// applies every finished column to the panel's later columns (the fills, ~7.5 FMAs and ~7
-// LDS multiplier reads per column). Here a fill wave F holds the same 64 rows, applies
-// every finished column k to the columns j >= k + 4 and hands column k + 4 over to A
-// through LDS (colF, flag fflag[k + 4]); A keeps only the chain and the last three updates
-// of the next column (k-2, k-1, k), so its next column arrives with columns 0 .. c-3
-// applied. Each column still receives the finished columns in order 0, 1, 2, ... by the
-// same fused multiply-adds, so the factor is bitwise that of v2.
-// Records: A writes each finished column straight into the block column in Ab (lanes <= c
-// of the diagonal block as the final zeros / pivot) and rd_c into rdiag[16 s + c], which
-// doubles as the column's flag (rdiag starts at -1 for every column; rd is never -1).
-// ---------------------------------------------------------------------------------
-__device__ __forceinline__ bool lds_wait_ne(const double* p, double sentinel) {
-    for (int it = 0; it < (1 << 20); ++it) {
-        if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != sentinel) return true;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return false;
-}
-
-__device__ __forceinline__ void diag3_sweep_a(double* Ab, const double* colF, const unsigned* fflag, double* rdiag,
-                                              int s, int lane, int64_t gcol0, int64_t N, EvalResult* res) {
-    asm volatile("" : "+v"(lane));
-    const int R0 = 16 * s;
-    const int row = R0 + lane;
-    const bool live = row < NB;
-    double* blk = Ab + bidx(live ? (row >> 4) : s, s) * 256;
-    double* wblk = live ? blk : const_cast<double*>(colF);  // record target (colF[0, 256) is unused)
-    const double* Ld = Ab + bidx(s, s) * 256;  // L(R0 + r, R0 + c) at Ld[c * 16 + r] once column c is recorded
-    const int rr = row & 15;
-    double v[16];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] = blk[c * 16 + rr];  // columns 4 .. 15 come from F
-    const int64_t npiv64 = N - (gcol0 + R0);  // columns >= npiv are padding (unit pivots)
-    const int npiv = (int)(npiv64 < 0 ? 0 : (npiv64 > 16 ? 16 : npiv64));
-    const unsigned padmask = (0xffffu << npiv) & 0xffffu;
-    const bool padlane = lane < 16 && ((padmask >> lane) & 1u);
-    double k375 = 0.375;  // kept in a VGPR (not an inline constant)
-    PIN(k375);
-    double m1[17], m2[17];  // m1[c] = L(R0 + c + 1, c - 1), m2[c] = L(R0 + c + 1, c - 2): uniform
-#pragma unroll
-    for (int c = 0; c < 17; ++c) m1[c] = m2[c] = 0.0;
-    double mypiv = 1.0;
-    bool timeout = false;
-    // F's column j and its flag are read two iterations ahead, together (the flag read
-    // executes first in this wave's LDS order, so when it shows the flag set the column read
-    // after it returns the handed-over values; otherwise both are read again)
-    unsigned fl[16];
-    double cf[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        fl[j] = 1u;
-        cf[j] = 0.0;
-    }
-    auto fetch = [&](int j) {
-        fl[j] = __hip_atomic_load(&fflag[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        asm volatile("" ::: "memory");  // the column read stays after the flag read
-        cf[j] = colF[j * 64 + lane];
-    };
-    fetch(4);
-    double piv = readlane_d(v[0], 0);
-    double p = ((padmask & 1u) != 0u) ? 1.0 : piv;
-    double y = __builtin_amdgcn_rsq(p);
-    SB();
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-#ifdef GAPLAC_STAMPS
-        if (s == 5) STAMP(90 + c);
-#endif
-        mypiv = lane == c ? v[c] : mypiv;  // the non-PD test runs after the sweep
-        double t = p * y;
-        PIN(t);  // (the pins keep the chain's steps above the hand-over check's branch)
-        SB();
-        double e = fma(-t, y, 1.0);
-        PIN(e);
-        SB();
-        // column c+1 (F's, fetched two iterations ago; columns 1 .. 3 raw from the block)
-        // gets columns c-2 and c-1 in the chain's shadow
-        if (c + 1 < 16) {
-            if (c + 1 >= 4) {
-                int it = 0;
-                while (fl[c + 1] == 0u && it < (1 << 20)) {
-                    ++it;
-                    fetch(c + 1);
-                }
-                if (fl[c + 1] == 0u) timeout = true;
-                v[c + 1] = cf[c + 1];
-            }
-            if (c >= 2) {
-                v[c + 1] = fma(-v[c - 2], m2[c], v[c + 1]);
-                PIN(v[c + 1]);
-            }
-            if (c >= 1) {
-                v[c + 1] = fma(-v[c - 1], m1[c], v[c + 1]);
-                PIN(v[c + 1]);
-            }
-        }
-        const double cc = fma(e, k375, 0.5);
-        const double ye = y * e;
-        SB();
-        const double rd = fma(ye, cc, y);  // 1/sqrt(p), <= 1 ulp
-        SB();
-        // the diagonal lane's own value is its pivot, so it becomes p * rd = sqrt(p)
-        v[c] = v[c] * rd;
-        SB();
-        // the record (column c's final values into the block column, then rd: the flag) and
-        // F's column c + 3, early: the next LDS wait (above) then finds them done. Unmasked
-        // stores keep the compiler's LDS counts exact; lanes past the last row write to
-        // colF's unused first four columns
-        wblk[c * 16 + rr] = lane > c ? v[c] : (lane == c ? (padlane ? 1.0 : v[c]) : 0.0);
-        rdiag[R0 + c] = rd;  // every lane, the same value
-        if (c + 3 < 16 && c + 3 >= 5) fetch(c + 3);
-        double ln = 0.0;
-        if (c + 1 < 16) ln = readlane_d(v[c], c + 1);
-        SB();
-        if (c + 1 < 16) v[c + 1] = fma(-v[c], ln, v[c + 1]);
-        SB();
-        if (c + 1 < 16) {
-            piv = readlane_d(v[c + 1], c + 1);
-            p = ((padmask >> (c + 1)) & 1u) ? 1.0 : piv;
-            y = __builtin_amdgcn_rsq(p);  // the next pivot's
-            PIN(y);
-        }
-        SB();
-        // this column's multipliers of the next two columns, read back from the record
-        // (LDS broadcast reads: a v_readlane pair costs ~16 issue cycles)
-        if (c + 2 < 16) m1[c + 1] = Ld[c * 16 + c + 2];
-        if (c + 3 < 16) m2[c + 2] = Ld[c * 16 + c + 3];
-        SB();
-    }
-    // OpenBLAS potf2 (the reference's dpotrf, 0.3.20) tests ajj <= 0 only: a NaN pivot is
-    // not reported and propagates to a NaN logpdf, as in the reference
-    const unsigned long long badm = __ballot(lane < 16 && !((padmask >> lane) & 1u) && mypiv <= 0.0);
-    if (badm && lane == 0) atomicMin(&res->info, (unsigned long long)(gcol0 + R0 + __builtin_ctzll(badm) + 1));
-    if (timeout && lane == 0) atomicOr(&res->err, 1u);
-}
-
-// F: rows 16 s + lane (A's rows), columns 4 .. 15 of panel s. Record k is applied to every
-// column j >= k + 4, column k + 4 first; that column then has columns 0 .. k applied and
-// goes to A.
-__device__ __forceinline__ void diag3_sweep_f(const double* Ab, double* colF, unsigned* fflag, const double* rdiag,
-                                              int s, int lane, EvalResult* res) {
-    asm volatile("" : "+v"(lane));
-    const int R0 = 16 * s;
-    const int row = R0 + lane;
-    const bool live = row < NB;
-    const double* blk = Ab + bidx(live ? (row >> 4) : s, s) * 256;
-    const double* Ld = Ab + bidx(s, s) * 256;
-    const int rr = row & 15;
-    double v[16];
-#pragma unroll
-    for (int j = 4; j < 16; ++j) v[j] = blk[j * 16 + rr];
-    bool timeout = false;
-    // record k's flag, row value and multipliers are read together (the flag first in this
-    // wave's LDS order: when it shows rd, the reads after it see the record A wrote before
-    // it), the next record's right after column k + 4 is handed over, so their latency runs
-    // beside the rest of record k's updates
-    double fl = 0.0, rec = 0.0, m[16];
-    auto issue = [&](int k) {
-        fl = __hip_atomic_load(&rdiag[R0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        asm volatile("" ::: "memory");  // the record reads stay after the flag read
-        rec = blk[k * 16 + rr];  // L(row, R0 + k)
-#pragma unroll
-        for (int j = k + 4; j < 16; ++j) m[j] = Ld[k * 16 + j];
-    };
-    issue(0);
-    SB();
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        for (int it = 0; fl == -1.0 && it < (1 << 22); ++it) issue(k);
-        if (fl == -1.0) timeout = true;
-        const double rk = rec;
-        double mk[16];
-#pragma unroll
-        for (int j = k + 4; j < 16; ++j) mk[j] = m[j];
-        // column k + 4 first: it has every earlier record applied (pinned in place below)
-        v[k + 4] = fma(-rk, mk[k + 4], v[k + 4]);
-        colF[(k + 4) * 64 + lane] = v[k + 4];
-        asm volatile("" ::: "memory");
-        if (lane == 0) fflag[k + 4] = 1u;  // after the column in this wave's LDS order
-        SB();
-        if (k + 1 < 12) issue(k + 1);  // next record's reads in flight under this record's updates
-        SB();
-#pragma unroll
-        for (int j = k + 5; j < 16; ++j) {
-            v[j] = fma(-rk, mk[j], v[j]);
-            PIN(v[j]);  // applied now, not sunk into the hand-over of column j
-        }
-        SB();
-    }
-    if (timeout && lane == 0) atomicOr(&res->err, 1u);
-}
-
-// B (rows 16 s + 64 + lane, s < 4) in v3: diag2_sweep_b's arithmetic with the flag in
-// rdiag and the multipliers read from A's records in the diagonal block.
-__device__ __forceinline__ void diag3_sweep_b(double* Ab, const double* rdiag, int s, int lane, EvalResult* res) {
-    asm volatile("" : "+v"(lane));
-    const int row = 16 * s + 64 + lane;
-    const bool live = row < NB;
-    double* blk = Ab + bidx(live ? (row >> 4) : NDB - 1, s) * 256;
-    const double* Ld = Ab + bidx(s, s) * 256;
-    const int rr = row & 15;
-    double v[16];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) v[c] = blk[c * 16 + rr];
-    bool timeout = false;
-    double fl = __hip_atomic_load(&rdiag[16 * s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        for (int it = 0; fl == -1.0 && it < (1 << 20); ++it) {
-            __builtin_amdgcn_s_sleep(1);
-            fl = __hip_atomic_load(&rdiag[16 * s + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        if (fl == -1.0) {
-            timeout = true;
-            fl = __builtin_nan("");
-        }
-        const double rd = fl;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the record's values after its flag
-        double lc[16];
-#pragma unroll
-        for (int c2 = c + 1; c2 < 16; ++c2) lc[c2] = Ld[c * 16 + c2];
-        if (c + 1 < 16) fl = __hip_atomic_load(&rdiag[16 * s + c + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const double l = v[c] * rd;
-        v[c] = l;
-#pragma unroll
-        for (int c2 = c + 1; c2 < 16; ++c2) v[c2] = fma(-l, lc[c2], v[c2]);
-    }
-    if (timeout && lane == 0) atomicOr(&res->err, 1u);
-    if (live) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) blk[c * 16 + rr] = v[c];
-    }
-}
-
 // Dinv_s = L_ss^{-1} (column-major 16x16 into global): lane j < 16 solves L x = e_j
 // right-looking (x[m] final, then every later row updated with it).
 template <int AUX>
@@ -1356,17 +1114,13 @@ __device__ __forceinline__ void diag2_store_column(const double* Ab, double* Ag,
 // 512 threads: wave 0 = A (the pivot chain), wave 1 = B (rows 64+ of panels 0-3), waves 2-7
 // the trailing updates, the stores of finished block columns and (wave 7) the inverses.
 // Waves w and w + 4 share a SIMD, so every SIMD's matrix pipe takes trailing work.
-#ifndef GAPLAC_DINV_WAVE
-#define GAPLAC_DINV_WAVE 6  // the diagonal kernel's inverse wave: 6 (SIMD 2); 4 shares wave A's SIMD
-#endif
-template <int AUX, int FW = GAPLAC_DIAG_FW, int DINV_WAVE = GAPLAC_DINV_WAVE>
+template <int AUX>
 __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restrict__ Ag, int64_t lda, int64_t N,
                                                  int64_t g0, double* __restrict__ Dinv, EvalResult* __restrict__ res,
                                                  double* Dl = nullptr, unsigned* prog = nullptr) {
-    double* colbuf = smem;  // v2: the column records; v3: F's hand-over columns (colF)
+    double* colbuf = smem;
     double* rdiag = colbuf + DIAG2_COLBUF;
     double* Ab = rdiag + NB;
-    unsigned* fflag = reinterpret_cast<unsigned*>(Ab + NPK * 256);  // v3: column j handed over by F
     const int t = otid(), wave = t >> 6, lane = t & 63;
     // the chain first (wave-uniform branches: s_setprio takes an immediate)
     if (wave == 0) __builtin_amdgcn_s_setprio(3);
@@ -1406,15 +1160,7 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
             }
         }
     }
-    if (FW) {
-        if (wave == 3) {  // every column's flag (rdiag) and F's hand-over flags
-            rdiag[lane] = -1.0;
-            rdiag[64 + lane] = -1.0;
-            if (lane < 16) fflag[lane] = 0u;
-        }
-    } else if (wave == 3 && lane < 16) {
-        colbuf[lane * 64 + lane] = -1.0;  // the records' flags
-    }
+    if (wave == 3 && lane < 16) colbuf[lane * 64 + lane] = -1.0;  // the records' flags
     // a barrier that does not wait for the other blocks' loads (__syncthreads would)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1423,9 +1169,7 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
         if (s >= 1) {
             // phase 1: panel s-1 into block column s (the diagonal block first, on wave 0)
             for (int I = s + wave; I < NDB; I += 8) dblk_update(Ab, I, s, s - 1, lane);
-            if (FW) {
-                if (wave == 3 && lane < 16) fflag[lane] = 0u;  // F's hand-over flags of panel s
-            } else if (wave == 3 && lane < 16) {
+            if (wave == 3 && lane < 16) {
                 rdiag[16 * (s - 1) + lane] = colbuf[lane * 64 + lane];  // rd of panel s-1's columns
                 colbuf[lane * 64 + lane] = -1.0;                        // the records' flags
             }
@@ -1439,28 +1183,9 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
         if (prog && s >= 2 && wave == 3 && lane == 0)  // columns and inverses 0 .. s-2 final
             __hip_atomic_store(prog, (unsigned)(s - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (wave == 0) {
-            if (FW)
-                diag3_sweep_a(Ab, colbuf, fflag, rdiag, s, lane, g0, N, res);
-            else
-                diag2_sweep_a(Ab, colbuf, s, lane, g0, N, res);
+            diag2_sweep_a(Ab, colbuf, s, lane, g0, N, res);
         } else if (wave == 1 && s < 4) {
-            if (FW)
-                diag3_sweep_b(Ab, rdiag, s, lane, res);
-            else
-                diag2_sweep_b(Ab, colbuf, s, lane, res);
-        } else if (FW && wave == 7) {
-            diag3_sweep_f(Ab, colbuf, fflag, rdiag, s, lane, res);
-            if (s == 0) {  // wave 7's share of the rest of the block
-#pragma unroll
-                for (int i = 0; i < 10; ++i) {
-                    const int q = tt + 384 * i;
-                    if (q < 28 * 128) {
-                        int I, J;
-                        diag2_block_of(q >> 7, I, J);
-                        *reinterpret_cast<double2*>(&Ab[bidx(I, J) * 256 + 2 * (q & 127)]) = rest[i];
-                    }
-                }
-            }
+            diag2_sweep_b(Ab, colbuf, s, lane, res);
         } else {
             if (s == 0 && wave >= 2) {  // the rest of the block into LDS
 #pragma unroll
@@ -1474,20 +1199,15 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
                 }
             }
             if (s >= 1) {
-                // the inverse's wave (VALU work) sits off wave A's SIMD (waves w and w + 4 share
-                // one: round 3 had it on wave 4, beside A); the trailing blocks (MFMA) go to the
-                // other waves 2 .. 7 but F
-                if (wave >= 2) diag2_store_column<AUX>(Ab, Ag, lda, s - 1, t - 128, FW ? 320 : 384);
+                // wave 4 shares wave A's SIMD: it only stores and inverts (light), the
+                // trailing blocks go to waves 2, 3, 5, 6, 7 (and 1 from panel 4 on)
+                if (wave >= 2) diag2_store_column<AUX>(Ab, Ag, lda, s - 1, t - 128, 384);
                 STAMPT(128, 40 + s);  // wave 2: after its share of the stores
-                if (wave == DINV_WAVE) {
+                if (wave == 4) {
                     diag2_dinv<AUX>(Ab, Dinv, rdiag, s - 1, lane, Dl);
                 } else {
-                    // trailing waves: 2 .. 7 without the inverse's wave (and F's, wave 7, in v3),
-                    // numbered 0 ..; wave 1 joins from panel 4 on
-                    const int wi = wave - 2 - (wave > DINV_WAVE ? 1 : 0);
-                    const int nw = FW ? 4 : 5;
-                    const int w = wave == 1 ? 0 : (s < 4 ? 0 : 1) + wi;
-                    diag2_trailing(Ab, s, w, s < 4 ? nw : nw + 1, lane);
+                    const int w = wave == 1 ? 0 : (s < 4 ? 0 : 1) + (wave < 4 ? wave - 2 : wave - 3);
+                    diag2_trailing(Ab, s, w, s < 4 ? 5 : 6, lane);
                 }
             }
         }
@@ -1501,15 +1221,15 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
         STAMPT(448, 72 + s);
         __syncthreads();
     }
-    if (!FW && wave == 3 && lane < 16) rdiag[16 * (NDB - 1) + lane] = colbuf[lane * 64 + lane];
+    if (wave == 3 && lane < 16) rdiag[16 * (NDB - 1) + lane] = colbuf[lane * 64 + lane];
     if (prog && wave >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (prog && wave == 3 && lane == 0)  // columns and inverses 0 .. 6 final
         __hip_atomic_store(prog, (unsigned)(NDB - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     STAMP(17);
-    if (wave == DINV_WAVE) diag2_dinv<AUX>(Ab, Dinv, rdiag, NDB - 1, lane, Dl);
+    if (wave == 4) diag2_dinv<AUX>(Ab, Dinv, rdiag, NDB - 1, lane, Dl);
     STAMP(18);
-    if (wave != DINV_WAVE) diag2_store_column<AUX>(Ab, Ag, lda, NDB - 1, wave < DINV_WAVE ? t : t - 64, 448);
+    if (wave != 4) diag2_store_column<AUX>(Ab, Ag, lda, NDB - 1, wave < 4 ? t : t - 64, 448);
     STAMP(19);
 }
 #undef SB

@@ -15,17 +15,8 @@ __global__ __launch_bounds__(256) void diag_v1(double* Ag, int64_t lda, int64_t 
 }
 __global__ __launch_bounds__(512) void diag_v2(double* Ag, int64_t lda, int64_t N, int64_t g0, double* Dinv, EvalResult* res) {
   __shared__ double smem[DIAG2_SMEM];
-  potrf_diag2_body<0, 0, 4>(smem, Ag, lda, N, g0, Dinv, res);
+  potrf_diag2_body<0>(smem, Ag, lda, N, g0, Dinv, res);
 }
-__global__ __launch_bounds__(512) void diag_v3(double* Ag, int64_t lda, int64_t N, int64_t g0, double* Dinv, EvalResult* res) {
-  __shared__ double smem[DIAG2_SMEM];
-  potrf_diag2_body<0, 1, 6>(smem, Ag, lda, N, g0, Dinv, res);
-}
-__global__ __launch_bounds__(512) void diag_v4(double* Ag, int64_t lda, int64_t N, int64_t g0, double* Dinv, EvalResult* res) {
-  __shared__ double smem[DIAG2_SMEM];
-  potrf_diag2_body<0, 0, 6>(smem, Ag, lda, N, g0, Dinv, res);
-}
-
 int main() {
   const int nt = 4, Np = nt * NB;
   std::vector<double> h((size_t)Np * Np, 0.0);
@@ -59,16 +50,14 @@ int main() {
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
     if (v == 1) diag_v1<<<1, 256>>>(A, Np, N, 0, Dinv, res);
-    else if (v == 2) diag_v2<<<1, 512>>>(A, Np, N, 0, Dinv, res);
-    else if (v == 3) diag_v3<<<1, 512>>>(A, Np, N, 0, Dinv, res);
-    else diag_v4<<<1, 512>>>(A, Np, N, 0, Dinv, res);
+    else diag_v2<<<1, 512>>>(A, Np, N, 0, Dinv, res);
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(ms, e0, e1));
     CK(hipMemcpy(out.data(), A, out.size() * 8, hipMemcpyDeviceToHost));
     CK(hipMemcpy(dinv.data(), Dinv, dinv.size() * 8, hipMemcpyDeviceToHost));
     return 0;
   };
-  for (int v = 1; v <= 4; ++v) {
+  for (int v = 1; v <= 2; ++v) {
     for (int rep = 0; rep < 4; ++rep) {
       float ms;
       if (run(v, h, 1 << 30, &ms)) return 1;
@@ -97,56 +86,48 @@ int main() {
           printf("  v%d s=%d: phase1+barrier %5llu | phase2 w0 %5llu w1 %5llu w%d %5llu\n", v, s,
                  p2 - (s ? st[2 * s] : st[0]), st[2 + 2 * s] - p2, st[29 + s] - p2, v == 1 ? 3 : 2, st[21 + s] - p2);  // v2: stamps of waves 1 and 2
         }
-        if (v >= 2)
+        if (v == 2)
           for (int s = 0; s < 8; ++s) {
             const unsigned long long p2 = st[1 + 2 * s];
             printf("  v%d s=%d phase2 ends: w0 %5llu w1 %5llu w2 %5llu (stores %5llu) w3 %5llu w4 %5llu w5 %5llu w6 %5llu w7 %5llu\n", v, s,
                    st[2 + 2 * s] - p2, st[29 + s] - p2, st[21 + s] - p2, s ? st[40 + s] - p2 : 0ull, st[48 + s] - p2,
                    st[80 + s] - p2, st[56 + s] - p2, st[64 + s] - p2, st[72 + s] - p2);
           }
-        if (v == 3) {
-          printf("  v3 s=5 A column starts:");
-          for (int c = 1; c < 16; ++c) printf(" %llu", st[90 + c] - st[89 + c]);
-          printf("\n");
-        }
         printf("  v%d last dinv %llu store %llu total %llu cycles\n", v, st[18] - st[17], st[19] - st[18], st[19] - st[20]);
       }
     }
   }
-  // v2 against v1, and v3 against v2 (bitwise), with padding inside the block (N = 100, 127,
-  // 37, 1: unit pivots from there) and without (N = 2^30)
+  // v2 against v1 with padding inside the block (N = 100, 127, 37, 1: unit pivots from
+  // there) and without (N = 2^30)
   for (int64_t Npad : {(int64_t)1 << 30, (int64_t)100, (int64_t)127, (int64_t)37, (int64_t)1}) {
     float ms;
     std::vector<double> hp = h;
     for (int j = 0; j < Np; ++j)
       for (int i = 0; i < Np; ++i)
         if ((i >= Npad || j >= Npad) && i != j) hp[(size_t)j * Np + i] = (i == Npad && j < Npad) ? 0.3 * std::sin(j) : 0.0;
-    std::vector<double> o[5], d[5];
-    EvalResult hv[5];
-    for (int v = 1; v <= 4; ++v) {
+    std::vector<double> o[3], d[3];
+    EvalResult hv[3];
+    for (int v = 1; v <= 2; ++v) {
       if (run(v, hp, Npad, &ms)) return 1;
       o[v] = out;
       d[v] = dinv;
       CK(hipMemcpy(&hv[v], res, sizeof hv[v], hipMemcpyDeviceToHost));
     }
-    double dl = 0, dd = 0, dl3 = 0, dd3 = 0;
+    double dl = 0, dd = 0;
     for (int j = 0; j < NB; ++j)
       for (int i = j; i < NB; ++i) {
         dl = std::fmax(dl, std::fabs(o[2][(size_t)j * Np + i] - o[1][(size_t)j * Np + i]));
-        dl3 = std::fmax(dl3, std::fabs(o[3][(size_t)j * Np + i] - o[2][(size_t)j * Np + i]));
-        dl3 = std::fmax(dl3, std::fabs(o[4][(size_t)j * Np + i] - o[2][(size_t)j * Np + i]));
+
       }
     for (int k = 0; k < DINV_PER_BLOCK; ++k) {
       dd = std::fmax(dd, std::fabs(d[2][k] - d[1][k]));
-      dd3 = std::fmax(dd3, std::fabs(d[3][k] - d[2][k]));
-      dd3 = std::fmax(dd3, std::fabs(d[4][k] - d[2][k]));
+
     }
-    printf("padded N=%lld: max|L2-L1| %.2e max|Dinv2-Dinv1| %.2e | max|L3,4-L2| %.2e max|Dinv3,4-Dinv2| %.2e | info %llx/%llx/%llx err %u/%u\n",
-           (long long)Npad, dl, dd, dl3, dd3, (unsigned long long)hv[1].info, (unsigned long long)hv[2].info,
-           (unsigned long long)hv[3].info, hv[2].err, hv[3].err);
+    printf("padded N=%lld: max|L2-L1| %.2e max|Dinv2-Dinv1| %.2e | info %llx/%llx err %u\n", (long long)Npad, dl, dd,
+           (unsigned long long)hv[1].info, (unsigned long long)hv[2].info, hv[2].err);
   }
   // non-PD: zero the block's (37,37) pivot region -> info must be 38 in both
-  for (int v = 1; v <= 4; ++v) {
+  for (int v = 1; v <= 2; ++v) {
     std::vector<double> hb = h;
     for (int i = 0; i < Np; ++i) { hb[(size_t)37 * Np + i] = 0; hb[(size_t)i * Np + 37] = 0; }
     float ms;
