@@ -16,14 +16,22 @@
 //   bcast(s)       the host broadcasts panel buffer s&1 from the owner (RCCL on the
 //                  comm stream, gaplac_dist_comm_begin/_end bracket it)
 //   update(s)      all ranks: bulk trailing update of their SPs > s+1 with panel s
-//                  (s_main); SP s+1 gets panel s in factor(s+1) instead
+//                  (s_main); SP s+1 gets panel s in factor(s+1) instead. Paired updates
+//                  (the single-GPU schedule's): an even step s whose
+//                  trailing matrix still has >= pair_m tile rows after SP s+3 updates only
+//                  SPs s+2 and s+3 (the next chain needs them); step s+1 then updates SP
+//                  s+3 with panel s+1 and every SP >= s+4 with panels s and s+1 at once
+//                  (K = 2 x 128 W: half the launches, twice the depth)
 //   finish         all ranks: partial logdet / quad / info over their columns; the host
 //                  sums them across ranks (one allreduce of 3 numbers)
 // The host calls, per rank: begin; factor(0) [owner]; bcast(0); for s = 0..nsp-1:
 // { factor(s+1) [owner of s+1]; update(s); bcast(s+1) }; finish. Every call only
 // enqueues work: the streams overlap the bulk update with the next panel's chain.
-// Panel buffers are double-buffered; events keep a buffer from being re-filled (packed
-// by its owner or received) before the updates that read it have run.
+// Panel buffers: two PAIR buffers; panels s and s+1 (s even) share pair buffer (s/2) & 1
+// with the rows of panel s as the common origin (ld = Np - first row of SP s; the odd
+// panel's columns start 128 W rows down), so a paired update reads both as one K = 256 W
+// panel. Events keep a pair buffer from being re-filled (packed by its owner or received)
+// before the updates and lookaheads that read its previous pair have run.
 #include "gaplac_internal.h"
 
 #include <cstddef>
@@ -32,6 +40,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -42,7 +51,11 @@ struct gaplac_dist {
     int device = 0, nranks = 1, rank = 0, W = 4;
     hipStream_t s_main = nullptr, s_panel = nullptr, s_comm = nullptr;
     hipEvent_t ev_gram = nullptr, ev_panel_done = nullptr;
-    hipEvent_t ev_recv[2] = {}, ev_packed[2] = {}, ev_free_main[2] = {}, ev_free_panel[2] = {};
+    // ev_recv / ev_packed per panel parity; ev_step[s & 1]: update(s) done (the last bulk
+    // update of SP s+2's columns); ev_free_main / ev_free_panel per pair buffer: its last
+    // bulk update / lookahead reader done
+    hipEvent_t ev_recv[2] = {}, ev_packed[2] = {}, ev_step[2] = {}, ev_free_main[2] = {}, ev_free_panel[2] = {};
+    int pair_m = 40;  // GAPLAC_PAIR_M: paired updates while >= pair_m tile rows follow SP s+3
     // geometry of the current evaluation
     int64_t N = -1, Np = 0;
     int nt = 0, nsp = 0, nloc = 0;
@@ -53,13 +66,15 @@ struct gaplac_dist {
     double* Dinv = nullptr;
     size_t Dinv_elems = 0;
     double* pbuf[2] = {};
-    size_t pbuf_cap = 0;   // elements per buffer
+    size_t pbuf_cap = 0;   // elements per (pair) buffer
     bool pbuf_external = false;
     uint32_t* tiles = nullptr;
     size_t tiles_elems = 0;
     int gram_count = 0;                  // gram list at tiles[0 .. gram_count)
     std::vector<size_t> bulk_off;        // per owned-SP ordinal u: suffix list offset
     std::vector<int> bulk_cnt;           //                            and tile count
+    std::vector<size_t> band_off;        // per owned-SP ordinal u: its own tiles only
+    std::vector<int> band_cnt;
     int64_t lists_N = -1;
     double* dX = nullptr;
     size_t dX_elems = 0;
@@ -112,12 +127,21 @@ int sp_first(const gaplac_dist* d, int s) { return s * d->W; }
 int sp_width(const gaplac_dist* d, int s) { return std::min(d->W, d->nt - s * d->W); }
 int sp_local(const gaplac_dist* d, int s) { return (s / d->nranks) * d->W; }  // first local column
 bool owns(const gaplac_dist* d, int s) { return s % d->nranks == d->rank; }
-// panel buffer geometry of SP s: rows r0 .. Np-1, ld = Np - r0, width*NB columns
 int64_t panel_row0(const gaplac_dist* d, int s) { return (int64_t)sp_first(d, s) * NB; }
-int64_t panel_ld(const gaplac_dist* d, int s) { return d->Np - panel_row0(d, s); }
-
+// pair buffer of panel s: (s / 2) & 1; its origin row is that of the pair's even panel
+int pair_buf(int s) { return (s >> 1) & 1; }
+int64_t pair_row0(const gaplac_dist* d, int s) { return panel_row0(d, s & ~1); }
+int64_t pair_ld(const gaplac_dist* d, int s) { return d->Np - pair_row0(d, s); }
+// first element of panel s (its row panel_row0(s), column 0) in its pair buffer
+double* panel_ptr(const gaplac_dist* d, int s) {
+    return d->pbuf[pair_buf(s)] + (int64_t)(s & 1) * d->W * NB * pair_ld(d, s) + (panel_row0(d, s) - pair_row0(d, s));
+}
 Panel panel_of(const gaplac_dist* d, int s) {
-    return Panel{d->pbuf[s & 1], panel_ld(d, s), panel_row0(d, s)};
+    return Panel{d->pbuf[pair_buf(s)] + (int64_t)(s & 1) * d->W * NB * pair_ld(d, s), pair_ld(d, s), pair_row0(d, s)};
+}
+// does step s defer (paired updates)? Even steps only: panels s and s+1 share a buffer.
+bool pair_step(const gaplac_dist* d, int s) {
+    return d->pair_m > 0 && (s & 1) == 0 && s + 4 <= d->nsp && d->nt - (s + 4) * d->W >= d->pair_m;
 }
 
 // Tile lists: the Gram list (all owned lower tiles), then for every owned SP ordinal u
@@ -151,6 +175,16 @@ int build_lists(gaplac_dist* d) {
         d->bulk_off[(size_t)u] = host.size();
         d->bulk_cnt[(size_t)u] = (int)v.size();
         for (const E& e : v) host.push_back((uint32_t)e.bi | ((uint32_t)e.lj << 16));
+    }
+    d->band_off.assign((size_t)nown, 0);
+    d->band_cnt.assign((size_t)nown, 0);
+    for (int u = 0; u < nown; ++u) {  // SP u's tiles, rows outer (one band, as the single path's)
+        d->band_off[(size_t)u] = host.size();
+        const int l0 = u * d->W, l1 = std::min(d->nloc, l0 + d->W);
+        for (int bi = cm.global(l0); bi < d->nt; ++bi)
+            for (int lj = l0; lj < l1; ++lj)
+                if (bi >= cm.global(lj)) host.push_back((uint32_t)bi | ((uint32_t)lj << 16));
+        d->band_cnt[(size_t)u] = (int)(host.size() - d->band_off[(size_t)u]);
     }
     int rc;
     if ((rc = dgrow(d, &d->tiles, &d->tiles_elems, host.size()))) return rc;
@@ -211,9 +245,10 @@ int gaplac_dist_create(int device, int nranks, int rank, int spw, gaplac_dist** 
         return fail("stream", e);
     if ((e = hipStreamCreateWithPriority(&d->s_main, hipStreamNonBlocking, least)) != hipSuccess)
         return fail("stream", e);
+    if (const char* e = std::getenv("GAPLAC_PAIR_M")) d->pair_m = std::max(0, std::atoi(e));
     hipEvent_t* evs[] = {&d->ev_gram, &d->ev_panel_done, &d->ev_recv[0], &d->ev_recv[1], &d->ev_packed[0],
-                         &d->ev_packed[1], &d->ev_free_main[0], &d->ev_free_main[1], &d->ev_free_panel[0],
-                         &d->ev_free_panel[1]};
+                         &d->ev_packed[1], &d->ev_step[0], &d->ev_step[1], &d->ev_free_main[0],
+                         &d->ev_free_main[1], &d->ev_free_panel[0], &d->ev_free_panel[1]};
     for (hipEvent_t* ev : evs)
         if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return fail("event", e);
     if ((e = hipMalloc(reinterpret_cast<void**>(&d->dres), sizeof(EvalResult))) != hipSuccess)
@@ -234,8 +269,8 @@ int gaplac_dist_destroy(gaplac_dist* d) {
     for (hipStream_t s : {d->s_main, d->s_panel, d->s_comm})
         if (s) (void)hipStreamSynchronize(s);
     hipEvent_t evs[] = {d->ev_gram, d->ev_panel_done, d->ev_recv[0], d->ev_recv[1], d->ev_packed[0],
-                        d->ev_packed[1], d->ev_free_main[0], d->ev_free_main[1], d->ev_free_panel[0],
-                        d->ev_free_panel[1]};
+                        d->ev_packed[1], d->ev_step[0], d->ev_step[1], d->ev_free_main[0],
+                        d->ev_free_main[1], d->ev_free_panel[0], d->ev_free_panel[1]};
     for (hipEvent_t ev : evs)
         if (ev) (void)hipEventDestroy(ev);
     for (void* p : {(void*)d->C, (void*)d->Dinv, (void*)d->tiles, (void*)d->dX, (void*)d->dv, (void*)d->dres,
@@ -277,7 +312,7 @@ int gaplac_dist_set_panel_buffers(gaplac_dist* d, void* b0, void* b1, int64_t ca
 }
 
 // Geometry for N: padded order, tile / super-panel counts, this rank's local tile
-// columns, and the doubles one panel buffer needs (largest panel = SP 0).
+// columns, and the doubles one (pair) panel buffer needs (the pair of SPs 0 and 1).
 int gaplac_dist_geometry(gaplac_dist* d, int64_t N, int64_t* Np, int32_t* nt, int32_t* nsp, int32_t* nloc,
                          int64_t* panel_elems) {
     if (!d || N < 1) return derr(d, GAPLAC_E_ARG, "bad geometry query");
@@ -290,7 +325,7 @@ int gaplac_dist_geometry(gaplac_dist* d, int64_t N, int64_t* Np, int32_t* nt, in
     if (nt) *nt = t;
     if (nsp) *nsp = ns;
     if (nloc) *nloc = nl;
-    if (panel_elems) *panel_elems = np * (int64_t)std::min(d->W, t) * NB;
+    if (panel_elems) *panel_elems = np * (int64_t)std::min(2 * d->W, t) * NB;
     return 0;
 }
 
@@ -364,13 +399,18 @@ int gaplac_dist_factor(gaplac_dist* d, int32_t s) {
     hipStream_t sp = d->s_panel;
     const int c0 = sp_first(d, s), w = sp_width(d, s), lc0 = sp_local(d, s);
     const int64_t ldc = d->Np;
-    // update(s-2) (s_main) was the last bulk update of SP s's columns, and it read panel
-    // buffer s&1, which the pack below overwrites
-    DCK(d, hipStreamWaitEvent(sp, d->ev_free_main[s & 1], 0));
+    // update(s-2) (s_main) was the last bulk update of SP s's columns (a paired update at
+    // an odd step covers SPs >= step + 3, a deferring step's bands SPs step + 2, step + 3),
+    // and the pack below overwrites pair buffer pair_buf(s): its previous pair's last bulk
+    // update ran before (ev_free_main; its lookahead readers are earlier on this stream)
+    DCK(d, hipStreamWaitEvent(sp, d->ev_step[s & 1], 0));
+    DCK(d, hipStreamWaitEvent(sp, d->ev_free_main[pair_buf(s)], 0));
     if (s > 0) {
         DCK(d, hipStreamWaitEvent(sp, d->ev_recv[(s - 1) & 1], 0));
         launch_col_update(sp, d->C, ldc, panel_of(d, s - 1), d->nt, c0, lc0, w, sp_width(d, s - 1) * NB, nullptr);
-        DCK(d, hipEventRecord(d->ev_free_panel[(s - 1) & 1], sp));
+        // this rank's latest lookahead reading the pair buffer (the receive of the buffer's
+        // next pair waits for it on the comm stream)
+        DCK(d, hipEventRecord(d->ev_free_panel[pair_buf(s - 1)], sp));
     }
     for (int c = c0; c < c0 + w; ++c) {
         const int lc = lc0 + (c - c0);
@@ -382,9 +422,9 @@ int gaplac_dist_factor(gaplac_dist* d, int32_t s) {
             launch_potrf_diag(sp, Acol + (int64_t)c * NB, ldc, d->N, (int64_t)c * NB, Dk, d->dres, nullptr);
         launch_trsm(sp, Acol, ldc, d->nt, c, Dk, nullptr);
     }
-    const int64_t r0 = panel_row0(d, s), ldp = panel_ld(d, s);
-    DCK(d, hipMemcpy2DAsync(d->pbuf[s & 1], (size_t)ldp * 8, d->C + (int64_t)lc0 * NB * ldc + r0, (size_t)ldc * 8,
-                            (size_t)ldp * 8, (size_t)w * NB, hipMemcpyDeviceToDevice, sp));
+    const int64_t r0 = panel_row0(d, s), ldp = pair_ld(d, s);
+    DCK(d, hipMemcpy2DAsync(panel_ptr(d, s), (size_t)ldp * 8, d->C + (int64_t)lc0 * NB * ldc + r0, (size_t)ldc * 8,
+                            (size_t)(d->Np - r0) * 8, (size_t)w * NB, hipMemcpyDeviceToDevice, sp));
     DCK(d, hipEventRecord(d->ev_packed[s & 1], sp));
     DCK(d, hipEventRecord(d->ev_panel_done, sp));
     d->factored_any = true;
@@ -395,8 +435,10 @@ int gaplac_dist_factor(gaplac_dist* d, int32_t s) {
 // Device buffer, element count and root rank of the broadcast of panel s.
 int gaplac_dist_panel(gaplac_dist* d, int32_t s, void** ptr, int64_t* count, int32_t* root) {
     if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "panel: step %d out of range", s);
-    if (ptr) *ptr = d->pbuf[s & 1];
-    if (count) *count = panel_ld(d, s) * sp_width(d, s) * NB;
+    // the panel's columns in its pair buffer, from its first row to the end of its last
+    // column (an odd panel's column gaps above its first row go along: 128 W rows each)
+    if (ptr) *ptr = panel_ptr(d, s);
+    if (count) *count = (int64_t)sp_width(d, s) * NB * pair_ld(d, s) - (panel_row0(d, s) - pair_row0(d, s));
     if (root) *root = s % d->nranks;
     return 0;
 }
@@ -409,9 +451,9 @@ int gaplac_dist_comm_begin(gaplac_dist* d, int32_t s, void** stream) {
     DCK(d, hipSetDevice(d->device));
     if (owns(d, s)) {
         DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_packed[s & 1], 0));
-    } else {
-        DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_free_main[s & 1], 0));
-        DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_free_panel[s & 1], 0));
+    } else {  // the pair buffer's previous pair: its last bulk update and last lookahead
+        DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_free_main[pair_buf(s)], 0));
+        DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_free_panel[pair_buf(s)], 0));
     }
     if (stream) *stream = d->s_comm;
     return 0;
@@ -425,25 +467,52 @@ int gaplac_dist_comm_end(gaplac_dist* d, int32_t s) {
     return 0;
 }
 
-// Bulk trailing update with panel s of this rank's SPs > s+1 (s_main).
+// Bulk trailing update with panel s of this rank's SPs > s+1 (s_main), or with paired
+// updates (pair_step): a deferring step s updates SPs s+2, s+3 only; step s+1 updates SP
+// s+3 with panel s+1 and the SPs >= s+4 with panels s, s+1 (one K = 256 W launch).
 int gaplac_dist_update(gaplac_dist* d, int32_t s) {
     if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "update: step %d out of range", s);
     DCK(d, hipSetDevice(d->device));
     DCK(d, hipStreamWaitEvent(d->s_main, d->ev_recv[s & 1], 0));
-    // first owned SP with index > s+1
-    const int rel = s + 1 - d->rank;
-    const int u = rel < 0 ? 0 : rel / d->nranks + 1;
-    if (u < (int)d->bulk_cnt.size() && d->bulk_cnt[(size_t)u] > 0) {
-        BulkArgs ba{d->C, d->Np, panel_of(d, s), d->tiles + d->bulk_off[(size_t)u], d->bulk_cnt[(size_t)u],
-                    sp_width(d, s) * NB, 0, 0, cmap(d)};
+    const bool defer = pair_step(d, s), paired = s >= 1 && pair_step(d, s - 1);
+    // owned-SP ordinal of the first owned SP >= g
+    auto ord_from = [&](int g) {
+        const int rel = g - d->rank;
+        return rel <= 0 ? 0 : (rel + d->nranks - 1) / d->nranks;
+    };
+    auto launch = [&](const uint32_t* tiles, int cnt, const Panel& pn, int kd) -> int {
+        if (cnt <= 0) return 0;
+        BulkArgs ba{d->C, d->Np, pn, tiles, cnt, kd, 0, 0, cmap(d)};
         ba.max_r = d->nt - 1;    // list entries: global row block
         ba.max_c = d->nloc - 1;  //              and local tile column
         DistGuard guard(d);
         launch_bulk(d->s_main, ba, nullptr);
-        int rc;
-        if ((rc = guard.check())) return rc;
+        return guard.check();
+    };
+    auto band = [&](int g, const Panel& pn, int kd) -> int {  // SP g alone, if owned
+        if (g >= d->nsp || !owns(d, g)) return 0;
+        const size_t u = (size_t)(g / d->nranks);
+        return launch(d->tiles + d->band_off[u], d->band_cnt[u], pn, kd);
+    };
+    auto suffix = [&](int g, const Panel& pn, int kd) -> int {  // owned SPs >= g
+        const int u = ord_from(g);
+        if (u >= (int)d->bulk_cnt.size()) return 0;
+        return launch(d->tiles + d->bulk_off[(size_t)u], d->bulk_cnt[(size_t)u], pn, kd);
+    };
+    const int kd = sp_width(d, s) * NB;
+    int rc;
+    if (defer) {
+        if ((rc = band(s + 2, panel_of(d, s), kd)) || (rc = band(s + 3, panel_of(d, s), kd))) return rc;
+    } else if (paired) {
+        DCK(d, hipStreamWaitEvent(d->s_main, d->ev_recv[(s - 1) & 1], 0));
+        if ((rc = band(s + 2, panel_of(d, s), kd))) return rc;
+        if ((rc = suffix(s + 3, panel_of(d, s - 1), sp_width(d, s - 1) * NB + kd))) return rc;
+    } else {
+        if ((rc = suffix(s + 2, panel_of(d, s), kd))) return rc;
     }
-    DCK(d, hipEventRecord(d->ev_free_main[s & 1], d->s_main));
+    DCK(d, hipEventRecord(d->ev_step[s & 1], d->s_main));
+    // the pair's last bulk reader: its odd step (or an even step with no odd partner)
+    if ((s & 1) || s + 1 >= d->nsp) DCK(d, hipEventRecord(d->ev_free_main[pair_buf(s)], d->s_main));
     DCK(d, hipGetLastError());
     return 0;
 }

@@ -95,8 +95,16 @@ class DistRank:
             self._check(self.lib.gaplac_dist_set_panel_buffers(
                 self.h, c_void_p(self._bufs[0].data_ptr()), c_void_p(self._bufs[1].data_ptr()), need))
 
-    def panel_tensor(self, s: int, count: int):
-        return self._bufs[s & 1][:count]
+    def panel_tensor(self, s: int, count: int, ptr: int = None):
+        """The torch view of panel s (count doubles at ptr, inside one of the two pair
+        buffers: gaplac_dist_panel)."""
+        if ptr is None:
+            ptr = self.panel(s)[0]
+        for b in self._bufs:
+            off = (ptr - b.data_ptr()) // 8
+            if 0 <= off and off + count <= b.numel():
+                return b[off:off + count]
+        raise GaplacError(_native.E_ARG, f"panel {s} is outside the panel buffers")
 
     # ---- steps
     def begin(self, X: np.ndarray, terms, noise: float, v: np.ndarray) -> int:
@@ -186,9 +194,9 @@ class TorchTransport:
         import torch
         import torch.distributed as dist
         (r,) = ranks
-        _ptr, count, root = r.panel(s)
+        ptr, count, root = r.panel(s)
         stream = r.comm_begin(s)
-        buf = r.panel_tensor(s, count)
+        buf = r.panel_tensor(s, count, ptr)
         src = dist.get_global_rank(self.group, root) if self.group is not None else root
         if stream and buf.is_cuda:
             st = torch.cuda.ExternalStream(stream, device=buf.device)

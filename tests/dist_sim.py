@@ -34,7 +34,7 @@ class SimRank:
         need = self.geometry(N)["panel_elems"]
         self._bufs = [torch.zeros(need, dtype=torch.float64) for _ in range(2)]
 
-    def panel_tensor(self, s, count):
+    def panel_tensor(self, s, count, ptr=None):
         return self._bufs[s & 1][:count]
 
     # global tile column of local tile column lj (ColMap::global)
