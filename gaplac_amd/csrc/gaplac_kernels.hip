@@ -2325,7 +2325,7 @@ __device__ __forceinline__ void tail_trsm_pipe(double* smem, unsigned* rowf, dou
             int avail = 0;
             if (lane == 0) {
                 const unsigned long long t0 = wall_clock64();
-                for (;;) {
+                for (unsigned it = 1;; ++it) {
                     if (__hip_atomic_load(ddone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
                         avail = NDB;
                     } else {
@@ -2333,8 +2333,9 @@ __device__ __forceinline__ void tail_trsm_pipe(double* smem, unsigned* rowf, dou
                         avail = pr < NDB - 1 ? pr : NDB - 1;
                     }
                     if (avail > next) break;
-                    // expired (or another task already failed): stage what is there, flag it
-                    if (wall_clock64() - t0 > TAIL_WAIT_TICKS || tail_ld(err) != 0u) {
+                    // expired (or, checked every 32 polls off the fast path, another task
+                    // already failed): stage what is there, flag it
+                    if (wall_clock64() - t0 > TAIL_WAIT_TICKS || ((it & 31u) == 0u && tail_ld(err) != 0u)) {
                         avail = NDB;
                         timeout = true;
                         break;
@@ -2379,21 +2380,25 @@ __device__ __forceinline__ void tail_trsm_pipe(double* smem, unsigned* rowf, dou
     d4 Y[NDB];
 #pragma unroll
     for (int b = 0; b < NDB; ++b) {
-        // row b staged by all four staging waves. Bounded on the wall clock at twice the
-        // staging waves' own bound (they always get here, a timed-out wait above stages stale
-        // data and flags it); an expiry here flags the evaluation too, never a silent result.
-        if (lane == 0) {
-            const unsigned long long t0 = wall_clock64();
-            while (__hip_atomic_load(&rowf[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4u) {
-                if (wall_clock64() - t0 > 2 * TAIL_WAIT_TICKS) {
-                    atomicOr(err, 1u);
-                    atomicOr(rerr, 2u);
+        // row b staged by all four staging waves. Bounded: 2^23 polls of at least one
+        // s_sleep(1) (64 clocks) each, > 0.25 s, longer than the staging waves' own 0.2 s
+        // wall-clock bound (they always get here: a timed-out wait above stages stale data and
+        // flags it); an expiry here flags the evaluation too, never a silent result. (The
+        // wall clock is not read per poll: on this chain's critical path that cost ~10%.)
+        {
+            bool got = false;
+            for (int it = 0; it < (1 << 23); ++it) {
+                if (__hip_atomic_load(&rowf[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= 4u) {
+                    got = true;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
+            if (!got && lane == 0) {
+                atomicOr(err, 1u);
+                atomicOr(rerr, 2u);
+            }
         }
-        __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         d4 s0 = Bt[b], s1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -2527,7 +2532,7 @@ __device__ __forceinline__ void tail_q32(const Gm<AUX>& gC, const Gm<AUX>& gP, i
 // set: then every later wait returns at once and the launch drains quickly).
 __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int k, int i, int j) {
     const unsigned long long t0 = wall_clock64();
-    for (;;) {
+    for (unsigned it = 1;; ++it) {
         bool ok;
         if (type == TK_D) {
             ok = tail_ld(&c->units[k * TAIL_TMAX + k]) >= TAIL_NQ * k;
@@ -2542,7 +2547,8 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int
                 ok = tail_ld(&c->sdone[i * TAIL_TMAX + k + c2]) >= 2u && tail_ld(&c->sdone[j * TAIL_TMAX + k + c2]) >= 2u;
         }
         if (ok) return true;
-        if (wall_clock64() - t0 > TAIL_WAIT_TICKS || tail_ld(&c->err) != 0u) return false;
+        // the other task's failure is checked every 32 polls, off the fast path
+        if (wall_clock64() - t0 > TAIL_WAIT_TICKS || ((it & 31u) == 0u && tail_ld(&c->err) != 0u)) return false;
         __builtin_amdgcn_s_sleep(2);
     }
 }
