@@ -2581,7 +2581,8 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         if (a.trace && threadIdx.x == 0) a.trace[3 * tk + 1] = wall_clock64();
         const int gk = a.ts + k;
         double* colk = A + (int64_t)gk * NB * a.lda;
-        const bool faulted = type == TK_D && k == a.fault;  // debug (GAPLAC_TAIL_FAULT): never runs nor publishes
+        // debug (GAPLAC_TAIL_FAULT): D(fault) never runs nor publishes
+        const bool faulted = type == TK_D && k == a.fault;
         if (faulted) {
         } else if (type == TK_D) {
             if ((int64_t)gk * NB < a.N)
