@@ -26,7 +26,9 @@ struct gaplac_ctx {
     int device = 0;
     hipStream_t s_main = nullptr, s_panel = nullptr;
     hipStream_t s_extra = nullptr;  // extra rows (gradient / posterior), beside the bulk updates
+    hipStream_t s_xrest = nullptr;  // extra rows: their updates beyond the next SP
     hipEvent_t ev_xinit = nullptr, ev_xdone = nullptr;
+    hipEvent_t ev_xc[2] = {}, ev_xr[2] = {};  // extra rows: SP chain done (s_extra), SP rest done (s_xrest)
     hipEvent_t ev_P[2] = {}, ev_R[2] = {}, ev_gram = nullptr, ev_gram2 = nullptr;
     double* A = nullptr;
     size_t A_elems = 0;
@@ -416,11 +418,14 @@ int factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, i
 // Identity rows (gradient): only rows E <= c of column c are nonzero (Y = L^{-T} is upper
 // triangular), so each step touches rows [0, c] / [0, end of SP); tiles below Y's diagonal
 // stay exactly zero and are never written. Cross-covariance rows (posterior): all rows.
-void extra_rows_step(gaplac_ctx* ctx, hipStream_t sm, int64_t lda, int nt, int p) {
+// extra-row updates of at least this many tiles run as whole 128x128 tiles (tile_syrk_kernel),
+// not quadrants: gradient 79.4 -> 78.0 ms with the split below (profiles/r04r_xr_ab.txt)
+constexpr int XR_TILE_MIN = 128;
+
+static void extra_rows_chain(gaplac_ctx* ctx, hipStream_t sm, int64_t lda, int nt, int c0, int c1) {
     const int W = ctx->spw;
     const bool tri = ctx->xr_mode == 1;
     const int mt = ctx->xr_tiles;
-    const int c0 = W * p, c1 = std::min(W * p + W, nt);
     for (int c = c0; c < c1; ++c) {
         double* Acol = ctx->A + (int64_t)c * NB * lda;
         if (c > c0) {
@@ -428,18 +433,24 @@ void extra_rows_step(gaplac_ctx* ctx, hipStream_t sm, int64_t lda, int nt, int p
             BulkArgs ba{ctx->A, lda, Panel{Acol - NB * lda, lda, 0}, nullptr, rows * (c1 - c), NB, nt, c,
                         ColMap{1, 0, W}};
             ba.rect_rows = rows;
+            ba.tile_min = XR_TILE_MIN;
             launch_bulk(sm, ba, slot(ctx, 7, 0));
         }
         launch_trsm_rows(sm, Acol, lda, c, nt, tri ? c + 1 : mt, ctx->Dinv + (size_t)c * DINV_PER_BLOCK,
                          slot(ctx, 7, 0));
     }
-    if (c1 < nt) {
-        const int rows = tri ? c1 : mt;
-        BulkArgs ba{ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nullptr, rows * (nt - c1),
-                    (c1 - c0) * NB, nt, c1, ColMap{1, 0, W}};
-        ba.rect_rows = rows;
-        launch_bulk(sm, ba, slot(ctx, 7, 0));
-    }
+}
+
+// SP [c0, c1)'s extra-row tiles applied to tile columns [jb, je) of the extra rows (K = 128 W)
+static void extra_rows_update(gaplac_ctx* ctx, hipStream_t sm, int64_t lda, int nt, int c0, int c1, int jb,
+                              int je) {
+    if (je <= jb) return;
+    const int rows = ctx->xr_mode == 1 ? c1 : ctx->xr_tiles;
+    BulkArgs ba{ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nullptr, rows * (je - jb),
+                (c1 - c0) * NB, nt, jb, ColMap{1, 0, ctx->spw}};
+    ba.rect_rows = rows;
+    ba.tile_min = XR_TILE_MIN;
+    launch_bulk(sm, ba, slot(ctx, 7, 0));
 }
 
 // Super-panel boundaries: tile columns sp[p] .. sp[p+1]-1 form SP p, width spw. With a
@@ -601,11 +612,31 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             HIPQ(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
         }
         if (ctx->xr_mode) {
-            // extra rows on their own stream: they only need SP p final (P(p)) and touch
-            // rows no other stream writes, so they fill the bulk stream's idle time
+            // extra rows: they only need SP p final (P(p)) and touch rows no other stream
+            // writes. s_extra takes SP p's column chain and then its update of SP p+1's
+            // columns; the update of the columns after those (the bulk of the K = 128 W work)
+            // goes on s_xrest, so the chain of SP p+1 runs beside it instead of after it
+            // (DESIGN.md §9). Every tile still gets the SPs in order: the update of SP p+1's
+            // columns waits for SP p-1's update of the columns after SP p, SP p's chain for
+            // SP p-2's.
             hipStream_t sx = ctx->serial ? sm : ctx->s_extra;
-            if (sx != sm) HIPQ(ctx, hipStreamWaitEvent(sx, ctx->ev_P[p & 1], 0));
-            extra_rows_step(ctx, sx, lda, nt, p);
+            if (sx == sm) {
+                extra_rows_chain(ctx, sx, lda, nt, c0, c1);
+                extra_rows_update(ctx, sx, lda, nt, c0, c1, c1, nt);
+            } else {
+                hipStream_t sr = ctx->s_xrest;
+                if (p >= 1) {  // SP p-1 on the columns after SP p
+                    HIPQ(ctx, hipStreamWaitEvent(sr, ctx->ev_xc[(p - 1) & 1], 0));
+                    extra_rows_update(ctx, sr, lda, nt, spc[(size_t)p - 1], c0, c1, nt);
+                    HIPQ(ctx, hipEventRecord(ctx->ev_xr[(p - 1) & 1], sr));
+                }
+                HIPQ(ctx, hipStreamWaitEvent(sx, ctx->ev_P[p & 1], 0));
+                if (p >= 2) HIPQ(ctx, hipStreamWaitEvent(sx, ctx->ev_xr[(p - 2) & 1], 0));
+                extra_rows_chain(ctx, sx, lda, nt, c0, c1);
+                HIPQ(ctx, hipEventRecord(ctx->ev_xc[p & 1], sx));
+                if (p >= 1) HIPQ(ctx, hipStreamWaitEvent(sx, ctx->ev_xr[(p - 1) & 1], 0));
+                extra_rows_update(ctx, sx, lda, nt, c0, c1, c1, p + 2 <= nsp ? spc[(size_t)p + 2] : nt);
+            }
         }
     }
     if (spc[(size_t)nsp] < nt) {
@@ -647,6 +678,8 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     }
     if (ctx->xr_mode && !ctx->serial) {
         HIPQ(ctx, hipEventRecord(ctx->ev_xdone, ctx->s_extra));
+        HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_xdone, 0));
+        HIPQ(ctx, hipEventRecord(ctx->ev_xdone, ctx->s_xrest));
         HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_xdone, 0));
     }
     launch_reduce(sm, ctx->A, lda, N, (int64_t)nt * NB, ColMap{1, 0, 1}, ctx->dres);
@@ -795,6 +828,7 @@ int ensure_workspace(gaplac_ctx* ctx, int64_t N) {
         int least = 0, greatest = 0;
         HIPCK(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
         HIPCK(ctx, hipStreamCreateWithPriority(&ctx->s_extra, hipStreamNonBlocking, least));
+        HIPCK(ctx, hipStreamCreateWithPriority(&ctx->s_xrest, hipStreamNonBlocking, least));
     }
     if (ctx->xr_mode == 2) {
         const size_t M = (size_t)ctx->xr_M;
@@ -1230,6 +1264,10 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
             return fail("event", e);
         if ((e = hipEventCreateWithFlags(&ctx->ev_R[q], hipEventDisableTiming)) != hipSuccess)
             return fail("event", e);
+        if ((e = hipEventCreateWithFlags(&ctx->ev_xc[q], hipEventDisableTiming)) != hipSuccess)
+            return fail("event", e);
+        if ((e = hipEventCreateWithFlags(&ctx->ev_xr[q], hipEventDisableTiming)) != hipSuccess)
+            return fail("event", e);
     }
     if ((e = hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming)) != hipSuccess)
         return fail("event", e);
@@ -1266,6 +1304,7 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     if (ctx->s_main) (void)hipStreamSynchronize(ctx->s_main);
     if (ctx->s_panel) (void)hipStreamSynchronize(ctx->s_panel);
     if (ctx->s_extra) (void)hipStreamSynchronize(ctx->s_extra);
+    if (ctx->s_xrest) (void)hipStreamSynchronize(ctx->s_xrest);
     for (gaplac_ctx* c : ctx->lanes) gaplac_ctx_destroy(c);
     ctx->lanes.clear();
     if (ctx->borrowed_inputs) {
@@ -1275,6 +1314,8 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     for (int q = 0; q < 2; ++q) {
         if (ctx->ev_P[q]) (void)hipEventDestroy(ctx->ev_P[q]);
         if (ctx->ev_R[q]) (void)hipEventDestroy(ctx->ev_R[q]);
+        if (ctx->ev_xc[q]) (void)hipEventDestroy(ctx->ev_xc[q]);
+        if (ctx->ev_xr[q]) (void)hipEventDestroy(ctx->ev_xr[q]);
     }
     if (ctx->ev_gram) (void)hipEventDestroy(ctx->ev_gram);
     if (ctx->ev_gram2) (void)hipEventDestroy(ctx->ev_gram2);
@@ -1322,6 +1363,7 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     if (ctx->s_main) (void)hipStreamDestroy(ctx->s_main);
     if (ctx->s_panel) (void)hipStreamDestroy(ctx->s_panel);
     if (ctx->s_extra) (void)hipStreamDestroy(ctx->s_extra);
+    if (ctx->s_xrest) (void)hipStreamDestroy(ctx->s_xrest);
     delete ctx;
     return 0;
 }
@@ -1332,6 +1374,7 @@ int gaplac_ctx_release(gaplac_ctx* ctx) {
     HIPCK(ctx, hipStreamSynchronize(ctx->s_main));
     HIPCK(ctx, hipStreamSynchronize(ctx->s_panel));
     if (ctx->s_extra) HIPCK(ctx, hipStreamSynchronize(ctx->s_extra));
+    if (ctx->s_xrest) HIPCK(ctx, hipStreamSynchronize(ctx->s_xrest));
     for (gaplac_ctx* c : ctx->lanes) gaplac_ctx_destroy(c);
     ctx->lanes.clear();
     auto drop = [](double*& p, size_t& n) {
@@ -1503,6 +1546,7 @@ int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D, 
             (void)hipStreamSynchronize(c->s_main);
             (void)hipStreamSynchronize(c->s_panel);
             if (c->s_extra) (void)hipStreamSynchronize(c->s_extra);
+            if (c->s_xrest) (void)hipStreamSynchronize(c->s_xrest);
         }
         return code;
     };

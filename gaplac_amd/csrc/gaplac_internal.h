@@ -79,6 +79,7 @@ struct BulkArgs {
     int rect_rows = 0;
     int max_r = -1, max_c = -1;  // largest lo16 / hi16 list entry (-1: an m x m triangle list)
     int whole = 0;    // 1: a band list as 128x128 tile workgroups (tile_band_kernel), never quadrants
+    int tile_min = 0;  // > 0: at least this many tiles go to tile_syrk_kernel even below the quadrant limit
 };
 
 // Persistent tail (gaplac_kernels.hip tail_kernel): completion counters of

@@ -2964,7 +2964,7 @@ void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt) {
     }
     if (!guard_launch("bulk update", a.C, 0, tiles_end(a.ldc, a.bi0 + max_r, a.lj0 + max_c))) return;
     const int grid = ((a.ntiles + 7) >> 3) << 3;
-    if (syrk_is_small(a.ntiles) && !a.whole)
+    if (syrk_is_small(a.ntiles) && !a.whole && !(a.tile_min > 0 && a.ntiles >= a.tile_min))
         quad_bulk_kernel<<<dim3((unsigned)(4 * grid)), dim3(256), 0, s>>>(a, kt);
     else if (a.whole)
         tile_band_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
