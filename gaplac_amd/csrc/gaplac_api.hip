@@ -79,7 +79,7 @@ struct gaplac_ctx {
     TailCtl* tctl = nullptr;     // its completion counters (zeroed per launch)
     uint32_t* ttasks = nullptr;  // its task list for ttasks_T tile columns
     size_t ttasks_elems = 0;
-    int ttasks_T = -1, ttasks_n = 0;
+    int ttasks_T = -1, ttasks_X = 0, ttasks_n = 0;
     std::string ttrace_path;     // GAPLAC_TAIL_TRACE: append per-task times of every tail launch here
     int tail_fault = -1;         // GAPLAC_TAIL_FAULT (tests only): skip this tail column's diagonal block
     unsigned long long* ttrace = nullptr;
@@ -458,9 +458,16 @@ static void extra_rows_update(gaplac_ctx* ctx, hipStream_t sm, int64_t lda, int 
 // most tail_s tile columns after it; those columns are factored by serial_tail().
 // The whole matrix in the persistent tail (no super-panels): plain logpdf with at most
 // tail_s (and TAIL_TMAX) tile columns.
+// Which evaluations take a tail: plain logpdf, and the posterior when its cross-covariance
+// rows fit beside the tail's columns (the persistent tail factors them along, §10); the
+// gradient's identity rows (one per column) never do.
+static bool tail_allowed(const gaplac_ctx* ctx) {
+    return ctx->xr_mode == 0 || (ctx->xr_mode == 2 && ctx->tailk && ctx->tail_s > 0 &&
+                                 ctx->xr_tiles + std::min(ctx->tail_s, TAIL_TMAX) <= TAIL_TMAX);
+}
+
 static bool whole_in_tail(const gaplac_ctx* ctx, int nt) {
-    return ctx->xr_mode == 0 && ctx->tailk && ctx->tail_s > 0 && nt <= TAIL_TMAX &&
-           nt <= ctx->tail_s;
+    return tail_allowed(ctx) && ctx->tailk && ctx->tail_s > 0 && nt <= TAIL_TMAX && nt <= ctx->tail_s;
 }
 
 static std::vector<int> superpanel_starts(const gaplac_ctx* ctx, int nt) {
@@ -470,7 +477,7 @@ static std::vector<int> superpanel_starts(const gaplac_ctx* ctx, int nt) {
     if (whole_in_tail(ctx, nt)) return sp;
     int c = 0;
     while (c < nt) {
-        if (ctx->xr_mode == 0 && ctx->tail_s > 0 && c > 0 && nt - c <= ctx->tail_s) break;
+        if (tail_allowed(ctx) && ctx->tail_s > 0 && c > 0 && nt - c <= ctx->tail_s) break;
         c = std::min(c + ctx->spw, nt);
         sp.push_back(c);
     }
@@ -641,27 +648,38 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     }
     if (spc[(size_t)nsp] < nt) {
         const int ts = spc[(size_t)nsp], T = nt - ts;
-        if (ctx->tailk && T <= TAIL_TMAX) {
+        // the posterior's cross-covariance rows: factored along inside the tail
+        const int X = ctx->xr_mode == 2 ? ctx->xr_tiles : 0;
+        if (ctx->tailk && T + X <= TAIL_TMAX && (ctx->xr_mode == 0 || X > 0)) {
             // the tail as one persistent dataflow launch
+            if (ctx->xr_mode && !ctx->serial) {
+                // the extra rows' super-panel updates of the tail's columns land first
+                HIPQ(ctx, hipEventRecord(ctx->ev_xdone, ctx->s_extra));
+                HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_xdone, 0));
+                HIPQ(ctx, hipEventRecord(ctx->ev_xdone, ctx->s_xrest));
+                HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_xdone, 0));
+            }
             if (ctx->dry) {  // gaplac_plan_check: the task list's dependency order
                 std::vector<uint32_t> host;
-                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP);
+                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X);
                 std::string why;
-                if (!check_tail_tasks(T, host, &why)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
+                if (!check_tail_tasks(T, host, &why, X)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
             }
-            if (ctx->ttasks_T != T && !ctx->dry) {
+            if ((ctx->ttasks_T != T || ctx->ttasks_X != X) && !ctx->dry) {
                 std::vector<uint32_t> host;
-                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP);
+                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X);
                 int rc;
                 if ((rc = ensure(ctx, &ctx->ttasks, &ctx->ttasks_elems, host.size()))) return rc;
                 HIPCK(ctx, hipMemcpy(ctx->ttasks, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
                 ctx->ttasks_T = T;
+                ctx->ttasks_X = X;
                 ctx->ttasks_n = (int)host.size();
             }
             if (!ctx->tctl && !ctx->dry)
                 HIPCK(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->tctl), sizeof(TailCtl)));
             HIPQ(ctx, hipMemsetAsync(ctx->tctl, 0, sizeof(TailCtl), sm));
-            const int nts = ctx->dry ? (int)(T * (T + 1) * (T + 2) / 6 + 3 * T * T) : ctx->ttasks_n;
+            const int nts = ctx->dry ? (int)(T * (T + 1) * (T + 2) / 6 + 3 * T * T + X * T * (T + 3) / 2)
+                                     : ctx->ttasks_n;
             if (!ctx->ttrace_path.empty() && !ctx->dry) {
                 int rc;
                 if ((rc = ensure(ctx, &ctx->ttrace, &ctx->ttrace_elems, 3 * (size_t)nts))) return rc;
@@ -669,6 +687,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             TailArgs ta{ctx->A, lda, N, ts, T, ctx->Dinv, ctx->dres, ctx->tctl, ctx->ttasks, nts,
                         ctx->ttrace_path.empty() ? nullptr : ctx->ttrace};
             ta.fault = ctx->tail_fault;
+            ta.xrows = X;
             // batch lanes run their tails side by side: each persistent grid takes its share
             // of the CUs (one tail workgroup fills a CU's LDS), so no tail waits for another
             launch_tail(sm, ta, std::min(std::max(1, ctx->ncu / std::max(1, ctx->tail_share)), nts), slot(ctx, 10, 0));

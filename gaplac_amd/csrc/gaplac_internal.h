@@ -112,6 +112,7 @@ struct TailArgs {
     // fault is skipped, never publishing, so every wait behind it expires and the evaluation
     // must come back as GAPLAC_E_HIP; -1 = off
     int fault = -1;
+    int xrows = 0;  // extra tile rows below the matrix factored along (tile rows ts+T .. ts+T+xrows-1)
 };
 constexpr int TAIL_MODEL_SHIFT = 27;
 constexpr int TAIL_MAX_MODELS = 32;
@@ -123,8 +124,11 @@ constexpr int TAIL_MAX_MODELS = 32;
 // quad_last columns the TRSMs are whole-tile tasks after the diagonal block, not two row
 // halves pipelined behind it; group (1, 2 or 4): near tiles take that many columns per
 // task (K = 128 group) where the chain allows.
+// xrows > 0: xrows extra tile rows below the matrix (relative rows T .. T+xrows-1, the
+// posterior's cross-covariance rows) factored along: whole-tile TRSMs and updates only.
 void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart = nullptr, int gw = 4,
-                      int near = 4, int quad_last = TAIL_TMAX, bool whole_trsm = false, int group = 1);
+                      int near = 4, int quad_last = TAIL_TMAX, bool whole_trsm = false, int group = 1,
+                      int xrows = 0);
 // B models' task lists interleaved (each model's own order kept, so the result is a
 // topological order per model). lag = 0: task by task, all models in step. lag > 0: a
 // software pipeline: model m runs lag * m tile columns behind model 0, and the tasks of the
@@ -132,7 +136,7 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
 void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<size_t>& colstart, int B, int lag,
                            std::vector<uint32_t>& out);
 // The list is a topological order of the tail's dataflow that applies every update once.
-bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why);
+bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why, int xrows = 0);
 void launch_tail(hipStream_t s, const TailArgs& a, int grid, KTime* kt);
 
 // Host-side footprint guard. Before launching, every launcher computes the

@@ -2686,7 +2686,7 @@ void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<s
 // Single evaluations use GW = 4, NEAR = 4 (latency); batched launches fewer per-column
 // updates (throughput).
 void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart, int gw, int near,
-                      int quad_last, bool whole_trsm, int group) {
+                      int quad_last, bool whole_trsm, int group, int xrows) {
     group = group >= 4 ? 4 : group >= 2 ? 2 : 1;  // divides the deep width (4 or 8): groups stay in a block
     // deep width; near distance (>= 2: the next two diagonal tiles take per-column Q tasks)
     const int GW = gw == 8 ? 8 : 4, NEAR = std::max(2, near);
@@ -2718,6 +2718,31 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
     auto deep_block = [&](int b) { return GW * b + GW - 1 <= T - 2; };
     auto far_from = [&](int b) { return GW * b + GW + NEAR; };  // first far tile column
     std::vector<std::vector<uint32_t>> later((size_t)std::max(T, 1));  // spread deep tasks per column
+    // Extra rows (xrows > 0), off the chain, at the end of column g's list: their whole-tile
+    // TRSMs with column g, column g's update of their tiles in the rest of g's block of 4
+    // columns, and at the block's last column ONE K = 512 task per extra tile right of the
+    // block (those of the next block at once, the rest spread over the next 4 columns'
+    // lists: always before the TRSM of the tile that needs them). The last block, if not
+    // followed by a whole block, takes per-column updates throughout.
+    auto xcol = [&](int g) {
+        if (xrows <= 0) return;
+        const int k0 = g - g % 4;
+        const bool deep = k0 + 4 <= T - 1;  // a tile column right of the block exists
+        const int jend = deep ? k0 + 4 : T;
+        for (int e = T; e < T + xrows; ++e) out.push_back(tail_enc(TK_S, TAIL_S_WHOLE, g, e, 0));
+        for (int e = T; e < T + xrows; ++e)
+            for (int j = g + 1; j < jend; ++j) out.push_back(tail_enc(TK_U, 0, g, e, j));
+        if (deep && g == k0 + 3) {
+            std::vector<uint32_t> rest;
+            for (int j = k0 + 4; j < T; ++j)
+                for (int e = T; e < T + xrows; ++e) (j < k0 + 8 ? out : rest).push_back(tail_enc(TK_U, TAIL_UD, k0, e, j));
+            const size_t n = rest.size();
+            for (size_t x = 0; x < n; ++x) {
+                const int col = g + 1 + (int)(x * 4 / std::max<size_t>(n, 1));
+                later[(size_t)std::min(col, T - 2)].push_back(rest[x]);
+            }
+        }
+    };
     out.push_back(tail_enc(TK_D, 0, 0, 0, 0));
     S(1, 0);
     for (int g = 0; g + 1 < T; ++g) {
@@ -2763,15 +2788,18 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
                 later[(size_t)std::min(col, T - 2)].push_back(rest[x]);
             }
         }
+        xcol(g);
     }
+    xcol(T - 1);
 }
 
 // Host check of a task list (gaplac_plan_check's dry walk): run the tasks one at a time in
 // list order, each only once its wait condition (tail_wait) holds on the tasks before it,
 // i.e. the list is a topological order of the dataflow, and at the end every tile has
 // received every column's update exactly once, every TRSM and diagonal block has run.
-bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why) {
-    std::vector<unsigned> units((size_t)T * T, 0), sdone((size_t)T * T, 0), ddone((size_t)T, 0);
+bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why, int xrows) {
+    const int R = T + xrows;  // tile rows (the extra rows below the matrix: TRSMs and updates only)
+    std::vector<unsigned> units((size_t)R * T, 0), sdone((size_t)R * T, 0), ddone((size_t)T, 0);
     auto fail = [&](size_t n, const char* what) {
         char b[160];
         std::snprintf(b, sizeof b, "tail task %zu of %zu (T = %d): %s", n, list.size(), T, what);
@@ -2783,6 +2811,8 @@ bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why
         const int type = (int)(e & 3u), q = (int)((e >> 2) & 15u), k = (int)((e >> 6) & 127u);
         const int i = (int)((e >> 13) & 127u), j = (int)((e >> 20) & 127u);
         const unsigned whole = i == j ? TAIL_NQ : 4u;
+        if (k >= T || i >= R || j >= T || (i >= T && (type == TK_D || type == TK_Q)))
+            return fail(n, "task outside the tile range");
         if (type == TK_D) {
             if (units[(size_t)k * T + k] != TAIL_NQ * (unsigned)k) return fail(n, "D before its tile is updated");
             ddone[(size_t)k] += 1;
@@ -2806,7 +2836,7 @@ bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why
     }
     for (int j = 0; j < T; ++j) {
         if (ddone[(size_t)j] != 1u) return fail(list.size(), "a diagonal block missing or repeated");
-        for (int i = j; i < T; ++i) {
+        for (int i = j; i < R; ++i) {
             const unsigned whole = i == j ? TAIL_NQ : 4u;
             if (units[(size_t)i * T + j] != whole * (unsigned)j) return fail(list.size(), "a tile missed an update");
             if (i > j && sdone[(size_t)i * T + j] != 2u) return fail(list.size(), "a TRSM missing or repeated");
@@ -3106,7 +3136,7 @@ void launch_tail(hipStream_t s, const TailArgs& a, int grid, KTime* kt) {
     if (a.ntasks <= 0 || a.T <= 0) return;
     if (a.nmodels < 1 || a.nmodels > TAIL_MAX_MODELS ||
         !guard_launch("tail_kernel", a.A, 0,
-                      (int64_t)(a.nmodels - 1) * a.a_stride + tiles_end(a.lda, a.ts + a.T - 1, a.ts + a.T - 1)))
+                      (int64_t)(a.nmodels - 1) * a.a_stride + tiles_end(a.lda, a.ts + a.T + a.xrows - 1, a.ts + a.T - 1)))
         return;
     tail_kernel<<<dim3((unsigned)grid), dim3(512), 0, s>>>(a, kt);
 }

@@ -26,7 +26,7 @@ def plan(N, mode, M=0, spw=4):
 
 
 @pytest.mark.parametrize("spw", [1, 2, 4, 5, 8])
-@pytest.mark.parametrize("mode,M", [(0, 0), (1, 0), (2, 1), (2, 130), (2, 1000)])
+@pytest.mark.parametrize("mode,M", [(0, 0), (1, 0), (2, 1), (2, 130), (2, 1000), (2, 6016), (2, 6200)])
 def test_every_launch_inside_the_workspace(mode, M, spw):
     for N in SIZES:
         if mode == 1 and N > 16384:
@@ -44,6 +44,11 @@ def test_launch_counts_follow_the_schedule():
     assert v0 == 0 and 49 * 3 < l0 < 49 * 6 + 10
     l1, _, _ = plan(16384, 1)
     assert l1 > l0  # the gradient adds the identity-row launches and the C^-1 tiles
+    # the posterior's cross-covariance rows ride in the same tail while they fit beside its
+    # 80 columns (M <= 48 tile rows): the super-panel phase's extra-row launches only
+    l2, v2, _ = plan(16384, 2, M=1024)
+    l3, v3, _ = plan(16384, 2, M=48 * 128 + 1)  # 49 tile rows: no tail, every column a super-panel
+    assert v2 == v3 == 0 and l0 < l2 < l3
 
 
 @pytest.mark.parametrize("N", [1, 127, 128, 129, 254, 255, 300, 4096])
