@@ -1358,6 +1358,9 @@ __global__ __launch_bounds__(256) void trsm_subst_kernel(
 #ifndef GAPLAC_KB
 #define GAPLAC_KB 16
 #endif
+#ifndef GAPLAC_BULK_DMA
+#define GAPLAC_BULK_DMA 0
+#endif
 constexpr int KB = GAPLAC_KB;  // k-chunk staged in LDS (8 or 16)
 static_assert(KB == 8 || KB == 16, "k-chunk of the tile kernels: 8 or 16");
 constexpr int LR = NB + 16;  // LDS k-row stride: lanes 16..31 land on banks 32..63
@@ -1440,6 +1443,46 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
     } while (0)
 
     const int NCH = kdepth / KB;
+#if GAPLAC_BULK_DMA
+    // LDS-DMA staging (A/B variant): P and Q rows straight into LDS (global_load_lds, 16 B
+    // per lane, one 128-row column segment per instruction), P unnegated and negated by the
+    // MFMA's B-operand neg modifier; no staging registers, no LDS stores in the MFMA stream.
+    (void)Pr; (void)Qr; (void)s4; (void)krow;
+    auto issue = [&](int ch, int buf) {
+#pragma unroll
+        for (int it = 0; it < 2 * KB / 4; ++it) {
+            const int t = w + 4 * it, o = t / KB, r = t % KB;
+            const double* src = (o ? Q : P) + (int64_t)(ch * KB + r) * ldp + 2 * lane;
+            __builtin_amdgcn_global_load_lds((GlobalCPtr)src, (LdsPtr)&sm[buf][o][r][0], 16, 0, 0);
+        }
+    };
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ch = 0; ch < NCH; ++ch) {
+        const int buf = ch & 1;
+        if (ch + 1 < NCH) issue(ch + 1, buf ^ 1);
+        if (active) {
+#pragma unroll
+            for (int ks = 0; ks < KB; ks += 4) {
+                double fa[4], fb[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    fa[m] = sm[buf][1][ks + fr][64 * wj + 16 * m + fc];
+                    fb[m] = sm[buf][0][ks + fr][64 * wi + 16 * m + fc];
+                }
+#pragma unroll
+                for (int mj = 0; mj < 4; ++mj)
+#pragma unroll
+                    for (int mi = 0; mi < 4; ++mi)
+                        acc[mi][mj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mj], fb[mi], acc[mi][mj], 0, 0, 2);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    return;
+#endif
     GAPLAC_GLOAD(0);
     GAPLAC_LSTORE(0);
     __syncthreads();
