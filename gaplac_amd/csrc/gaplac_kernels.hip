@@ -1343,12 +1343,12 @@ __global__ __launch_bounds__(256) void trsm_subst_kernel(
 //   C(bi, bj) -= P_bi P_bj^T,   P = the kdepth panel columns (Panel operand),
 // with C tile (bi, bj) stored in local tile column lj (ColMap: bj = cm.global(lj)).
 // 4 waves as 2x2, each wave a 64x64 sub-tile = 4x4 v_mfma_f64_16x16x4f64 accumulators.
-// Operands are staged through LDS in 16-deep k-chunks, double-buffered with a register
-// prefetch of the next chunk. The MFMA computes D = Q*P^T (the j-side fragment is the A
-// operand) so that a lane's accumulator column is C's row: stores are 128-byte column
-// segments of the column-major matrix. The C tile is loaded straight into the
-// accumulators before the k-loop and P is staged negated, so the MFMA chain produces
-// C - P Q^T and the epilogue is stores only.
+// Operands are staged through LDS in 16-deep k-chunks by LDS-DMA, double-buffered (the
+// next chunk in flight while the current one is multiplied). The MFMA computes D = Q*P^T
+// (the j-side fragment is the A operand) so that a lane's accumulator column is C's row:
+// stores are 128-byte column segments of the column-major matrix. The C tile is loaded
+// straight into the accumulators before the k-loop and the MFMA negates P (neg modifier),
+// so the chain produces C - P Q^T and the epilogue is stores only.
 // Tile placement: a precomputed list maps blockIdx -> (bi, lj) = (bi0 + lo16, lj0 + hi16).
 // The list is ordered so that the blocks one XCD runs (blockIdx % 8, dealt round-robin by
 // the dispatcher) walk one contiguous run of 8x8 super-tiles: the panel row blocks of its
@@ -1357,9 +1357,6 @@ __global__ __launch_bounds__(256) void trsm_subst_kernel(
 // ---------------------------------------------------------------------------------
 #ifndef GAPLAC_KB
 #define GAPLAC_KB 16
-#endif
-#ifndef GAPLAC_BULK_DMA
-#define GAPLAC_BULK_DMA 0
 #endif
 constexpr int KB = GAPLAC_KB;  // k-chunk staged in LDS (8 or 16)
 static_assert(KB == 8 || KB == 16, "k-chunk of the tile kernels: 8 or 16");
@@ -1406,48 +1403,13 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
     const int lane = tid & 63, w = tid >> 6;
     const int wi = w & 1, wj = w >> 1;
     const int fr = lane >> 4, fc = lane & 15;
-    // staging: thread -> (k row krow + 4 it, rows 2 lane, 2 lane + 1) of both operands
-    const int krow = tid >> 6;  // 0..3
-    const double* Pr = P + (int64_t)krow * ldp + 2 * lane;
-    const double* Qr = Q + (int64_t)krow * ldp + 2 * lane;
-    const int64_t s4 = 4 * ldp;
-    double2 p0, p1, p2, p3, q0, q1, q2, q3;
-#define GAPLAC_GLOAD(ch)                                                               \
-    do {                                                                               \
-        const int64_t o_ = (int64_t)(ch) * KB * ldp;                                   \
-        p0 = *reinterpret_cast<const double2*>(Pr + o_);                               \
-        p1 = *reinterpret_cast<const double2*>(Pr + o_ + s4);                          \
-        q0 = *reinterpret_cast<const double2*>(Qr + o_);                               \
-        q1 = *reinterpret_cast<const double2*>(Qr + o_ + s4);                          \
-        if constexpr (KB == 16) {                                                      \
-            p2 = *reinterpret_cast<const double2*>(Pr + o_ + 2 * s4);                  \
-            p3 = *reinterpret_cast<const double2*>(Pr + o_ + 3 * s4);                  \
-            q2 = *reinterpret_cast<const double2*>(Qr + o_ + 2 * s4);                  \
-            q3 = *reinterpret_cast<const double2*>(Qr + o_ + 3 * s4);                  \
-        }                                                                              \
-    } while (0)
-#define GAPLAC_LSTORE(buf)                                                             \
-    do {                                                                               \
-        double* sp_ = &sm[buf][0][krow][2 * lane];                                     \
-        double* sq_ = &sm[buf][1][krow][2 * lane];                                     \
-        *reinterpret_cast<double2*>(sp_) = make_double2(-p0.x, -p0.y);                 \
-        *reinterpret_cast<double2*>(sp_ + 4 * LR) = make_double2(-p1.x, -p1.y);        \
-        *reinterpret_cast<double2*>(sq_) = q0;                                         \
-        *reinterpret_cast<double2*>(sq_ + 4 * LR) = q1;                                \
-        if constexpr (KB == 16) {                                                      \
-            *reinterpret_cast<double2*>(sp_ + 8 * LR) = make_double2(-p2.x, -p2.y);    \
-            *reinterpret_cast<double2*>(sp_ + 12 * LR) = make_double2(-p3.x, -p3.y);   \
-            *reinterpret_cast<double2*>(sq_ + 8 * LR) = q2;                            \
-            *reinterpret_cast<double2*>(sq_ + 12 * LR) = q3;                           \
-        }                                                                              \
-    } while (0)
-
-    const int NCH = kdepth / KB;
-#if GAPLAC_BULK_DMA
-    // LDS-DMA staging (A/B variant): P and Q rows straight into LDS (global_load_lds, 16 B
-    // per lane, one 128-row column segment per instruction), P unnegated and negated by the
-    // MFMA's B-operand neg modifier; no staging registers, no LDS stores in the MFMA stream.
-    (void)Pr; (void)Qr; (void)s4; (void)krow;
+    // LDS-DMA staging: the chunk's 2 KB rows (KB panel columns of P, then of Q: 128 contiguous
+    // rows each) go straight into LDS, one global_load_lds (16 B per lane) per row, wave w
+    // taking rows w, w + 4, ...; no staging registers and no LDS stores in the MFMA stream.
+    // P stays unnegated in LDS: the MFMA's B-operand neg modifier (blgp = 2 on f64 MFMA)
+    // makes the chain C - P Q^T, bitwise what staging -P gave (register-staged version: 208
+    // VGPRs, 0.794 / 0.833 of peak at the 16k / 64k shapes alone; this one 189 VGPRs, 0.819 /
+    // 0.852, tools/bulk_probe.hip, profiles/r04y_bulk_probe.txt).
     auto issue = [&](int ch, int buf) {
 #pragma unroll
         for (int it = 0; it < 2 * KB / 4; ++it) {
@@ -1456,12 +1418,13 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
             __builtin_amdgcn_global_load_lds((GlobalCPtr)src, (LdsPtr)&sm[buf][o][r][0], 16, 0, 0);
         }
     };
+    const int NCH = kdepth / KB;
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int ch = 0; ch < NCH; ++ch) {
         const int buf = ch & 1;
-        if (ch + 1 < NCH) issue(ch + 1, buf ^ 1);
+        if (ch + 1 < NCH) issue(ch + 1, buf ^ 1);  // the buffer every wave left at the last barrier
         if (active) {
 #pragma unroll
             for (int ks = 0; ks < KB; ks += 4) {
@@ -1478,40 +1441,10 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
                         acc[mi][mj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mj], fb[mi], acc[mi][mj], 0, 0, 2);
             }
         }
+        // the next chunk landed (every wave's own DMA), then visible to all waves
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    return;
-#endif
-    GAPLAC_GLOAD(0);
-    GAPLAC_LSTORE(0);
-    __syncthreads();
-    for (int ch = 0; ch < NCH; ++ch) {
-        const int buf = ch & 1;
-        const bool more = ch + 1 < NCH;
-        if (more) GAPLAC_GLOAD(ch + 1);
-        if (active) {
-#pragma unroll
-            for (int ks = 0; ks < KB; ks += 4) {
-                double fa[4], fb[4];
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    fa[m] = sm[buf][1][ks + fr][64 * wj + 16 * m + fc];
-                    fb[m] = sm[buf][0][ks + fr][64 * wi + 16 * m + fc];
-                }
-#pragma unroll
-                for (int mj = 0; mj < 4; ++mj)
-#pragma unroll
-                    for (int mi = 0; mi < 4; ++mi)
-                        acc[mi][mj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mj], fb[mi],
-                                                                            acc[mi][mj], 0, 0, 0);
-            }
-        }
-        if (more) GAPLAC_LSTORE(buf ^ 1);
-        __syncthreads();
-    }
-#undef GAPLAC_GLOAD
-#undef GAPLAC_LSTORE
 }
 
 __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
@@ -1557,9 +1490,12 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
     }
 }
 
-// One tile per workgroup, 208 VGPRs: two resident bulk workgroups leave exactly the 96
-// registers a quadrant chain kernel needs.
-__global__ __launch_bounds__(256, 2) void tile_syrk_kernel(BulkArgs a, KTime* __restrict__ kt) {
+// One tile per workgroup, 189 VGPRs (208 with register staging): two resident bulk
+// workgroups leave 134 registers per SIMD lane, more than the 96 a quadrant chain kernel needs.
+#ifndef GAPLAC_BULK_OCC
+#define GAPLAC_BULK_OCC 2
+#endif
+__global__ __launch_bounds__(256, GAPLAC_BULK_OCC) void tile_syrk_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
     tile_syrk_body(a, (int)blockIdx.x);
     kt_end(kt);

@@ -130,3 +130,25 @@ def test_large_n_properties(ctx):
     s = ctx.rand(X, terms, 0.1, z)
     _, _, q = ctx.logpdf(X, terms, 0.1, s, full=True)
     assert abs(q - float(z @ z)) <= 1e-9 * float(z @ z)
+
+
+def test_tail_and_superpanel_paths_agree(monkeypatch):
+    # N = 12000 (94 tile columns): super-panels, then the persistent tail with the M = 1024
+    # cross-covariance rows factored along; GAPLAC_TAILK=0 runs every column
+    # as a super-panel with the extra rows on their own streams. The two schedules round
+    # differently only in the order of independent sums: they agree far inside the bar.
+    if not gpu_available():
+        pytest.skip("no GPU")
+    rng = np.random.default_rng(41)
+    N, M = 12000, 1024
+    X = np.column_stack([rng.uniform(0, 10, N), rng.integers(0, N // 3, N).astype(float)])
+    Xs = np.column_stack([rng.uniform(0, 10, M), rng.integers(0, N // 3, M).astype(float)])
+    y = rng.normal(size=N)
+    terms = [(SQEXP, 0, 1.5, 0), (OU, 0, 3.0, 1), (CAT, 1, 0.0, 2), (NOISE, -1, 0.1, 3)]
+    with Context(0) as c:
+        m1, v1 = c.posterior_mean_var(X, terms, 0.1, y, Xs)
+    monkeypatch.setenv("GAPLAC_TAILK", "0")
+    with Context(0) as c:
+        m2, v2 = c.posterior_mean_var(X, terms, 0.1, y, Xs)
+    assert np.max(np.abs(m1 - m2)) <= 1e-11 * max(1.0, np.max(np.abs(m2)))
+    assert np.max(np.abs(v1 - v2)) <= 1e-11 * max(1.0, np.max(np.abs(v2)))
