@@ -1527,6 +1527,7 @@ __global__ __launch_bounds__(256, 2) void tile_band_kernel(BulkArgs a, KTime* __
 #define GAPLAC_QG 2
 #endif
 constexpr int QG = GAPLAC_QG;
+static_assert((NB / 4) % QG == 0, "the quadrant k-loop takes K in groups of 4 QG columns");
 // Bulk updates with at most this many 128x128 tiles run as quadrants (4 WGs per tile).
 constexpr int QUAD_BULK_MAX_TILES = 512;
 
@@ -2467,15 +2468,8 @@ __device__ __forceinline__ void tail_update(const Gm<AUX>& gC, const Gm<AUX>& gP
                 gC.st((uint32_t)((int64_t)(c0 + 16 * mj + fr + 4 * rg) * lda + r0 + 16 * mi + fc), acc[mi][mj][rg]);
 }
 
-// The whole-tile update C -= P Q^T over the K = 128 KD columns of tile columns
-// k .. k+KD-1, panels staged in LDS: per chunk of 16 panel columns each wave moves four
-// 1 KB column segments (P rows row0.. by waves 0-3, Q rows qrow0.. by waves 4-7) with
-// LDS-DMA (global_load_lds, 16 B per lane, sc1 like every load of handed-off data), two
-// chunk buffers, the next chunk in flight while the current one is multiplied. Each wave
-// reads its fragments from LDS: one copy of each panel row per workgroup instead of one per
-// wave that uses it (tail_update reads P 4x and Q 2x from L2). The 8 waves, their 4x2
-// blocks of 16x16 and the MFMA sequence per accumulator are tail_update<AUX, 4, 2, KD>'s:
-// bitwise the same result.
+// (An LDS-staged whole-tile variant of tail_update, panels moved once per workgroup by
+// LDS-DMA instead of per wave from L2, was measured in round 3 and not kept)
 // One 32x32 block of C -= P Q^T, K = 128 (the critical diagonal-tile update, split ten
 // ways): waves 0-3 take one 16x16 sub-block each and load all 32 k-steps of their two
 // fragments before the first MFMA, so the handed-off panel's memory latency is paid once.
