@@ -1394,11 +1394,16 @@ __device__ __forceinline__ void tile_decode(const BulkArgs& a, int idx, int& bi,
 // tile j) are column-major with leading dimension ldp. Lane element (mi, mj, rg) is tile
 // entry (row 64 wi + 16 mi + (lane & 15), column 64 wj + 16 mj + (lane >> 4) + 4 rg).
 // Inactive waves (upper quadrant of a diagonal tile) only help with the staging.
-typedef double MmaLds[2][2][KB][LR];  // the k-chunk staging buffers of tile_mma_neg
+template <int KBT>
+using MmaLdsT = double[2][2][KBT][LR];  // the k-chunk staging buffers of tile_mma_neg
+typedef MmaLdsT<KB> MmaLds;
 static_assert(sizeof(MmaLds) >= GRAM_LDS * sizeof(double), "gram_tile reuses the staging LDS");
 
+template <int KBT = KB>
 __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const double* __restrict__ Q,
-                                             int64_t ldp, int kdepth, bool active, d4 (&acc)[4][4], MmaLds& sm) {
+                                             int64_t ldp, int kdepth, bool active, d4 (&acc)[4][4],
+                                             MmaLdsT<KBT>& sm) {
+    constexpr int KB = KBT;
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
     const int wi = w & 1, wj = w >> 1;
@@ -1447,11 +1452,12 @@ __device__ __forceinline__ void tile_mma_neg(const double* __restrict__ P, const
     }
 }
 
+template <int KBT = KB>
 __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
     const int chunk = (a.ntiles + 7) >> 3;
     const int idx = (b & 7) * chunk + (b >> 3);
     if (idx >= a.ntiles) return;
-    __shared__ MmaLds sm;
+    __shared__ MmaLdsT<KBT> sm;
     int bi, bj, lj;
     tile_decode(a, idx, bi, bj, lj);
     const int64_t r0 = (int64_t)bi * NB;
@@ -1477,7 +1483,7 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
                     acc[mi][mj][rg] = Ci[(int64_t)(64 * wj + 16 * mj + fr + 4 * rg) * ldc];
         }
     }
-    tile_mma_neg(P, Q, a.pn.ld, a.kdepth, active, acc, sm);
+    tile_mma_neg<KBT>(P, Q, a.pn.ld, a.kdepth, active, acc, sm);
     if (!active) return;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
@@ -1492,10 +1498,7 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
 
 // One tile per workgroup, 189 VGPRs (208 with register staging): two resident bulk
 // workgroups leave 134 registers per SIMD lane, more than the 96 a quadrant chain kernel needs.
-#ifndef GAPLAC_BULK_OCC
-#define GAPLAC_BULK_OCC 2
-#endif
-__global__ __launch_bounds__(256, GAPLAC_BULK_OCC) void tile_syrk_kernel(BulkArgs a, KTime* __restrict__ kt) {
+__global__ __launch_bounds__(256, 2) void tile_syrk_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
     tile_syrk_body(a, (int)blockIdx.x);
     kt_end(kt);
@@ -1507,6 +1510,17 @@ __global__ __launch_bounds__(256, GAPLAC_BULK_OCC) void tile_syrk_kernel(BulkArg
 __global__ __launch_bounds__(256, 2) void tile_band_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
     tile_syrk_body(a, (int)blockIdx.x);
+    kt_end(kt);
+}
+
+// Large trailing updates (at least BULK_BIG_TILES tiles, N >= ~26k): 8-deep chunks (37 KB
+// of LDS) and 168 VGPRs, three resident workgroups per CU. Alone 0.874 vs 0.852 of peak at
+// the 64k shape; not for the 16k schedule, where three bulk workgroups leave no registers
+// for the chain's quadrant kernels.
+constexpr int BULK_BIG_TILES = 20000;
+__global__ __launch_bounds__(256, 3) void tile_syrk_big_kernel(BulkArgs a, KTime* __restrict__ kt) {
+    kt_begin(kt);
+    tile_syrk_body<8>(a, (int)blockIdx.x);
     kt_end(kt);
 }
 
@@ -2942,6 +2956,15 @@ void launch_trsm_rows(hipStream_t s, double* Acol, int64_t lda, int k, int bi0, 
 
 bool syrk_is_small(int ntiles) { return ntiles <= QUAD_BULK_MAX_TILES; }
 
+// GAPLAC_BULK_BIG=0 keeps every bulk update on tile_syrk_kernel (A/B)
+static bool bulk_big_enabled() {
+    static const bool on = [] {
+        const char* v = std::getenv("GAPLAC_BULK_BIG");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
 static int device_cus() {
     static const int n = [] {
         int dev = 0, cus = 0;
@@ -2971,6 +2994,8 @@ void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt) {
         quad_bulk_kernel<<<dim3((unsigned)(4 * grid)), dim3(256), 0, s>>>(a, kt);
     else if (a.whole)
         tile_band_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
+    else if (a.ntiles >= BULK_BIG_TILES && bulk_big_enabled())
+        tile_syrk_big_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
     else
         tile_syrk_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
 }
