@@ -548,8 +548,8 @@ __device__ __forceinline__ void dblk_update(double* Ab, int I, int J, int k, int
     for (int q = 0; q < 4; ++q) acc[q] = C[(fr + 4 * q) * 16 + fc];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-LJ[(4 * kk + fr) * 16 + fc], LI[(4 * kk + fr) * 16 + fc],
-                                                   acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(LJ[(4 * kk + fr) * 16 + fc], LI[(4 * kk + fr) * 16 + fc],
+                                                   acc, 0, 0, 1);  // neg A
 #pragma unroll
     for (int q = 0; q < 4; ++q) C[(fr + 4 * q) * 16 + fc] = acc[q];
 }
@@ -572,8 +572,8 @@ __device__ __forceinline__ void dblk_update2(double* Ab, int I1, int J1, int I2,
     }
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-        a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(-LJ1[(4 * kk + fr) * 16 + fc], LI1[(4 * kk + fr) * 16 + fc], a1, 0, 0, 0);
-        a2 = __builtin_amdgcn_mfma_f64_16x16x4f64(-LJ2[(4 * kk + fr) * 16 + fc], LI2[(4 * kk + fr) * 16 + fc], a2, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(LJ1[(4 * kk + fr) * 16 + fc], LI1[(4 * kk + fr) * 16 + fc], a1, 0, 0, 1);
+        a2 = __builtin_amdgcn_mfma_f64_16x16x4f64(LJ2[(4 * kk + fr) * 16 + fc], LI2[(4 * kk + fr) * 16 + fc], a2, 0, 0, 1);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1309,12 +1309,12 @@ __device__ __forceinline__ void trsm_subst_kernel_body(double* __restrict__ Acol
             const double* Lbc = Ls + (b * (b - 1) / 2 + c) * 256;
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
-                const double lbc = -Lbc[(4 * kk + fr) * 16 + fc];  // L_bc[j][m], m = 4kk + fr
+                const double lbc = Lbc[(4 * kk + fr) * 16 + fc];  // L_bc[j][m], m = 4kk + fr (negated: neg A)
                 // two partial sums (even / odd c): halves the dependent-accumulator chain
                 if (c & 1)
-                    s1 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s1, 0, 0, 0);
+                    s1 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s1, 0, 0, 1);
                 else
-                    s0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s0, 0, 0, 0);
+                    s0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s0, 0, 0, 1);
             }
         }
         s0 += s1;
@@ -1579,11 +1579,11 @@ __device__ __forceinline__ void quad_update(double* __restrict__ C, int64_t ldc,
     auto compute = [&](int buf) {
 #pragma unroll
         for (int s = 0; s < QG; ++s) {
-            const double b0 = -fb[buf][s][0], b1 = -fb[buf][s][1];
-            acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][s][0], b0, acc[0][0], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][s][0], b1, acc[1][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][s][1], b0, acc[0][1], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][s][1], b1, acc[1][1], 0, 0, 0);
+            const double b0 = fb[buf][s][0], b1 = fb[buf][s][1];  // negated by the MFMA (neg B)
+            acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][s][0], b0, acc[0][0], 0, 0, 2);
+            acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][s][0], b1, acc[1][0], 0, 0, 2);
+            acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][s][1], b0, acc[0][1], 0, 0, 2);
+            acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][s][1], b1, acc[1][1], 0, 0, 2);
         }
     };
     const int ng = kdepth / (4 * QG);  // 4 per 128 panel columns
@@ -2272,11 +2272,11 @@ __device__ __forceinline__ void tail_trsm(double* smem, double* Acol, int64_t ld
             const double* Lbc = Ls + (b * (b - 1) / 2 + c) * 256;
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
-                const double lbc = -Lbc[(4 * kk + fr) * 16 + fc];
+                const double lbc = Lbc[(4 * kk + fr) * 16 + fc];  // negated by the MFMA (neg A)
                 if (c & 1)
-                    s1 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s1, 0, 0, 0);
+                    s1 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s1, 0, 0, 1);
                 else
-                    s0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s0, 0, 0, 0);
+                    s0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s0, 0, 0, 1);
             }
         }
         s0 += s1;
@@ -2400,11 +2400,11 @@ __device__ __forceinline__ void tail_trsm_pipe(double* smem, unsigned* rowf, dou
             const double* Lbc = Ls + (b * (b - 1) / 2 + c) * 256;
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
-                const double lbc = -Lbc[(4 * kk + fr) * 16 + fc];
+                const double lbc = Lbc[(4 * kk + fr) * 16 + fc];  // negated by the MFMA (neg A)
                 if (c & 1)
-                    s1 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s1, 0, 0, 0);
+                    s1 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s1, 0, 0, 1);
                 else
-                    s0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s0, 0, 0, 0);
+                    s0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lbc, Y[c][kk], s0, 0, 0, 1);
             }
         }
         s0 += s1;
@@ -2458,10 +2458,10 @@ __device__ __forceinline__ void tail_update(const Gm<AUX>& gC, const Gm<AUX>& gP
         for (int st = 0; st < G; ++st)
 #pragma unroll
             for (int mi = 0; mi < RB; ++mi) {
-                const double b = -fb[buf][st][mi];
+                const double b = fb[buf][st][mi];  // negated by the MFMA (neg B)
 #pragma unroll
                 for (int mj = 0; mj < CB; ++mj)
-                    acc[mi][mj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][st][mj], b, acc[mi][mj], 0, 0, 0);
+                    acc[mi][mj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[buf][st][mj], b, acc[mi][mj], 0, 0, 2);
             }
     };
     constexpr int NG = KD * NB / (4 * G);  // 8 groups per 128 panel columns
@@ -2509,7 +2509,7 @@ __device__ __forceinline__ void tail_q32(const Gm<AUX>& gC, const Gm<AUX>& gP, i
         fa[st] = gP.ld((uint32_t)(col + q0 + fc));
     }
 #pragma unroll
-    for (int st = 0; st < KS; ++st) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[st], -fb[st], acc, 0, 0, 0);
+    for (int st = 0; st < KS; ++st) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[st], fb[st], acc, 0, 0, 2);  // neg B
 #pragma unroll
     for (int rg = 0; rg < 4; ++rg) gC.st((uint32_t)((int64_t)(c0 + fr + 4 * rg) * lda + r0 + fc), acc[rg]);
 }
