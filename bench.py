@@ -371,7 +371,7 @@ def main():
         traffic, traffic_src = load_traffic()
         roofline = {
             "bound": "mfma",
-            "kernel": "tile_syrk_kernel (bulk trailing update, 128x128 tiles, K=512 or 1024 (paired), fp64 MFMA 16x16x4)",
+            "kernel": "tile_syrk_kernel (bulk trailing update, 128x128 tiles, K=512 or 1024 (paired), LDS-DMA staged, fp64 MFMA 16x16x4)",
             "achieved": round(achieved, 3),
             "peak": PEAK_F64_TFLOPS,
             "unit": "TFLOP/s",
