@@ -74,6 +74,8 @@ struct gaplac_ctx {
     int pair_ext = 1;     // 1 = a deferring step also updates the band after next (§3.2)
     int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
     int pair_m = 40;      // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
+    int pair_depth = 0;   // GAPLAC_PAIR_DEPTH: super-panels per deferred bulk update (0: 4 from 256 tile
+                          //   columns on, else 2; N = 65536 1439 -> 1427 ms, 16k 26.97 -> 27.14 ms at 3-4)
     int ncu = 256;        // compute units of the device
     bool tailk = true;    // GAPLAC_TAILK: the serial tail as one persistent dataflow launch (tail_kernel)
     TailCtl* tctl = nullptr;     // its completion counters (zeroed per launch)
@@ -513,7 +515,9 @@ static bool pair_defer(const gaplac_ctx* ctx, const std::vector<int>& spc, int n
     const int nsp = (int)spc.size() - 1;
     const int jb = p + 2 <= nsp ? spc[(size_t)p + 2] : spc[(size_t)nsp];
     const int je = p + 3 <= nsp ? spc[(size_t)p + 3] : spc[(size_t)nsp];
-    return ctx->pair_m > 0 && pend < 0 && !ctx->serial && !ctx->xr_mode && je > jb && p + 1 + ctx->pair_ext < nsp &&
+    const int depth = ctx->pair_depth > 0 ? ctx->pair_depth : nt >= 256 ? 4 : 2;
+    return ctx->pair_m > 0 && (pend < 0 || p - pend + 1 < depth) && !ctx->serial && !ctx->xr_mode && je > jb &&
+           p + 1 + ctx->pair_ext < nsp &&
            p + 3 + ctx->pair_ext <= nsp && nt - spc[(size_t)p + 3 + ctx->pair_ext] >= ctx->pair_m;
 }
 
@@ -598,7 +602,18 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
                 launch_col_update(sm, ctx->A, lda, pn, nt, b0, b0, b1 - b0, kb, slot(ctx, 5, 0));
             }
         };
-        if (defer) {
+        // first panel column a band starting at tile column b0 still lacks: columns >= dcol
+        // lack every super-panel from pend on, the others only this step's
+        auto first_panel = [&](int b0) { return pend >= 0 && b0 >= dcol ? spc[(size_t)pend] : c0; };
+        if (defer && pend >= 0) {
+            // a deeper deferral (GAPLAC_PAIR_DEPTH > 2): the next-needed band gets this
+            // step's panel, the band after it every panel from pend on
+            band(jb, je, first_panel(jb));
+            HIPQ(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
+            const int e1 = ctx->pair_ext > 0 ? spc[(size_t)p + 4] : je;
+            if (je < e1) band(je, e1, first_panel(je));
+            dcol = std::max(dcol, e1);
+        } else if (defer) {
             band(jb, je, c0);
             HIPQ(ctx, hipEventRecord(ctx->ev_R[p & 1], sm));
             dcol = je;
@@ -1246,6 +1261,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_SERIAL")) ctx->serial = s[0] == '1';
     if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_PAIR_M")) ctx->pair_m = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_PAIR_DEPTH")) ctx->pair_depth = std::max(2, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BAND_TILES_M")) ctx->band_tiles_m = std::max(1, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAILK")) ctx->tailk = s[0] != '0';
