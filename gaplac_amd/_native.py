@@ -52,6 +52,17 @@ EXPORTED = (
     "gaplac_dist_update",
     "gaplac_dist_finish",
     "gaplac_dist_local",
+    "gaplac_dist_configure",
+    "gaplac_dist_chunks",
+    "gaplac_dist_panel_chunk",
+    "gaplac_dist_comm_begin_chunk",
+    "gaplac_dist_comm_end_chunk",
+    "gaplac_dist_plan_check",
+    "gaplac_dist_plan",
+    "gaplac_dist_replay_enable",
+    "gaplac_dist_replay_chunk",
+    "gaplac_dist_replay_stamps",
+    "gaplac_dist_replay_info",
 )
 
 
@@ -149,6 +160,18 @@ def load() -> ctypes.CDLL:
     lib.gaplac_dist_update.argtypes = [c_void_p, c_int32]
     lib.gaplac_dist_finish.argtypes = [c_void_p, _DP, _DP, _I64P]
     lib.gaplac_dist_local.argtypes = [c_void_p, c_void_p, c_int64]
+    lib.gaplac_dist_configure.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32]
+    lib.gaplac_dist_chunks.argtypes = [c_void_p, c_int32, _I32P]
+    lib.gaplac_dist_panel_chunk.argtypes = [c_void_p, c_int32, c_int32, _VPP, _I64P, _I32P]
+    lib.gaplac_dist_comm_begin_chunk.argtypes = [c_void_p, c_int32, c_int32, _VPP]
+    lib.gaplac_dist_comm_end_chunk.argtypes = [c_void_p, c_int32, c_int32]
+    lib.gaplac_dist_plan_check.argtypes = [c_int32, c_int32, c_int32, c_int32, _I64P, c_char_p, c_int64]
+    lib.gaplac_dist_plan.argtypes = [c_int32, c_int32, c_int32, c_int32, _I32P, c_int64, _I64P]
+    lib.gaplac_dist_replay_enable.argtypes = [c_void_p, c_int64]
+    lib.gaplac_dist_replay_chunk.argtypes = [c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int64, c_int64,
+                                             c_int64, c_int64]
+    lib.gaplac_dist_replay_stamps.argtypes = [c_void_p, c_void_p, c_int64]
+    lib.gaplac_dist_replay_info.argtypes = [c_void_p, c_int32, c_int32, _I64P, _I32P, _I32P]
     for name in EXPORTED:
         getattr(lib, name).restype = getattr(lib, name).restype or c_int
     lib.gaplac_last_error.restype = c_char_p

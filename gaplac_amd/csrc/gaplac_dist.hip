@@ -10,28 +10,36 @@
 // Steps (the host drives them; the only exchange is the panel broadcast):
 //   begin          all ranks: local Gram tiles (s_main)
 //   factor(s)      owner of SP s (s_panel, critical path): apply panel s-1 to SP s
-//                  (lookahead), factor SP s column by column (column updates inside
-//                  the SP, diagonal potrf, panel TRSM), pack rows >= first row of SP s
-//                  into panel buffer s&1
-//   bcast(s)       the host broadcasts panel buffer s&1 from the owner (RCCL on the
-//                  comm stream, gaplac_dist_comm_begin/_end bracket it)
-//   update(s)      all ranks: bulk trailing update of their SPs > s+1 with panel s
-//                  (s_main); SP s+1 gets panel s in factor(s+1) instead. Paired updates
-//                  (the single-GPU schedule's): an even step s whose
-//                  trailing matrix still has >= pair_m tile rows after SP s+3 updates only
-//                  SPs s+2 and s+3 (the next chain needs them); step s+1 then updates SP
-//                  s+3 with panel s+1 and every SP >= s+4 with panels s and s+1 at once
-//                  (K = 2 x 128 W: half the launches, twice the depth)
+//                  (lookahead, one launch per broadcast chunk as each chunk arrives),
+//                  factor SP s column by column (column updates inside the SP, diagonal
+//                  potrf, panel TRSM) and pack each chunk of columns into the panel buffer
+//                  as soon as its last column is final
+//   bcast(s, c)    the host broadcasts chunk c of panel s from the owner (RCCL on the comm
+//                  stream; gaplac_dist_comm_begin_chunk / _end_chunk bracket it)
+//   update(s)      all ranks: panel s (and, with deferred updates, the panels before it in
+//                  its group) applied to their SPs > s+1 following the step plan below
+//                  (s_main); SP s+1 gets panel s in factor(s+1) instead
 //   finish         all ranks: partial logdet / quad / info over their columns; the host
 //                  sums them across ranks (one allreduce of 3 numbers)
-// The host calls, per rank: begin; factor(0) [owner]; bcast(0); for s = 0..nsp-1:
-// { factor(s+1) [owner of s+1]; update(s); bcast(s+1) }; finish. Every call only
+// The host calls, per rank: begin; factor(0) [owner]; bcast(0, *); for s = 0..nsp-1:
+// { factor(s+1) [owner of s+1]; update(s); bcast(s+1, *) }; finish. Every call only
 // enqueues work: the streams overlap the bulk update with the next panel's chain.
-// Panel buffers: two PAIR buffers; panels s and s+1 (s even) share pair buffer (s/2) & 1
-// with the rows of panel s as the common origin (ld = Np - first row of SP s; the odd
-// panel's columns start 128 W rows down), so a paired update reads both as one K = 256 W
-// panel. Events keep a pair buffer from being re-filled (packed by its owner or received)
-// before the updates and lookaheads that read its previous pair have run.
+//
+// Step plan (build_plan, checked by check_plan / gaplac_dist_plan_check). Panels are grouped
+// in aligned groups of D (GAPLAC_DIST_DEPTH; the single-GPU path's deferred updates,
+// DESIGN.md §3.2 and §3.6): inside a group only the bands the next chains need (SPs s+2
+// and s+3) get the panels they lack, and the SPs after them get every panel of the group
+// at once at the group's last step (K = D x 128 W). Every step updates SP s+2 first and
+// then records ev_step, so the owner of SP s+2 starts its chain without waiting for the
+// rest of the update.
+//
+// Panel buffers: two GROUP buffers; the D panels of group g share buffer g & 1 with the
+// rows of the group's first panel as the common origin (ld = Np - that row; panel i of the
+// group starts 128 W i columns in and its rows above its own first row are never read), so
+// a deferred update reads the group's panels as one K = D x 128 W panel. A chunk (cw tile
+// columns, GAPLAC_DIST_CHUNK) is contiguous in the buffer. Events keep a group buffer from
+// being re-filled (packed by its owner or received) before the updates, lookaheads and
+// broadcasts that read its previous group have run.
 #include "gaplac_internal.h"
 
 #include <cstddef>
@@ -47,26 +55,64 @@
 
 using namespace gaplac;
 
+namespace {
+constexpr int MAXC = 8;  // chunks per panel (W <= 8)
+
+// One operation of a step's bulk update: SP g alone (BAND) or every owned SP >= g (SUF),
+// with the panels pf .. pl (one group); MARK: ev_step (SP s+2 is up to date).
+enum { OP_BAND = 0, OP_SUF = 1, OP_MARK = 2 };
+struct DOp {
+    int kind, g, pf, pl;
+};
+
+// Device timestamps of the replay, 100 MHz s_memrealtime ticks, per step
+// s: UPD(s) update(s) started, BAND(s) SP s+2 up to date in update(s), END(s) update(s)
+// done, PACK(s, c) chunk c packed, RECV(s, c) chunk c received (sent, on its owner).
+constexpr int ST_PER_STEP = 3 + 2 * MAXC;
+inline int st_upd(int s) { return s * ST_PER_STEP; }
+inline int st_band(int s) { return s * ST_PER_STEP + 1; }
+inline int st_end(int s) { return s * ST_PER_STEP + 2; }
+inline int st_pack(int s, int c) { return s * ST_PER_STEP + 3 + c; }
+inline int st_recv(int s, int c) { return s * ST_PER_STEP + 3 + MAXC + c; }
+
+// Release of one modelled transfer: spin until max_i(stamps[dep_i] + add_i) (dep_i = -1:
+// unused, -2: the kernel's own start), then stamp `out`. Bounded: never spins past start + 2 s.
+struct Release {
+    int dep[3];
+    long long add[3];
+    int out;
+};
+}  // namespace
+
 struct gaplac_dist {
     int device = 0, nranks = 1, rank = 0, W = 4;
+    int D = 2;         // GAPLAC_DIST_DEPTH: panels per deferral group
+    int cw = 4;        // GAPLAC_DIST_CHUNK: tile columns per broadcast chunk
+    int big_mode = 1;  // GAPLAC_DIST_BIG: 0 never, 1 per rank (no chain beside the launch), 2 by launch size
+    int big_min = 2048;  // GAPLAC_DIST_BIG_MIN: tiles of a launch for the per-rank choice
+    int alone = 0;     // GAPLAC_DIST_ALONE: the owner of SP s+1 starts update(s) after its chain
     hipStream_t s_main = nullptr, s_panel = nullptr, s_comm = nullptr;
     hipEvent_t ev_gram = nullptr, ev_panel_done = nullptr;
-    // ev_recv / ev_packed per panel parity; ev_step[s & 1]: update(s) done (the last bulk
-    // update of SP s+2's columns); ev_free_main / ev_free_panel per pair buffer: its last
-    // bulk update / lookahead reader done
-    hipEvent_t ev_recv[2] = {}, ev_packed[2] = {}, ev_step[2] = {}, ev_free_main[2] = {}, ev_free_panel[2] = {};
-    int pair_m = 40;  // GAPLAC_PAIR_M: paired updates while >= pair_m tile rows follow SP s+3
+    // ev_recv / ev_packed per panel parity and chunk; ev_step[s & 1]: update(s) brought SP
+    // s+2 up to date; ev_free_main / ev_free_panel / ev_free_comm per group buffer: its last
+    // bulk update / lookahead / broadcast of the buffer's current group done
+    hipEvent_t ev_recv[2][MAXC] = {}, ev_packed[2][MAXC] = {};
+    hipEvent_t ev_step[2] = {}, ev_free_main[2] = {}, ev_free_panel[2] = {}, ev_free_comm[2] = {};
+    hipEvent_t ev_upd[2] = {};  // replay: update(s) started (its UPD stamp written)
+    int pair_m = 40;  // GAPLAC_PAIR_M: deferred updates while >= pair_m tile rows follow SP s+3
     // geometry of the current evaluation
     int64_t N = -1, Np = 0;
     int nt = 0, nsp = 0, nloc = 0;
     bool factored_any = false;
+    std::vector<std::vector<DOp>> plan;
+    int plan_nt = -1;
     // device buffers
     double* C = nullptr;
     size_t C_elems = 0;
     double* Dinv = nullptr;
     size_t Dinv_elems = 0;
     double* pbuf[2] = {};
-    size_t pbuf_cap = 0;   // elements per (pair) buffer
+    size_t pbuf_cap = 0;   // elements per group buffer
     bool pbuf_external = false;
     uint32_t* tiles = nullptr;
     size_t tiles_elems = 0;
@@ -84,6 +130,9 @@ struct gaplac_dist {
     EvalResult* hres = nullptr;  // pinned
     TermPack* dtp = nullptr;
     TermPack* htp = nullptr;     // pinned
+    // replay (gaplac_dist_replay_*): device stamps, nullptr = off
+    unsigned long long* stamps = nullptr;
+    size_t stamps_elems = 0;
     std::string err;
 };
 
@@ -122,26 +171,119 @@ int dgrow(gaplac_dist* d, T** p, size_t* cap, size_t n) {
     return 0;
 }
 
+// ---- the step plan (pure host logic) ----
+
+// Does step p defer (only the bands of SPs p+2, p+3 get the group's panels)? Groups are
+// aligned (a deferral starts at a group's first step and ends at its last one at the
+// latest); pend: the group's first panel while a deferral runs, -1 otherwise.
+bool defers(int p, int pend, int nsp, int nt, int W, int D, int pair_m) {
+    if (D < 2 || pair_m <= 0 || p + 4 > nsp || nt - (p + 4) * W < pair_m) return false;
+    return pend < 0 ? p % D == 0 : p % D != D - 1;
+}
+
+std::vector<std::vector<DOp>> build_plan(int nsp, int nt, int W, int D, int pair_m) {
+    std::vector<std::vector<DOp>> plan((size_t)std::max(nsp, 0));
+    int pend = -1, dcol = nsp;  // SPs >= dcol lack every panel from pend on
+    for (int p = 0; p < nsp; ++p) {
+        std::vector<DOp>& ops = plan[(size_t)p];
+        const bool defer = defers(p, pend, nsp, nt, W, D, pair_m);
+        auto first = [&](int g) { return pend >= 0 && g >= dcol ? pend : p; };
+        if (p + 2 < nsp) ops.push_back({OP_BAND, p + 2, first(p + 2), p});
+        ops.push_back({OP_MARK, p + 2, p, p});
+        if (defer) {
+            if (p + 3 < nsp) ops.push_back({OP_BAND, p + 3, first(p + 3), p});
+            if (pend < 0) pend = p;
+            dcol = std::max(pend == p ? 0 : dcol, p + 4);
+        } else if (pend >= 0) {
+            // the group's last step: SP p+3 and everything after it lack panels pend .. p
+            if (p + 3 < nsp) ops.push_back({OP_SUF, std::max(p + 3, dcol), pend, p});
+            pend = -1;
+            dcol = nsp;
+        } else if (p + 3 < nsp) {
+            ops.push_back({OP_SUF, p + 3, p, p});
+        }
+    }
+    return plan;
+}
+
+// Every SP g gets panels 0 .. g-1 exactly once and in order (the update ops of steps
+// <= g-2, before step g-2's mark, then the lookahead with panel g-1 in factor(g)); every op
+// of step p reads panels of p's group only, ending at p.
+bool check_plan(const std::vector<std::vector<DOp>>& plan, int nsp, int D, std::string* why) {
+    std::vector<int> next((size_t)nsp, 0);  // next panel SP g must receive
+    char buf[256];
+    auto fail = [&](const char* fmt, int a, int b, int c) {
+        if (why) {
+            std::snprintf(buf, sizeof buf, fmt, a, b, c);
+            *why = buf;
+        }
+        return false;
+    };
+    for (int p = 0; p < nsp; ++p) {
+        bool marked = false;
+        for (const DOp& op : plan[(size_t)p]) {
+            if (op.kind == OP_MARK) {
+                if (op.g != p + 2) return fail("step %d: mark for SP %d%s", p, op.g, 0);
+                marked = true;
+                continue;
+            }
+            if (op.pl != p || op.pf > op.pl || op.pf / D != p / D)
+                return fail("step %d reads panels %d..%d", p, op.pf, op.pl);
+            const int g1 = op.kind == OP_BAND ? op.g + 1 : nsp;
+            for (int g = op.g; g < g1; ++g) {
+                if (g <= p + 1) return fail("step %d updates SP %d (not after its lookahead) %d", p, g, 0);
+                if (g == p + 2 && marked) return fail("step %d updates SP %d after the mark%d", p, g, 0);
+                if (next[(size_t)g] != op.pf) return fail("SP %d gets panel %d, expected %d", g, op.pf, next[(size_t)g]);
+                next[(size_t)g] = op.pl + 1;
+            }
+        }
+        if (!marked) return fail("step %d has no mark%d%d", p, 0, 0);
+        // factor(p+1): the lookahead applies panel p to SP p+1
+        if (p + 1 < nsp) {
+            if (next[(size_t)p + 1] != p) return fail("SP %d reaches its chain with panels < %d, needs %d", p + 1,
+                                                      next[(size_t)p + 1], p);
+            next[(size_t)p + 1] = p + 1;
+        }
+    }
+    for (int g = 0; g < nsp; ++g)
+        if (next[(size_t)g] != g) return fail("SP %d ends with panels < %d%d", g, next[(size_t)g], 0);
+    return true;
+}
+
 ColMap cmap(const gaplac_dist* d) { return ColMap{d->nranks, d->rank, d->W}; }
 int sp_first(const gaplac_dist* d, int s) { return s * d->W; }
 int sp_width(const gaplac_dist* d, int s) { return std::min(d->W, d->nt - s * d->W); }
 int sp_local(const gaplac_dist* d, int s) { return (s / d->nranks) * d->W; }  // first local column
 bool owns(const gaplac_dist* d, int s) { return s % d->nranks == d->rank; }
 int64_t panel_row0(const gaplac_dist* d, int s) { return (int64_t)sp_first(d, s) * NB; }
-// pair buffer of panel s: (s / 2) & 1; its origin row is that of the pair's even panel
-int pair_buf(int s) { return (s >> 1) & 1; }
-int64_t pair_row0(const gaplac_dist* d, int s) { return panel_row0(d, s & ~1); }
-int64_t pair_ld(const gaplac_dist* d, int s) { return d->Np - pair_row0(d, s); }
-// first element of panel s (its row panel_row0(s), column 0) in its pair buffer
-double* panel_ptr(const gaplac_dist* d, int s) {
-    return d->pbuf[pair_buf(s)] + (int64_t)(s & 1) * d->W * NB * pair_ld(d, s) + (panel_row0(d, s) - pair_row0(d, s));
+// group buffer of panel s: (s / D) & 1; its origin row is that of the group's first panel
+int group_buf(const gaplac_dist* d, int s) { return (s / d->D) & 1; }
+int group_first(const gaplac_dist* d, int s) { return s / d->D * d->D; }
+int64_t group_row0(const gaplac_dist* d, int s) { return panel_row0(d, group_first(d, s)); }
+int64_t group_ld(const gaplac_dist* d, int s) { return d->Np - group_row0(d, s); }
+// column block of panel s in its group buffer (row origin = group_row0)
+double* panel_base(const gaplac_dist* d, int s) {
+    return d->pbuf[group_buf(d, s)] + (int64_t)(s - group_first(d, s)) * d->W * NB * group_ld(d, s);
 }
-Panel panel_of(const gaplac_dist* d, int s) {
-    return Panel{d->pbuf[pair_buf(s)] + (int64_t)(s & 1) * d->W * NB * pair_ld(d, s), pair_ld(d, s), pair_row0(d, s)};
+Panel panel_of(const gaplac_dist* d, int s) { return Panel{panel_base(d, s), group_ld(d, s), group_row0(d, s)}; }
+int nchunks(const gaplac_dist* d, int s) { return (sp_width(d, s) + d->cw - 1) / d->cw; }
+int chunk_col0(const gaplac_dist* d, int c) { return c * d->cw; }  // first tile column of chunk c in its SP
+int chunk_cols(const gaplac_dist* d, int s, int c) { return std::min(d->cw, sp_width(d, s) - c * d->cw); }
+Panel chunk_panel(const gaplac_dist* d, int s, int c) {
+    Panel p = panel_of(d, s);
+    p.P += (int64_t)chunk_col0(d, c) * NB * p.ld;
+    return p;
 }
-// does step s defer (paired updates)? Even steps only: panels s and s+1 share a buffer.
-bool pair_step(const gaplac_dist* d, int s) {
-    return d->pair_m > 0 && (s & 1) == 0 && s + 4 <= d->nsp && d->nt - (s + 4) * d->W >= d->pair_m;
+// the chunk's doubles in the buffer: from the panel's first row in its first column to the
+// end of its last column (the gap rows above the panel's first row inside the chunk go along)
+double* chunk_ptr(const gaplac_dist* d, int s, int c) {
+    return const_cast<double*>(chunk_panel(d, s, c).P) + (panel_row0(d, s) - group_row0(d, s));
+}
+int64_t chunk_count(const gaplac_dist* d, int s, int c) {
+    return (int64_t)chunk_cols(d, s, c) * NB * group_ld(d, s) - (panel_row0(d, s) - group_row0(d, s));
+}
+int64_t chunk_bytes_useful(const gaplac_dist* d, int s, int c) {  // rows >= the panel's first row only
+    return (int64_t)chunk_cols(d, s, c) * NB * (d->Np - panel_row0(d, s)) * 8;
 }
 
 // Tile lists: the Gram list (all owned lower tiles), then for every owned SP ordinal u
@@ -213,6 +355,35 @@ struct DistGuard {
     }
 };
 
+// ---- replay kernels: timestamps and modelled transfers ----
+__global__ void stamp_kernel(unsigned long long* slot) {
+    if (threadIdx.x == 0) *slot = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+}
+
+__global__ void release_kernel(unsigned long long* stamps, Release r) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+    long long target = 0;
+    for (int i = 0; i < 3; ++i)
+        if (r.dep[i] >= 0) target = std::max(target, (long long)stamps[r.dep[i]] + r.add[i]);
+        else if (r.dep[i] == -2) target = std::max(target, (long long)t0 + r.add[i]);
+    const long long limit = (long long)t0 + 200000000ll;  // 2 s at 100 MHz
+    if (target > limit) target = limit;
+    unsigned long long now = t0;
+    while ((long long)now < target) {
+        __builtin_amdgcn_s_sleep(4);
+        now = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+    }
+    stamps[r.out] = now;
+}
+
+int stamp(gaplac_dist* d, hipStream_t s, int slot) {
+    if (!d->stamps) return 0;
+    if (!guard_launch("stamp_kernel")) return 0;
+    stamp_kernel<<<dim3(1), dim3(64), 0, s>>>(d->stamps + slot);
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -222,7 +393,7 @@ const char* gaplac_dist_last_error(const gaplac_dist* d) { return d ? d->err.c_s
 int gaplac_dist_create(int device, int nranks, int rank, int spw, gaplac_dist** out) {
     if (!out) return GAPLAC_E_ARG;
     *out = nullptr;
-    if (nranks < 1 || rank < 0 || rank >= nranks || spw < 1 || spw > 8) return GAPLAC_E_ARG;
+    if (nranks < 1 || rank < 0 || rank >= nranks || spw < 1 || spw > MAXC) return GAPLAC_E_ARG;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return GAPLAC_E_NODEVICE;
     gaplac_dist* d = new gaplac_dist();
@@ -230,6 +401,8 @@ int gaplac_dist_create(int device, int nranks, int rank, int spw, gaplac_dist** 
     d->nranks = nranks;
     d->rank = rank;
     d->W = spw;
+    d->cw = spw;
+    d->big_mode = nranks == 1 ? 2 : 1;  // one rank: the single-GPU rule
     auto fail = [&](const char* what, hipError_t e) {
         std::fprintf(stderr, "gaplac_dist_create: %s: %s\n", what, hipGetErrorString(e));
         gaplac_dist_destroy(d);
@@ -246,9 +419,21 @@ int gaplac_dist_create(int device, int nranks, int rank, int spw, gaplac_dist** 
     if ((e = hipStreamCreateWithPriority(&d->s_main, hipStreamNonBlocking, least)) != hipSuccess)
         return fail("stream", e);
     if (const char* e = std::getenv("GAPLAC_PAIR_M")) d->pair_m = std::max(0, std::atoi(e));
-    hipEvent_t* evs[] = {&d->ev_gram, &d->ev_panel_done, &d->ev_recv[0], &d->ev_recv[1], &d->ev_packed[0],
-                         &d->ev_packed[1], &d->ev_step[0], &d->ev_step[1], &d->ev_free_main[0],
-                         &d->ev_free_main[1], &d->ev_free_panel[0], &d->ev_free_panel[1]};
+    if (const char* e = std::getenv("GAPLAC_DIST_DEPTH")) d->D = std::max(1, std::min(8, std::atoi(e)));
+    if (const char* e = std::getenv("GAPLAC_DIST_CHUNK")) d->cw = std::max(1, std::min(spw, std::atoi(e)));
+    if (const char* e = std::getenv("GAPLAC_DIST_BIG")) d->big_mode = std::max(0, std::min(2, std::atoi(e)));
+    if (const char* e = std::getenv("GAPLAC_DIST_BIG_MIN")) d->big_min = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("GAPLAC_DIST_ALONE")) d->alone = std::atoi(e) > 0;
+    std::vector<hipEvent_t*> evs = {&d->ev_gram, &d->ev_panel_done};
+    for (int b = 0; b < 2; ++b) {
+        for (int c = 0; c < MAXC; ++c) {
+            evs.push_back(&d->ev_recv[b][c]);
+            evs.push_back(&d->ev_packed[b][c]);
+        }
+        for (hipEvent_t* ev : {&d->ev_step[b], &d->ev_free_main[b], &d->ev_free_panel[b], &d->ev_free_comm[b],
+                               &d->ev_upd[b]})
+            evs.push_back(ev);
+    }
     for (hipEvent_t* ev : evs)
         if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return fail("event", e);
     if ((e = hipMalloc(reinterpret_cast<void**>(&d->dres), sizeof(EvalResult))) != hipSuccess)
@@ -268,13 +453,19 @@ int gaplac_dist_destroy(gaplac_dist* d) {
     (void)hipSetDevice(d->device);
     for (hipStream_t s : {d->s_main, d->s_panel, d->s_comm})
         if (s) (void)hipStreamSynchronize(s);
-    hipEvent_t evs[] = {d->ev_gram, d->ev_panel_done, d->ev_recv[0], d->ev_recv[1], d->ev_packed[0],
-                        d->ev_packed[1], d->ev_step[0], d->ev_step[1], d->ev_free_main[0],
-                        d->ev_free_main[1], d->ev_free_panel[0], d->ev_free_panel[1]};
+    std::vector<hipEvent_t> evs = {d->ev_gram, d->ev_panel_done};
+    for (int b = 0; b < 2; ++b) {
+        for (int c = 0; c < MAXC; ++c) {
+            evs.push_back(d->ev_recv[b][c]);
+            evs.push_back(d->ev_packed[b][c]);
+        }
+        for (hipEvent_t ev : {d->ev_step[b], d->ev_free_main[b], d->ev_free_panel[b], d->ev_free_comm[b], d->ev_upd[b]})
+            evs.push_back(ev);
+    }
     for (hipEvent_t ev : evs)
         if (ev) (void)hipEventDestroy(ev);
     for (void* p : {(void*)d->C, (void*)d->Dinv, (void*)d->tiles, (void*)d->dX, (void*)d->dv, (void*)d->dres,
-                    (void*)d->dtp})
+                    (void*)d->dtp, (void*)d->stamps})
         if (p) (void)hipFree(p);
     if (!d->pbuf_external)
         for (double* p : d->pbuf)
@@ -284,6 +475,32 @@ int gaplac_dist_destroy(gaplac_dist* d) {
     for (hipStream_t s : {d->s_main, d->s_panel, d->s_comm})
         if (s) (void)hipStreamDestroy(s);
     delete d;
+    return 0;
+}
+
+// Schedule options (the environment's GAPLAC_DIST_* are the defaults): depth = panels per
+// deferral group (1 = none), chunk = tile columns per broadcast chunk, big = bulk kernel
+// choice (0 never the large-launch kernel, 1 per rank: launches of >= big_min tiles with no
+// chain of this rank beside them, 2 by launch size as on one GPU: every rank of an
+// in-process loopback job shares one device), alone = 1: the owner of SP s+1 starts its
+// update(s) only after its chain of SP s+1 (the chain then has the GPU to itself; the
+// bulk share catches up while the rank waits for later panels). A value < 0 leaves the
+// option as it is.
+int gaplac_dist_configure(gaplac_dist* d, int32_t depth, int32_t chunk, int32_t big, int32_t big_min,
+                          int32_t alone) {
+    if (!d) return GAPLAC_E_ARG;
+    if (depth > 8 || chunk > d->W || big > 2) return derr(d, GAPLAC_E_ARG, "configure: bad option");
+    if (depth >= 1 && depth != d->D) {
+        if (d->pbuf_external) return derr(d, GAPLAC_E_ARG, "configure: depth changes the panel buffer size");
+        d->D = depth;
+        d->plan_nt = -1;
+    }
+    if (depth == 0) return derr(d, GAPLAC_E_ARG, "configure: depth 0");
+    if (chunk >= 1) d->cw = chunk;
+    if (chunk == 0) return derr(d, GAPLAC_E_ARG, "configure: chunk 0");
+    if (big >= 0) d->big_mode = big;
+    if (big_min >= 1) d->big_min = big_min;
+    if (alone >= 0) d->alone = alone > 0;
     return 0;
 }
 
@@ -312,7 +529,7 @@ int gaplac_dist_set_panel_buffers(gaplac_dist* d, void* b0, void* b1, int64_t ca
 }
 
 // Geometry for N: padded order, tile / super-panel counts, this rank's local tile
-// columns, and the doubles one (pair) panel buffer needs (the pair of SPs 0 and 1).
+// columns, and the doubles one group buffer needs (the group of SPs 0 .. D-1).
 int gaplac_dist_geometry(gaplac_dist* d, int64_t N, int64_t* Np, int32_t* nt, int32_t* nsp, int32_t* nloc,
                          int64_t* panel_elems) {
     if (!d || N < 1) return derr(d, GAPLAC_E_ARG, "bad geometry query");
@@ -325,7 +542,7 @@ int gaplac_dist_geometry(gaplac_dist* d, int64_t N, int64_t* Np, int32_t* nt, in
     if (nt) *nt = t;
     if (nsp) *nsp = ns;
     if (nloc) *nloc = nl;
-    if (panel_elems) *panel_elems = np * (int64_t)std::min(2 * d->W, t) * NB;
+    if (panel_elems) *panel_elems = np * (int64_t)std::min(d->D * d->W, t) * NB;
     return 0;
 }
 
@@ -353,6 +570,12 @@ int gaplac_dist_begin(gaplac_dist* d, int64_t N, int32_t D, const double* X, int
     d->nsp = nsp;
     d->nloc = nloc;
     d->factored_any = false;
+    if (d->plan_nt != nt) {
+        d->plan = build_plan(nsp, nt, d->W, d->D, d->pair_m);
+        std::string why;
+        if (!check_plan(d->plan, nsp, d->D, &why)) return derr(d, GAPLAC_E_ARG, "step plan: %s", why.c_str());
+        d->plan_nt = nt;
+    }
     if ((rc = dgrow(d, &d->C, &d->C_elems, (size_t)Np * nloc * NB))) return rc;
     if ((rc = dgrow(d, &d->Dinv, &d->Dinv_elems, (size_t)nloc * DINV_PER_BLOCK))) return rc;
     if (d->pbuf_external) {
@@ -382,6 +605,7 @@ int gaplac_dist_begin(gaplac_dist* d, int64_t N, int32_t D, const double* X, int
                          nloc - 1, nullptr);
         if ((rc = guard.check())) return rc;
     }
+    if (d->stamps && d->stamps_elems >= (size_t)nsp * ST_PER_STEP + 1) stamp(d, d->s_main, nsp * ST_PER_STEP);
     DCK(d, hipEventRecord(d->ev_gram, d->s_main));
     DCK(d, hipStreamWaitEvent(d->s_panel, d->ev_gram, 0));
     DCK(d, hipGetLastError());
@@ -389,8 +613,9 @@ int gaplac_dist_begin(gaplac_dist* d, int64_t N, int32_t D, const double* X, int
     return 0;
 }
 
-// Owner of SP s only. Lookahead update with panel s-1, then the SP's panel chain, then
-// the pack into panel buffer s&1 (all on s_panel).
+// Owner of SP s only. Lookahead update with panel s-1 (chunk by chunk, as each arrives),
+// then the SP's column chain, packing each chunk into the group buffer once its last
+// column is final (all on s_panel).
 int gaplac_dist_factor(gaplac_dist* d, int32_t s) {
     if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "factor: step %d out of range", s);
     if (!owns(d, s)) return derr(d, GAPLAC_E_ARG, "factor: rank %d does not own super-panel %d", d->rank, s);
@@ -399,19 +624,20 @@ int gaplac_dist_factor(gaplac_dist* d, int32_t s) {
     hipStream_t sp = d->s_panel;
     const int c0 = sp_first(d, s), w = sp_width(d, s), lc0 = sp_local(d, s);
     const int64_t ldc = d->Np;
-    // update(s-2) (s_main) was the last bulk update of SP s's columns (a paired update at
-    // an odd step covers SPs >= step + 3, a deferring step's bands SPs step + 2, step + 3),
-    // and the pack below overwrites pair buffer pair_buf(s): its previous pair's last bulk
-    // update ran before (ev_free_main; its lookahead readers are earlier on this stream)
+    // update(s-2) brought SP s up to date (ev_step, recorded right after its band)
     DCK(d, hipStreamWaitEvent(sp, d->ev_step[s & 1], 0));
-    DCK(d, hipStreamWaitEvent(sp, d->ev_free_main[pair_buf(s)], 0));
     if (s > 0) {
-        DCK(d, hipStreamWaitEvent(sp, d->ev_recv[(s - 1) & 1], 0));
-        launch_col_update(sp, d->C, ldc, panel_of(d, s - 1), d->nt, c0, lc0, w, sp_width(d, s - 1) * NB, nullptr);
-        // this rank's latest lookahead reading the pair buffer (the receive of the buffer's
-        // next pair waits for it on the comm stream)
-        DCK(d, hipEventRecord(d->ev_free_panel[pair_buf(s - 1)], sp));
+        const int q = s - 1, nc = nchunks(d, q);
+        for (int c = 0; c < nc; ++c) {
+            if (!owns(d, q)) DCK(d, hipStreamWaitEvent(sp, d->ev_recv[q & 1][c], 0));
+            launch_col_update(sp, d->C, ldc, chunk_panel(d, q, c), d->nt, c0, lc0, w, chunk_cols(d, q, c) * NB,
+                              nullptr);
+        }
+        // this rank's latest lookahead reading the group buffer (the receive of the
+        // buffer's next group waits for it on the comm stream)
+        DCK(d, hipEventRecord(d->ev_free_panel[group_buf(d, q)], sp));
     }
+    const int64_t r0 = panel_row0(d, s), ldp = group_ld(d, s);
     for (int c = c0; c < c0 + w; ++c) {
         const int lc = lc0 + (c - c0);
         double* Acol = d->C + (int64_t)lc * NB * ldc;
@@ -421,98 +647,162 @@ int gaplac_dist_factor(gaplac_dist* d, int32_t s) {
         if ((int64_t)c * NB < d->N)
             launch_potrf_diag(sp, Acol + (int64_t)c * NB, ldc, d->N, (int64_t)c * NB, Dk, d->dres, nullptr);
         launch_trsm(sp, Acol, ldc, d->nt, c, Dk, nullptr);
+        const int k = c - c0;  // column of the SP
+        const int ch = k / d->cw;
+        if (k == w - 1 || (k + 1) % d->cw == 0) {  // the chunk's last column is final: pack it
+            if (ch == 0) {
+                // the packs overwrite group buffer group_buf(s): its previous group must be
+                // done with on s_main (ev_free_main; at a group's later panels implied by
+                // ev_step, which follows every update of steps <= s - 3) and on the comm
+                // stream (ev_free_comm: its broadcasts, this rank's own sends included); its
+                // lookahead readers are earlier on this stream
+                if (s % d->D == 0) DCK(d, hipStreamWaitEvent(sp, d->ev_free_main[group_buf(d, s)], 0));
+                DCK(d, hipStreamWaitEvent(sp, d->ev_free_comm[group_buf(d, s)], 0));
+            }
+            const int kc0 = chunk_col0(d, ch), ncol = chunk_cols(d, s, ch);
+            double* dst = const_cast<double*>(chunk_panel(d, s, ch).P) + (r0 - group_row0(d, s));
+            DCK(d, hipMemcpy2DAsync(dst, (size_t)ldp * 8, d->C + (int64_t)(lc0 + kc0) * NB * ldc + r0, (size_t)ldc * 8,
+                                    (size_t)(d->Np - r0) * 8, (size_t)ncol * NB, hipMemcpyDeviceToDevice, sp));
+            stamp(d, sp, st_pack(s, ch));
+            DCK(d, hipEventRecord(d->ev_packed[s & 1][ch], sp));
+        }
     }
-    const int64_t r0 = panel_row0(d, s), ldp = pair_ld(d, s);
-    DCK(d, hipMemcpy2DAsync(panel_ptr(d, s), (size_t)ldp * 8, d->C + (int64_t)lc0 * NB * ldc + r0, (size_t)ldc * 8,
-                            (size_t)(d->Np - r0) * 8, (size_t)w * NB, hipMemcpyDeviceToDevice, sp));
-    DCK(d, hipEventRecord(d->ev_packed[s & 1], sp));
     DCK(d, hipEventRecord(d->ev_panel_done, sp));
     d->factored_any = true;
     DCK(d, hipGetLastError());
     return guard.check();
 }
 
-// Device buffer, element count and root rank of the broadcast of panel s.
-int gaplac_dist_panel(gaplac_dist* d, int32_t s, void** ptr, int64_t* count, int32_t* root) {
-    if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "panel: step %d out of range", s);
-    // the panel's columns in its pair buffer, from its first row to the end of its last
-    // column (an odd panel's column gaps above its first row go along: 128 W rows each)
-    if (ptr) *ptr = panel_ptr(d, s);
-    if (count) *count = (int64_t)sp_width(d, s) * NB * pair_ld(d, s) - (panel_row0(d, s) - pair_row0(d, s));
+int gaplac_dist_chunks(gaplac_dist* d, int32_t s, int32_t* out_chunks) {
+    if (!d || s < 0 || s >= d->nsp || !out_chunks) return derr(d, GAPLAC_E_ARG, "chunks: step %d out of range", s);
+    *out_chunks = nchunks(d, s);
+    return 0;
+}
+
+// Device buffer, element count and root rank of the broadcast of chunk c of panel s.
+int gaplac_dist_panel_chunk(gaplac_dist* d, int32_t s, int32_t c, void** ptr, int64_t* count, int32_t* root) {
+    if (!d || s < 0 || s >= d->nsp || c < 0 || c >= nchunks(d, s))
+        return derr(d, GAPLAC_E_ARG, "panel: step %d chunk %d out of range", s, c);
+    if (ptr) *ptr = chunk_ptr(d, s, c);
+    if (count) *count = chunk_count(d, s, c);
     if (root) *root = s % d->nranks;
     return 0;
 }
 
-// Make the comm stream ready for the broadcast of panel s (root: the panel is packed;
-// others: the buffer's previous contents are no longer read) and return it as an opaque
-// hipStream_t, on which the host enqueues the broadcast (ncclBroadcast / RCCL).
-int gaplac_dist_comm_begin(gaplac_dist* d, int32_t s, void** stream) {
-    if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "comm_begin: step %d out of range", s);
+// The whole panel s as one broadcast (every chunk; gaplac_dist_comm_end then releases all).
+int gaplac_dist_panel(gaplac_dist* d, int32_t s, void** ptr, int64_t* count, int32_t* root) {
+    if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "panel: step %d out of range", s);
+    if (ptr) *ptr = chunk_ptr(d, s, 0);
+    if (count) *count = (int64_t)sp_width(d, s) * NB * group_ld(d, s) - (panel_row0(d, s) - group_row0(d, s));
+    if (root) *root = s % d->nranks;
+    return 0;
+}
+
+// Make the comm stream ready for the broadcast of chunk c of panel s (root: the chunk is
+// packed; others, at the panel's first chunk: the group buffer's previous group is no
+// longer read) and return it as an opaque hipStream_t, on which the host enqueues the
+// broadcast (ncclBroadcast / RCCL).
+int gaplac_dist_comm_begin_chunk(gaplac_dist* d, int32_t s, int32_t c, void** stream) {
+    if (!d || s < 0 || s >= d->nsp || c < 0 || c >= nchunks(d, s))
+        return derr(d, GAPLAC_E_ARG, "comm_begin: step %d chunk %d out of range", s, c);
     DCK(d, hipSetDevice(d->device));
     if (owns(d, s)) {
-        DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_packed[s & 1], 0));
-    } else {  // the pair buffer's previous pair: its last bulk update and last lookahead
-        DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_free_main[pair_buf(s)], 0));
-        DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_free_panel[pair_buf(s)], 0));
+        DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_packed[s & 1][c], 0));
+    } else if (c == 0 && s % d->D == 0) {  // the buffer's previous group: its last bulk update and lookahead
+        DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_free_main[group_buf(d, s)], 0));
+        DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_free_panel[group_buf(d, s)], 0));
     }
     if (stream) *stream = d->s_comm;
     return 0;
 }
 
-// The broadcast of panel s is enqueued on the comm stream: later readers wait for it.
-int gaplac_dist_comm_end(gaplac_dist* d, int32_t s) {
-    if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "comm_end: step %d out of range", s);
-    DCK(d, hipSetDevice(d->device));
-    DCK(d, hipEventRecord(d->ev_recv[s & 1], d->s_comm));
+int gaplac_dist_comm_begin(gaplac_dist* d, int32_t s, void** stream) {
+    if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "comm_begin: step %d out of range", s);
+    int rc = gaplac_dist_comm_begin_chunk(d, s, 0, stream);
+    if (rc || !owns(d, s)) return rc;
+    for (int c = 1; c < nchunks(d, s); ++c) DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_packed[s & 1][c], 0));
     return 0;
 }
 
-// Bulk trailing update with panel s of this rank's SPs > s+1 (s_main), or with paired
-// updates (pair_step): a deferring step s updates SPs s+2, s+3 only; step s+1 updates SP
-// s+3 with panel s+1 and the SPs >= s+4 with panels s, s+1 (one K = 256 W launch).
+// The broadcast of chunk c of panel s is enqueued on the comm stream: later readers wait for it.
+int gaplac_dist_comm_end_chunk(gaplac_dist* d, int32_t s, int32_t c) {
+    if (!d || s < 0 || s >= d->nsp || c < 0 || c >= nchunks(d, s))
+        return derr(d, GAPLAC_E_ARG, "comm_end: step %d chunk %d out of range", s, c);
+    DCK(d, hipSetDevice(d->device));
+    DCK(d, hipEventRecord(d->ev_recv[s & 1][c], d->s_comm));
+    if (c == nchunks(d, s) - 1) DCK(d, hipEventRecord(d->ev_free_comm[group_buf(d, s)], d->s_comm));
+    return 0;
+}
+
+int gaplac_dist_comm_end(gaplac_dist* d, int32_t s) {
+    if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "comm_end: step %d out of range", s);
+    for (int c = 0; c < nchunks(d, s); ++c) {
+        int rc = gaplac_dist_comm_end_chunk(d, s, c);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+// Bulk trailing update of step s (s_main) following the step plan: SP s+2 first, then
+// ev_step, then the rest (a deferring step: SP s+3's band; otherwise the suffix).
 int gaplac_dist_update(gaplac_dist* d, int32_t s) {
     if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "update: step %d out of range", s);
     DCK(d, hipSetDevice(d->device));
-    DCK(d, hipStreamWaitEvent(d->s_main, d->ev_recv[s & 1], 0));
-    const bool defer = pair_step(d, s), paired = s >= 1 && pair_step(d, s - 1);
+    const int last = nchunks(d, s) - 1;
+    // the owner reads its own packed panel (its broadcast may still be running); the
+    // others wait for the whole panel to arrive. Panels before s were waited for by the
+    // updates before this one on the same stream.
+    DCK(d, hipStreamWaitEvent(d->s_main, owns(d, s) ? d->ev_packed[s & 1][last] : d->ev_recv[s & 1][last], 0));
+    if (d->alone && d->nranks > 1 && s + 1 < d->nsp && owns(d, s + 1))
+        DCK(d, hipStreamWaitEvent(d->s_main, d->ev_panel_done, 0));  // factor(s+1), enqueued just before
+    stamp(d, d->s_main, st_upd(s));
+    if (d->stamps) DCK(d, hipEventRecord(d->ev_upd[s & 1], d->s_main));
     // owned-SP ordinal of the first owned SP >= g
     auto ord_from = [&](int g) {
         const int rel = g - d->rank;
         return rel <= 0 ? 0 : (rel + d->nranks - 1) / d->nranks;
     };
+    // this rank runs a chain beside the update when it owns SP s+1 (factor(s+1) runs now)
+    const bool chain_beside = s + 1 < d->nsp && owns(d, s + 1);
     auto launch = [&](const uint32_t* tiles, int cnt, const Panel& pn, int kd) -> int {
         if (cnt <= 0) return 0;
         BulkArgs ba{d->C, d->Np, pn, tiles, cnt, kd, 0, 0, cmap(d)};
         ba.max_r = d->nt - 1;    // list entries: global row block
         ba.max_c = d->nloc - 1;  //              and local tile column
+        if (d->big_mode == 0) ba.big = 0;
+        else if (d->big_mode == 1) ba.big = (!chain_beside && cnt >= d->big_min) ? 1 : 0;
         DistGuard guard(d);
         launch_bulk(d->s_main, ba, nullptr);
         return guard.check();
     };
-    auto band = [&](int g, const Panel& pn, int kd) -> int {  // SP g alone, if owned
-        if (g >= d->nsp || !owns(d, g)) return 0;
-        const size_t u = (size_t)(g / d->nranks);
-        return launch(d->tiles + d->band_off[u], d->band_cnt[u], pn, kd);
+    auto kdepth = [&](int pf, int pl) {
+        int k = 0;
+        for (int q = pf; q <= pl; ++q) k += sp_width(d, q) * NB;
+        return k;
     };
-    auto suffix = [&](int g, const Panel& pn, int kd) -> int {  // owned SPs >= g
-        const int u = ord_from(g);
-        if (u >= (int)d->bulk_cnt.size()) return 0;
-        return launch(d->tiles + d->bulk_off[(size_t)u], d->bulk_cnt[(size_t)u], pn, kd);
-    };
-    const int kd = sp_width(d, s) * NB;
     int rc;
-    if (defer) {
-        if ((rc = band(s + 2, panel_of(d, s), kd)) || (rc = band(s + 3, panel_of(d, s), kd))) return rc;
-    } else if (paired) {
-        DCK(d, hipStreamWaitEvent(d->s_main, d->ev_recv[(s - 1) & 1], 0));
-        if ((rc = band(s + 2, panel_of(d, s), kd))) return rc;
-        if ((rc = suffix(s + 3, panel_of(d, s - 1), sp_width(d, s - 1) * NB + kd))) return rc;
-    } else {
-        if ((rc = suffix(s + 2, panel_of(d, s), kd))) return rc;
+    for (const DOp& op : d->plan[(size_t)s]) {
+        if (op.kind == OP_MARK) {
+            stamp(d, d->s_main, st_band(s));
+            DCK(d, hipEventRecord(d->ev_step[s & 1], d->s_main));
+            continue;
+        }
+        const Panel pn = panel_of(d, op.pf);
+        const int kd = kdepth(op.pf, op.pl);
+        if (op.kind == OP_BAND) {
+            if (op.g >= d->nsp || !owns(d, op.g)) continue;
+            const size_t u = (size_t)(op.g / d->nranks);
+            if ((rc = launch(d->tiles + d->band_off[u], d->band_cnt[u], pn, kd))) return rc;
+        } else {
+            const int u = ord_from(op.g);
+            if (u >= (int)d->bulk_cnt.size()) continue;
+            if ((rc = launch(d->tiles + d->bulk_off[(size_t)u], d->bulk_cnt[(size_t)u], pn, kd))) return rc;
+        }
     }
-    DCK(d, hipEventRecord(d->ev_step[s & 1], d->s_main));
-    // the pair's last bulk reader: its odd step (or an even step with no odd partner)
-    if ((s & 1) || s + 1 >= d->nsp) DCK(d, hipEventRecord(d->ev_free_main[pair_buf(s)], d->s_main));
+    stamp(d, d->s_main, st_end(s));
+    // the group's last bulk reader: its last step (or the last step of all)
+    if (s % d->D == d->D - 1 || s + 1 >= d->nsp)
+        DCK(d, hipEventRecord(d->ev_free_main[group_buf(d, s)], d->s_main));
     DCK(d, hipGetLastError());
     return 0;
 }
@@ -551,6 +841,154 @@ int gaplac_dist_local(gaplac_dist* d, double* out, int64_t ld) {
     if (d->nloc > 0)
         DCK(d, hipMemcpy2D(out, (size_t)ld * 8, d->C, (size_t)d->Np * 8, (size_t)d->Np * 8, (size_t)d->nloc * NB,
                            hipMemcpyDeviceToHost));
+    return 0;
+}
+
+// Host-only check of the step plan for nt tile columns (no HIP calls): every super-panel
+// gets every earlier panel exactly once, in order, before its chain; returns 0 or
+// GAPLAC_E_ARG with the first violation in msg. *out_ops: the plan's bulk launches per rank
+// count (bands + suffixes), for tests.
+int gaplac_dist_plan_check(int32_t nt, int32_t spw, int32_t depth, int32_t pair_m, int64_t* out_ops, char* msg,
+                           int64_t msglen) {
+    if (nt < 1 || spw < 1 || spw > MAXC || depth < 1 || depth > 8) return GAPLAC_E_ARG;
+    const int nsp = (nt + spw - 1) / spw;
+    const auto plan = build_plan(nsp, nt, spw, depth, pair_m);
+    std::string why;
+    const bool ok = check_plan(plan, nsp, depth, &why);
+    if (out_ops) {
+        int64_t n = 0;
+        for (const auto& ops : plan)
+            for (const DOp& op : ops) n += op.kind != OP_MARK;
+        *out_ops = n;
+    }
+    if (msg && msglen > 0) {
+        std::snprintf(msg, (size_t)msglen, "%s", why.c_str());
+    }
+    return ok ? 0 : GAPLAC_E_ARG;
+}
+
+// The step plan itself (host-only): per op (step, kind, g, pf, pl) as 5 int32 into out
+// (cap ints); *out_n = number of ops. kind: 0 band of SP g, 1 every SP >= g, 2 mark.
+int gaplac_dist_plan(int32_t nt, int32_t spw, int32_t depth, int32_t pair_m, int32_t* out, int64_t cap,
+                     int64_t* out_n) {
+    if (nt < 1 || spw < 1 || spw > MAXC || depth < 1 || depth > 8 || !out_n) return GAPLAC_E_ARG;
+    const int nsp = (nt + spw - 1) / spw;
+    const auto plan = build_plan(nsp, nt, spw, depth, pair_m);
+    int64_t n = 0;
+    for (int p = 0; p < nsp; ++p)
+        for (const DOp& op : plan[(size_t)p]) {
+            if (out && 5 * (n + 1) <= cap) {
+                int32_t* o = out + 5 * n;
+                o[0] = p;
+                o[1] = op.kind;
+                o[2] = op.g;
+                o[3] = op.pf;
+                o[4] = op.pl;
+            }
+            ++n;
+        }
+    *out_n = n;
+    return 0;
+}
+
+// ---- replay of one rank's schedule on one GPU (diagnostics) ----
+
+// Turn the device timestamps on for the next evaluation of order N (allocate and zero
+// them; N = 0: off), before gaplac_dist_begin; gaplac_dist_replay_stamps copies them out
+// (ticks of 10 ns): nsp x ST_PER_STEP per-step stamps, then the end of the rank's Gram.
+int gaplac_dist_replay_enable(gaplac_dist* d, int64_t N) {
+    if (!d || N < 0) return GAPLAC_E_ARG;
+    DCK(d, hipSetDevice(d->device));
+    if (N == 0) {
+        if (d->stamps) (void)hipFree(d->stamps);
+        d->stamps = nullptr;
+        d->stamps_elems = 0;
+        return 0;
+    }
+    int32_t nsp = 0;
+    gaplac_dist_geometry(d, N, nullptr, nullptr, &nsp, nullptr, nullptr);
+    int rc;
+    if ((rc = dgrow(d, &d->stamps, &d->stamps_elems, (size_t)nsp * ST_PER_STEP + 1))) return rc;
+    DCK(d, hipMemsetAsync(d->stamps, 0, d->stamps_elems * 8, d->s_main));
+    DCK(d, hipStreamSynchronize(d->s_main));
+    return 0;
+}
+
+int gaplac_dist_replay_stamps(gaplac_dist* d, uint64_t* out, int64_t n) {
+    if (!d || !d->stamps || !out || n < (int64_t)d->nsp * ST_PER_STEP + 1 ||
+        d->stamps_elems < (size_t)d->nsp * ST_PER_STEP + 1)
+        return derr(d, GAPLAC_E_ARG, "stamps: bad output");
+    DCK(d, hipSetDevice(d->device));
+    DCK(d, hipMemcpy(out, d->stamps, ((size_t)d->nsp * ST_PER_STEP + 1) * 8, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+// Modelled transfer of chunk c of panel s on this rank's comm stream, in place of the
+// broadcast. Arrival = max(owner ready + F, previous chunk's arrival) + transfer, where
+//   owner ready = max(RECV(s-1, last), UPD(s-2) + band_ticks)    (the owner's chain inputs)
+//   F = the owner's chain until the chunk is packed (f_ticks), transfer = lat + bytes / BW
+// for a panel of another rank (src: the owner's context, factored: its columns are copied
+// after the wait, and copy_ticks of that copy are taken off the wait), and
+//   arrival = max(PACK(s, c) + lat, RECV(s, c-1)) + bytes / BW
+// for this rank's own panel (its send). Then comm_end_chunk(s, c).
+int gaplac_dist_replay_chunk(gaplac_dist* d, const gaplac_dist* src, int32_t s, int32_t c, int64_t f_ticks,
+                             int64_t band_ticks, int64_t lat_ticks, int64_t xfer_ticks, int64_t copy_ticks) {
+    if (!d || !d->stamps || s < 0 || s >= d->nsp || c < 0 || c >= nchunks(d, s))
+        return derr(d, GAPLAC_E_ARG, "replay: step %d chunk %d (stamps %s)", s, c, d && d->stamps ? "on" : "off");
+    void* st = nullptr;
+    int rc;
+    if ((rc = gaplac_dist_comm_begin_chunk(d, s, c, &st))) return rc;
+    Release r{{-1, -1, -1}, {0, 0, 0}, st_recv(s, c)};
+    if (owns(d, s)) {
+        r.dep[0] = st_pack(s, c);
+        r.add[0] = lat_ticks + xfer_ticks;
+        if (c > 0) {
+            r.dep[1] = st_recv(s, c - 1);
+            r.add[1] = xfer_ticks;
+        }
+    } else {
+        if (!src || src->Np != d->Np || src->W != d->W || src->nranks != d->nranks || src->rank != s % d->nranks)
+            return derr(d, GAPLAC_E_ARG, "replay: source context is not the owner of panel %d", s);
+        const long long wait = f_ticks + lat_ticks + xfer_ticks - copy_ticks;
+        if (s == 0) {  // the owner's chain starts after its Gram (taken as long as this rank's)
+            DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_gram, 0));
+            r.dep[0] = -2;
+            r.add[0] = wait;
+        } else {
+            r.dep[0] = st_recv(s - 1, nchunks(d, s - 1) - 1);
+            r.add[0] = wait;
+        }
+        if (s >= 2) {
+            DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_upd[s & 1], 0));  // update(s-2) started
+            r.dep[1] = st_upd(s - 2);
+            r.add[1] = band_ticks + wait;
+        }
+        if (c > 0) {
+            r.dep[2] = st_recv(s, c - 1);
+            r.add[2] = xfer_ticks - copy_ticks;
+        }
+    }
+    if (guard_launch("release_kernel")) release_kernel<<<dim3(1), dim3(64), 0, d->s_comm>>>(d->stamps, r);
+    if (!owns(d, s)) {
+        const int lc0 = sp_local(src, s) + chunk_col0(d, c), ncol = chunk_cols(d, s, c);
+        const int64_t r0 = panel_row0(d, s);
+        double* dst = const_cast<double*>(chunk_panel(d, s, c).P) + (r0 - group_row0(d, s));
+        DCK(d, hipMemcpy2DAsync(dst, (size_t)group_ld(d, s) * 8, src->C + (int64_t)lc0 * NB * src->Np + r0,
+                                (size_t)src->Np * 8, (size_t)(d->Np - r0) * 8, (size_t)ncol * NB,
+                                hipMemcpyDeviceToDevice, d->s_comm));
+        stamp(d, d->s_comm, st_pack(s, c));  // a non-owner's PACK slot: the copy's end
+    }
+    return gaplac_dist_comm_end_chunk(d, s, c);
+}
+
+// Bytes of chunk c of panel s that a broadcast must move (rows from the panel's first
+// row; the replay's transfer model) and the per-step stamp layout.
+int gaplac_dist_replay_info(gaplac_dist* d, int32_t s, int32_t c, int64_t* bytes, int32_t* per_step,
+                            int32_t* maxc) {
+    if (!d || s < 0 || s >= d->nsp || c < 0 || c >= nchunks(d, s)) return derr(d, GAPLAC_E_ARG, "replay_info");
+    if (bytes) *bytes = chunk_bytes_useful(d, s, c);
+    if (per_step) *per_step = ST_PER_STEP;
+    if (maxc) *maxc = MAXC;
     return 0;
 }
 

@@ -80,6 +80,10 @@ struct BulkArgs {
     int max_r = -1, max_c = -1;  // largest lo16 / hi16 list entry (-1: an m x m triangle list)
     int whole = 0;    // 1: a band list as 128x128 tile workgroups (tile_band_kernel), never quadrants
     int tile_min = 0;  // > 0: at least this many tiles go to tile_syrk_kernel even below the quadrant limit
+    // large-launch kernel (tile_syrk_big_kernel, three workgroups per CU): -1 by launch size
+    // (>= BULK_BIG_TILES tiles), 0 never, 1 the caller chose it (a distributed rank with no
+    // chain beside this launch); quadrant-sized launches never take it
+    int big = -1;
 };
 
 // Persistent tail (gaplac_kernels.hip tail_kernel): completion counters of

@@ -2994,7 +2994,7 @@ void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt) {
         quad_bulk_kernel<<<dim3((unsigned)(4 * grid)), dim3(256), 0, s>>>(a, kt);
     else if (a.whole)
         tile_band_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
-    else if (a.ntiles >= BULK_BIG_TILES && bulk_big_enabled())
+    else if (bulk_big_enabled() && (a.big > 0 || (a.big < 0 && a.ntiles >= BULK_BIG_TILES)))
         tile_syrk_big_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);
     else
         tile_syrk_kernel<<<dim3((unsigned)grid), dim3(256), 0, s>>>(a, kt);

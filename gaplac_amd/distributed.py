@@ -23,6 +23,9 @@ Schedule (per rank; every library call only enqueues work except finish):
     begin; factor(0) [owner]; bcast(0)
     for s in 0..nsp-1: factor(s+1) [owner of s+1]; update(s); bcast(s+1)
     finish -> partial (logdet, quad, info); combine across ranks
+bcast(s) is one broadcast per chunk of panel s (a run of its tile columns): the owner packs
+a chunk as soon as its last column is final, and the next owner's lookahead consumes it as
+it arrives.
 """
 from __future__ import annotations
 
@@ -44,7 +47,8 @@ DEFAULT_SPW = 4
 class DistRank:
     """One rank's state (a gaplac_dist context) on `device`."""
 
-    def __init__(self, device: int, nranks: int, rank: int, spw: int = DEFAULT_SPW):
+    def __init__(self, device: int, nranks: int, rank: int, spw: int = DEFAULT_SPW, depth: int = -1,
+                 chunk: int = -1, big: int = -1, big_min: int = -1, alone: int = -1):
         self.lib = _native.load()
         h = c_void_p()
         rc = self.lib.gaplac_dist_create(int(device), int(nranks), int(rank), int(spw), byref(h))
@@ -53,6 +57,17 @@ class DistRank:
         self.h = h
         self.device, self.nranks, self.rank, self.spw = device, nranks, rank, spw
         self._bufs = None  # torch tensors backing the panel buffers (kept alive here)
+        self.configure(depth, chunk, big, big_min, alone)
+
+    def configure(self, depth: int = -1, chunk: int = -1, big: int = -1, big_min: int = -1, alone: int = -1):
+        """Schedule options (gaplac_dist_configure; -1 keeps the current value): deferral
+        depth, tile columns per broadcast chunk, bulk kernel choice (2 for ranks sharing one
+        device, as LoopbackTransport's do), chain alone (the bulk update waits while this
+        rank factors the next super-panel; 0 for ranks sharing one device)."""
+        if self._bufs is not None and depth != -1:
+            raise ArgumentError("configure the depth before the panel buffers are set")
+        self._check(self.lib.gaplac_dist_configure(self.h, int(depth), int(chunk), int(big), int(big_min),
+                                                   int(alone)))
 
     def close(self):
         if getattr(self, "h", None):
@@ -143,6 +158,28 @@ class DistRank:
     def comm_end(self, s: int):
         self._check(self.lib.gaplac_dist_comm_end(self.h, int(s)))
 
+    def chunks(self, s: int) -> int:
+        n = c_int32()
+        self._check(self.lib.gaplac_dist_chunks(self.h, int(s), byref(n)))
+        return n.value
+
+    def panel_chunk(self, s: int, c: int):
+        ptr, count, root = c_void_p(), c_int64(), c_int32()
+        self._check(self.lib.gaplac_dist_panel_chunk(self.h, int(s), int(c), byref(ptr), byref(count), byref(root)))
+        return ptr.value, count.value, root.value
+
+    def chunk_tensor(self, s: int, c: int):
+        ptr, count, _root = self.panel_chunk(s, c)
+        return self.panel_tensor(s, count, ptr)
+
+    def comm_begin_chunk(self, s: int, c: int) -> int:
+        st = c_void_p()
+        self._check(self.lib.gaplac_dist_comm_begin_chunk(self.h, int(s), int(c), byref(st)))
+        return st.value or 0
+
+    def comm_end_chunk(self, s: int, c: int):
+        self._check(self.lib.gaplac_dist_comm_end_chunk(self.h, int(s), int(c)))
+
     def update(self, s: int):
         self._check(self.lib.gaplac_dist_update(self.h, int(s)))
 
@@ -191,26 +228,28 @@ class TorchTransport:
         return tot
 
     def bcast(self, ranks: Sequence, s: int):
+        """One broadcast per chunk of panel s, each on the library's comm stream."""
         import torch
         import torch.distributed as dist
         (r,) = ranks
-        ptr, count, root = r.panel(s)
-        stream = r.comm_begin(s)
-        buf = r.panel_tensor(s, count, ptr)
-        src = dist.get_global_rank(self.group, root) if self.group is not None else root
-        if stream and buf.is_cuda:
-            st = torch.cuda.ExternalStream(stream, device=buf.device)
-            with torch.cuda.stream(st):
-                if self.timing:
-                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                    ev[0].record(st)
-                dist.broadcast(buf, src=src, group=self.group, async_op=True).wait()
-                if self.timing:
-                    ev[1].record(st)
-                    self._ev.append(ev)
-        else:
-            dist.broadcast(buf, src=src, group=self.group)
-        r.comm_end(s)
+        for c in range(r.chunks(s)):
+            _ptr, _count, root = r.panel_chunk(s, c)
+            stream = r.comm_begin_chunk(s, c)
+            buf = r.chunk_tensor(s, c)
+            src = dist.get_global_rank(self.group, root) if self.group is not None else root
+            if stream and buf.is_cuda:
+                st = torch.cuda.ExternalStream(stream, device=buf.device)
+                with torch.cuda.stream(st):
+                    if self.timing:
+                        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                        ev[0].record(st)
+                    dist.broadcast(buf, src=src, group=self.group, async_op=True).wait()
+                    if self.timing:
+                        ev[1].record(st)
+                        self._ev.append(ev)
+            else:
+                dist.broadcast(buf, src=src, group=self.group)
+            r.comm_end_chunk(s, c)
 
     def combine(self, parts: Sequence, device=None):
         import torch
@@ -238,31 +277,62 @@ class LoopbackTransport:
 
     def prepare(self, ranks: Sequence, N: int):
         for r in ranks:
+            if len(ranks) > 1 and hasattr(r, "configure"):
+                r.configure(big=2, alone=0)  # the ranks share one device: the single-GPU choices
             r.use_torch_panel_buffers(N)
 
     def bcast(self, ranks: Sequence, s: int):
         import torch
-        _p, count, root = ranks[0].panel(s)
+        root = s % ranks[0].nranks
         rootr = next(r for r in ranks if r.rank == root)
-        streams = {r.rank: torch.cuda.ExternalStream(r.comm_begin(s), device=torch.device("cuda", r.device))
-                   for r in ranks}
-        src = rootr.panel_tensor(s, count)
-        for r in ranks:
-            if r.rank == root:
-                continue
-            st = streams[r.rank]
-            st.wait_stream(streams[root])
-            with torch.cuda.stream(st):
-                r.panel_tensor(s, count).copy_(src, non_blocking=True)
-            streams[root].wait_stream(st)
-        for r in ranks:
-            r.comm_end(s)
+        for c in range(rootr.chunks(s)):
+            streams = {r.rank: torch.cuda.ExternalStream(r.comm_begin_chunk(s, c), device=torch.device("cuda", r.device))
+                       for r in ranks}
+            src = rootr.chunk_tensor(s, c)
+            for r in ranks:
+                if r.rank == root:
+                    continue
+                st = streams[r.rank]
+                st.wait_stream(streams[root])
+                with torch.cuda.stream(st):
+                    r.chunk_tensor(s, c).copy_(src, non_blocking=True)
+                streams[root].wait_stream(st)
+            for r in ranks:
+                r.comm_end_chunk(s, c)
 
     def combine(self, parts: Sequence, device=None):
         ld = sum(p[0] for p in parts)
         q = sum(p[1] for p in parts)
         infos = [p[2] for p in parts if p[2] > 0]
         return ld, q, (min(infos) if infos else 0)
+
+
+def plan(nt: int, spw: int, depth: int, pair_m: int = 40):
+    """The library's step plan (gaplac_dist_plan, host-only): a list per step of
+    (kind, sp, first panel, last panel), kind 0 = that SP, 1 = every SP from it on, 2 = the
+    step's event once SP step+2 is up to date."""
+    lib = _native.load()
+    n = c_int64()
+    rc = lib.gaplac_dist_plan(int(nt), int(spw), int(depth), int(pair_m), None, 0, byref(n))
+    if rc != 0:
+        raise ArgumentError(f"gaplac_dist_plan({nt}, {spw}, {depth}) failed: {rc}")
+    buf = (c_int32 * (5 * max(1, n.value)))()
+    lib.gaplac_dist_plan(int(nt), int(spw), int(depth), int(pair_m), buf, 5 * n.value, byref(n))
+    nsp = (nt + spw - 1) // spw
+    steps = [[] for _ in range(nsp)]
+    for i in range(n.value):
+        p, kind, g, pf, pl = buf[5 * i:5 * i + 5]
+        steps[p].append((kind, g, pf, pl))
+    return steps
+
+
+def plan_check(nt: int, spw: int, depth: int, pair_m: int = 40):
+    """gaplac_dist_plan_check: (ok, op count, message)."""
+    lib = _native.load()
+    ops = c_int64()
+    msg = ctypes.create_string_buffer(256)
+    rc = lib.gaplac_dist_plan_check(int(nt), int(spw), int(depth), int(pair_m), byref(ops), msg, 256)
+    return rc == 0, ops.value, msg.value.decode()
 
 
 def run_schedule(ranks: Sequence, transport, nsp: int):

@@ -257,10 +257,16 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
  *   gaplac_dist_finish(d, &logdet_part, &quad_part, &info_part)
  *   allreduce: logdet = sum, quad = sum, info = min over nonzero; then
  *   logpdf = -(N*log(2*pi) + logdet + quad) / 2   (NaN / PosDefException if info > 0)
- * where bcast(s) = gaplac_dist_panel(d, s, &buf, &count, &root);
- *                  gaplac_dist_comm_begin(d, s, &stream);
- *                  ncclBroadcast(buf, buf, count, ncclDouble, root, comm, stream);
- *                  gaplac_dist_comm_end(d, s);
+ * where bcast(s) = gaplac_dist_chunks(d, s, &nc);
+ *                  for c in 0..nc-1:
+ *                      gaplac_dist_panel_chunk(d, s, c, &buf, &count, &root);
+ *                      gaplac_dist_comm_begin_chunk(d, s, c, &stream);
+ *                      ncclBroadcast(buf, buf, count, ncclDouble, root, comm, stream);
+ *                      gaplac_dist_comm_end_chunk(d, s, c);
+ * A chunk is a run of the panel's tile columns (gaplac_dist_configure): its owner packs it
+ * as soon as its last column is final and the next owner's lookahead consumes it as it
+ * arrives, so broadcasts overlap both chains. The whole panel as one
+ * broadcast (gaplac_dist_panel / _comm_begin / _comm_end) is the one-chunk case.
  * ---------------------------------------------------------------------------------- */
 typedef struct gaplac_dist gaplac_dist;
 int gaplac_dist_create(int device, int nranks, int rank, int spw, gaplac_dist** out);
@@ -278,7 +284,21 @@ int gaplac_dist_set_panel_buffers(gaplac_dist* d, void* buf0, void* buf1, int64_
 int gaplac_dist_begin(gaplac_dist* d, int64_t N, int32_t D, const double* X, int64_t ldx,
                       int32_t T, const gaplac_term* terms, double noise, const double* v,
                       int inputs_on_device, int32_t* out_nsp);
+/* Schedule options, before gaplac_dist_set_panel_buffers / begin (< 0 keeps the current
+ * value; defaults from GAPLAC_DIST_DEPTH / _CHUNK / _BIG / _BIG_MIN / _ALONE): depth =
+ * super-panels per deferred bulk update (1..8), chunk = tile columns per broadcast chunk
+ * (1..spw), big = bulk kernel choice (0: never the large-launch kernel; 1: per rank,
+ * launches of >= big_min tiles while this rank runs no chain; 2: by launch size, as on one
+ * GPU — for ranks that share one device), alone = 1: a rank's bulk update waits while it
+ * factors the next super-panel (the chain gets the whole GPU). */
+int gaplac_dist_configure(gaplac_dist* d, int32_t depth, int32_t chunk, int32_t big, int32_t big_min,
+                          int32_t alone);
 int gaplac_dist_factor(gaplac_dist* d, int32_t s);   /* owner of super-panel s only */
+int gaplac_dist_chunks(gaplac_dist* d, int32_t s, int32_t* out_chunks);
+int gaplac_dist_panel_chunk(gaplac_dist* d, int32_t s, int32_t c, void** buf, int64_t* count,
+                            int32_t* root);
+int gaplac_dist_comm_begin_chunk(gaplac_dist* d, int32_t s, int32_t c, void** hip_stream);
+int gaplac_dist_comm_end_chunk(gaplac_dist* d, int32_t s, int32_t c);
 int gaplac_dist_panel(gaplac_dist* d, int32_t s, void** buf, int64_t* count, int32_t* root);
 int gaplac_dist_comm_begin(gaplac_dist* d, int32_t s, void** hip_stream);
 int gaplac_dist_comm_end(gaplac_dist* d, int32_t s);
@@ -287,6 +307,27 @@ int gaplac_dist_update(gaplac_dist* d, int32_t s);
 int gaplac_dist_finish(gaplac_dist* d, double* logdet_part, double* quad_part, int64_t* info_part);
 /* Debug / parity: this rank's column storage (Np x nloc*128, column-major) to host. */
 int gaplac_dist_local(gaplac_dist* d, double* out, int64_t ld);
+/* Host-only (no HIP calls): checks the step plan for nt tile columns — every super-panel
+ * gets every earlier panel once, in order, before its chain. 0 or GAPLAC_E_ARG (msg). */
+int gaplac_dist_plan_check(int32_t nt, int32_t spw, int32_t depth, int32_t pair_m, int64_t* out_ops,
+                           char* msg, int64_t msglen);
+/* Host-only: the plan's ops as (step, kind, sp, first panel, last panel) int32 quintuples
+ * (kind 0: that super-panel, 1: every super-panel from it on, 2: the step's event after
+ * super-panel step+2 is up to date); *out_n = op count, out may be NULL. */
+int gaplac_dist_plan(int32_t nt, int32_t spw, int32_t depth, int32_t pair_m, int32_t* out, int64_t cap,
+                     int64_t* out_n);
+/* Replay of one rank's schedule on one GPU (diagnostics): the other ranks'
+ * panels arrive as copies from their (already factored) contexts on a modelled timeline.
+ * replay_enable(N) before begin turns device timestamps on (0: off); replay_chunk replaces bcast's
+ * broadcast of one chunk (times in 10 ns ticks); replay_stamps copies the timestamps out;
+ * replay_info: a chunk's bytes and the stamp layout. Not in the reference. */
+int gaplac_dist_replay_enable(gaplac_dist* d, int64_t N);
+int gaplac_dist_replay_chunk(gaplac_dist* d, const gaplac_dist* owner, int32_t s, int32_t c,
+                             int64_t f_ticks, int64_t band_ticks, int64_t lat_ticks,
+                             int64_t xfer_ticks, int64_t copy_ticks);
+int gaplac_dist_replay_stamps(gaplac_dist* d, uint64_t* out, int64_t n);
+int gaplac_dist_replay_info(gaplac_dist* d, int32_t s, int32_t c, int64_t* bytes, int32_t* per_step,
+                            int32_t* maxc);
 
 #ifdef __cplusplus
 }

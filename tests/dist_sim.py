@@ -1,22 +1,27 @@
 """CPU test double of one distributed rank (the gaplac_dist_* step contract), in numpy.
 
 It implements the same per-rank contract as gaplac_amd.distributed.DistRank (ownership,
-local column storage, panel buffer geometry and parity, lookahead in factor(s+1), bulk
-update of super-panels > s+1) with a smaller tile edge, so the orchestration in
-gaplac_amd/distributed.py (schedule order, broadcast roots and counts, the combine) runs
-end to end under a gloo process group on CPU. Test infrastructure only; the Gram comes
-from the oracle restatement.
+local column storage, group panel buffers of `depth` panels with their geometry and
+parity, broadcast chunks of `chunk` tile columns, the lookahead in factor(s+1), and the
+bulk updates of the library's own step plan, gaplac_dist_plan) with a smaller tile edge, so
+the orchestration in gaplac_amd/distributed.py (schedule order, per-chunk broadcast roots
+and counts, the combine) runs end to end under a gloo process group on CPU. Test
+infrastructure only; the Gram comes from the oracle restatement.
 """
 import numpy as np
 
+from gaplac_amd import distributed as DI
 from oracle import restatement as R
 
 
 class SimRank:
-    def __init__(self, nranks: int, rank: int, spw: int = 2, nb: int = 16):
+    def __init__(self, nranks: int, rank: int, spw: int = 2, nb: int = 16, depth: int = 2, chunk: int = None,
+                 pair_m: int = 2):
         self.nranks, self.rank, self.spw, self.nb = nranks, rank, spw, nb
+        self.depth, self.cw, self.pair_m = depth, (chunk or spw), pair_m
         self.device = None
         self._bufs = None
+        self.applied = None  # per local tile column: panels applied, in order (checked by tests)
 
     def owns(self, s):
         return s % self.nranks == self.rank
@@ -27,15 +32,55 @@ class SimRank:
         nt = Np // nb
         nsp = (nt + W - 1) // W
         nloc = sum(min(W, nt - s * W) for s in range(self.rank, nsp, self.nranks))
-        return dict(Np=Np, nt=nt, nsp=nsp, nloc=nloc, panel_elems=Np * min(W, nt) * nb)
+        return dict(Np=Np, nt=nt, nsp=nsp, nloc=nloc, panel_elems=Np * min(self.depth * W, nt) * nb)
 
     def use_torch_panel_buffers(self, N):
         import torch
         need = self.geometry(N)["panel_elems"]
         self._bufs = [torch.zeros(need, dtype=torch.float64) for _ in range(2)]
 
+    # ---- panel geometry (gaplac_dist.hip: group_* / chunk_*)
+    def _width(self, s):
+        return min(self.spw, self.nt - s * self.spw)
+
+    def _group(self, s):
+        g0 = s // self.depth * self.depth
+        origin = g0 * self.spw * self.nb
+        return g0, origin, self.Np - origin
+
+    def _group_view(self, s):
+        """Column-major view of panel s's group buffer: [row - origin, panel column]."""
+        g0, origin, ld = self._group(s)
+        buf = self._bufs[(s // self.depth) & 1]
+        ncol = buf.numel() // ld
+        return buf[:ld * ncol].numpy().reshape(ncol, ld).T, g0, origin
+
+    def chunks(self, s):
+        return (self._width(s) + self.cw - 1) // self.cw
+
+    def _chunk_range(self, s, c):
+        """(offset, count) of chunk c of panel s in its group buffer."""
+        g0, origin, ld = self._group(s)
+        r0 = s * self.spw * self.nb
+        col0 = (s - g0) * self.spw * self.nb + c * self.cw * self.nb
+        ncols = min(self.cw, self._width(s) - c * self.cw) * self.nb
+        return col0 * ld + (r0 - origin), ncols * ld - (r0 - origin)
+
+    def panel_chunk(self, s, c):
+        return None, self._chunk_range(s, c)[1], s % self.nranks
+
+    def chunk_tensor(self, s, c):
+        off, count = self._chunk_range(s, c)
+        return self._bufs[(s // self.depth) & 1][off:off + count]
+
     def panel_tensor(self, s, count, ptr=None):
-        return self._bufs[s & 1][:count]
+        raise AssertionError("the transports address panels by chunk")
+
+    def comm_begin_chunk(self, s, c):
+        return 0
+
+    def comm_end_chunk(self, s, c):
+        pass
 
     # global tile column of local tile column lj (ColMap::global)
     def gcol(self, lj):
@@ -54,30 +99,33 @@ class SimRank:
             bj = self.gcol(lj)
             self.C[:, lj * nb:(lj + 1) * nb] = A[:, bj * nb:(bj + 1) * nb]
         self.info = 0
+        self.plan = DI.plan(self.nt, self.spw, self.depth, self.pair_m)
+        self.applied = [[] for _ in range(self.nloc)]
         return self.nsp
 
-    def _panel(self, s):
-        W, nb = self.spw, self.nb
-        w = min(W, self.nt - s * W)
-        r0 = s * W * nb
-        ldp = self.Np - r0
-        P = self._bufs[s & 1][:ldp * w * nb].numpy().reshape(w * nb, ldp).T  # column-major view
-        return P, r0
-
-    def _apply(self, s, lj0, ncols):
-        """C[:, local tile cols lj0..lj0+ncols) -= panel s contributions (rows >= column)."""
-        P, r0 = self._panel(s)
-        nb = self.nb
+    def _apply(self, q, lj0, ncols):
+        """C[:, local tile cols lj0..lj0+ncols) -= panel q's contributions (rows >= column)."""
+        P, g0, origin = self._group_view(q)
+        nb, W = self.nb, self.spw
+        c0 = (q - g0) * W * nb
+        Pq = P[:, c0:c0 + self._width(q) * nb]
         for lj in range(lj0, lj0 + ncols):
-            g0 = self.gcol(lj) * nb
-            rows = slice(g0, self.Np)
-            self.C[rows, lj * nb:(lj + 1) * nb] -= P[g0 - r0:, :] @ P[g0 - r0:g0 - r0 + nb, :].T
+            g = self.gcol(lj) * nb
+            rows = slice(g, self.Np)
+            self.C[rows, lj * nb:(lj + 1) * nb] -= Pq[g - origin:, :] @ Pq[g - origin:g - origin + nb, :].T
+            self.applied[lj].append(q)
+
+    def _apply_sp(self, sp, pf, pl):
+        W = self.spw
+        u = sp // self.nranks
+        for q in range(pf, pl + 1):
+            self._apply(q, u * W, min(W, self.nloc - u * W))
 
     def factor(self, s):
         assert self.owns(s)
         W, nb, N = self.spw, self.nb, self.N
         c0 = s * W
-        w = min(W, self.nt - c0)
+        w = self._width(s)
         lc0 = (s // self.nranks) * W
         if s > 0:
             self._apply(s - 1, lc0, w)
@@ -94,29 +142,28 @@ class SimRank:
             B[jj, jj] = d
             B[jj + 1:, jj] /= d
             B[jj + 1:, jj + 1:] -= np.outer(B[jj + 1:, jj], B[jj + 1:w * nb, jj])
-        ldp = self.Np - r0
-        self._bufs[s & 1][:ldp * w * nb] = __import__("torch").from_numpy(np.asfortranarray(B).T.reshape(-1).copy())
-
-    def panel(self, s):
-        W, nb = self.spw, self.nb
-        w = min(W, self.nt - s * W)
-        return None, (self.Np - s * W * nb) * w * nb, s % self.nranks
-
-    def comm_begin(self, s):
-        return 0
-
-    def comm_end(self, s):
-        pass
+        P, g0, origin = self._group_view(s)
+        col0 = (s - g0) * W * nb
+        P[r0 - origin:, col0:col0 + w * nb] = B
 
     def update(self, s):
         W = self.spw
-        for u in range((self.nloc + W - 1) // W):
-            sg = u * self.nranks + self.rank
-            if sg > s + 1:
-                self._apply(s, u * W, min(W, self.nloc - u * W))
+        for kind, g, pf, pl in self.plan[s]:
+            if kind == 0:
+                if g < self.nsp and self.owns(g):
+                    self._apply_sp(g, pf, pl)
+            elif kind == 1:
+                for u in range((self.nloc + W - 1) // W):
+                    sg = u * self.nranks + self.rank
+                    if sg >= g:
+                        self._apply_sp(sg, pf, pl)
 
     def finish(self):
         nb, N = self.nb, self.N
+        # every local column got every earlier panel exactly once, in order
+        for lj in range(self.nloc):
+            sp = self.gcol(lj) // self.spw
+            assert self.applied[lj] == list(range(sp)), (lj, self.applied[lj])
         ld = q = 0.0
         for lj in range(self.nloc):
             for e in range(nb):

@@ -24,11 +24,13 @@ class CpuLoopback(DI.LoopbackTransport):
             r.use_torch_panel_buffers(N)
 
     def bcast(self, ranks, s):
-        _p, count, root = ranks[0].panel(s)
-        src = next(r for r in ranks if r.rank == root).panel_tensor(s, count)
-        for r in ranks:
-            if r.rank != root:
-                r.panel_tensor(s, count).copy_(src)
+        root = s % ranks[0].nranks
+        rootr = next(r for r in ranks if r.rank == root)
+        for c in range(rootr.chunks(s)):
+            src = rootr.chunk_tensor(s, c)
+            for r in ranks:
+                if r.rank != root:
+                    r.chunk_tensor(s, c).copy_(src)
 
 
 def _case(N, seed=0):
@@ -41,10 +43,15 @@ def _case(N, seed=0):
     return X, terms, v
 
 
-@pytest.mark.parametrize("world,spw,N", [(1, 2, 150), (2, 2, 150), (3, 1, 200), (4, 2, 257), (5, 3, 95), (8, 1, 40)])
-def test_loopback_schedule_matches_oracle(world, spw, N):
+@pytest.mark.parametrize("world,spw,N,depth,chunk", [
+    (1, 2, 150, 2, 2), (2, 2, 150, 2, 1), (3, 1, 200, 1, 1), (4, 2, 257, 4, 1), (5, 3, 95, 3, 2), (8, 1, 40, 2, 1),
+    (2, 4, 600, 4, 1), (3, 4, 600, 3, 3), (8, 2, 700, 4, 2), (2, 3, 400, 8, 3)])
+def test_loopback_schedule_matches_oracle(world, spw, N, depth, chunk):
+    """Every rank count / deferral depth / chunk width: the library's step plan applied by
+    the numpy rank double gives every column every panel once, in order (SimRank.finish),
+    and the oracle's logpdf."""
     X, terms, v = _case(N, seed=world)
-    ranks = [SimRank(world, r, spw=spw, nb=16) for r in range(world)]
+    ranks = [SimRank(world, r, spw=spw, nb=16, depth=depth, chunk=chunk) for r in range(world)]
     lp, ld, q = DI.logpdf_dist(ranks, CpuLoopback(), X, terms, 0.1, v, full=True)
     rl, rd, rq = R.logpdf(X, terms, 0.1, v)
     assert abs(lp - rl) <= RTOL * abs(rl)
@@ -88,7 +95,7 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         X, terms, v = _case(230, seed=11)
-        r = SimRank(world, rank, spw=2, nb=16)
+        r = SimRank(world, rank, spw=2, nb=16, depth=4, chunk=1)
         lp, ld, qd = DI.logpdf_dist([r], DI.TorchTransport(), X, terms, 0.1, v, full=True)
         q.put((rank, lp, ld, qd))
     finally:
@@ -111,3 +118,28 @@ def test_gloo_world2_torch_transport():
     for rank, lp, ld, qd in got:
         assert abs(lp - rl) <= RTOL * abs(rl)
     assert got[0][1] == got[1][1]  # every rank returns the same value
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3, 4, 5, 8])
+@pytest.mark.parametrize("spw", [1, 2, 4, 8])
+def test_plan_check_every_size(depth, spw):
+    """gaplac_dist_plan_check over every matrix size up to 600 tile columns (N = 76800) and
+    the deferral cut-offs the library reads (GAPLAC_PAIR_M)."""
+    for pair_m in (0, 8, 40):
+        for nt in range(1, 601):
+            ok, ops, msg = DI.plan_check(nt, spw, depth, pair_m)
+            assert ok, (nt, spw, depth, pair_m, msg)
+
+
+def test_plan_defers_in_groups():
+    """N = 65536 (513 tile columns), W = 4: with depth 4 the suffix updates carry K = 4 x 512
+    while >= 40 tile rows follow, and every step marks SP s+2 before the rest."""
+    steps = DI.plan(513, 4, 4, 40)
+    sufs = [(p, op) for p, ops in enumerate(steps) for op in ops if op[0] == 1]
+    deep = [op for p, op in sufs if op[3] - op[2] == 3]
+    assert len(deep) >= 25
+    for p, ops in enumerate(steps):
+        kinds = [k for k, *_ in ops]
+        assert kinds.count(2) == 1
+        mark = kinds.index(2)
+        assert all(not (k == 0 and g == p + 2) for k, g, *_ in ops[mark + 1:])

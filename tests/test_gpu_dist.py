@@ -106,6 +106,25 @@ def test_loopback_large_matches_single_gpu(world, spw, N):
         assert abs(got - ref) <= 1e-11 * abs(ref)
 
 
+@pytest.mark.parametrize("world,spw,N,depth,chunk", [
+    (2, 2, 12000, 4, 1), (4, 2, 12000, 8, 2), (3, 4, 14000, 3, 1), (8, 2, 12000, 2, 1), (2, 4, 10000, 1, 2),
+    (5, 3, 9000, 4, 3)])
+def test_loopback_depth_and_chunks_match_single_gpu(world, spw, N, depth, chunk):
+    """Deferral groups of `depth` panels (K up to depth x 128 spw per bulk update) and
+    broadcast chunks of `chunk` tile columns (per-chunk packs, events and lookahead
+    launches) at sizes where the deferral and the tile kernel run; against the single-GPU
+    path and the oracle, twice through the same workspaces."""
+    X, terms, v = _case(N, seed=N + depth)
+    with Context(0) as ctx:
+        ref = ctx.logpdf(X, terms, 0.1, v)
+    ranks = [DI.DistRank(0, world, r, spw=spw, depth=depth, chunk=chunk) for r in range(world)]
+    for _ in range(2):
+        got = DI.logpdf_dist(ranks, DI.LoopbackTransport(), X, terms, 0.1, v)
+        assert abs(got - ref) <= 1e-11 * abs(ref)
+    for r in ranks:
+        r.close()
+
+
 def test_loopback_non_pd_info():
     rng = np.random.default_rng(5)
     N = 700
