@@ -65,14 +65,32 @@ def _blas_threads() -> int:
         return os.cpu_count() or 1
 
 
+def _host_cores() -> dict:
+    """What the CPU baseline may use: the process's CPU affinity set, the pool's per-GPU
+    CPU share (OMP_NUM_THREADS, set by the GPU pool and not overridden here) and the BLAS
+    threads the oracle actually runs (all usable cores)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return {"affinity_cores": aff, "omp_num_threads": int(omp) if omp and omp.isdigit() else None,
+            "blas_threads": _blas_threads()}
+
+
+def _cores_note(h: dict) -> str:
+    share = h["omp_num_threads"]
+    if share and share < h["affinity_cores"]:
+        return (f"{h['blas_threads']} BLAS threads = the pool's CPU share per GPU (OMP_NUM_THREADS={share}; "
+                f"the affinity mask shows {h['affinity_cores']} CPUs of the shared host)")
+    return f"{h['blas_threads']} BLAS threads of {h['affinity_cores']} CPUs in the affinity mask"
+
+
 def cpu_baseline(N: int, budget_s: float = 25.0):
     """Time the oracle (numpy Gram + scipy/OpenBLAS dpotrf + dtrsv) on the host cores."""
     from oracle import restatement as R
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max((d.get("num_threads", 1) for d in threadpool_info() if d.get("user_api") == "blas"), default=1)
-    except Exception:
-        threads = os.cpu_count() or 1
+    hc = _host_cores()
+    threads = hc["blas_threads"]
     X, v = make_inputs(N)
     n_small = 2048
     Xs, vs = make_inputs(n_small)
@@ -100,8 +118,9 @@ def cpu_baseline(N: int, budget_s: float = 25.0):
         "unit": "evals/s",
         "cores": int(threads),
         "kind": "port",
+        "host_cores": hc,
         "sample": f"{len(times)} full evals at N={N} (same workload, seed 2), median {med:.2f} s; "
-                  f"numpy Gram + scipy-openblas dpotrf('U') + dtrsv, {threads} BLAS threads on {cpu}",
+                  f"numpy Gram + scipy-openblas dpotrf('U') + dtrsv, {_cores_note(hc)}, on {cpu}",
     }
 
 
@@ -400,6 +419,7 @@ def main():
         "n4096": n4096,
         "n65536": n65536,
         "select": select4,
+        "select_share8": select4.get("share8") if select4 else None,
         "dist": dist_line,
     }
     if gram_alone:
@@ -539,6 +559,9 @@ def measure_config4(local_rank: int, torch, steps: int = 2):
     N = CF.N4
     X, y = CF.config4_inputs(N)
     models = select_models()
+    from gaplac_amd.replicas import shard
+    # one GPU's share of the 8-GPU job (replicas.shard: rank 0's 8 of the 64 formulas)
+    share8 = [models[i] for i in shard(len(models), 0, 8)]
     c = Context(local_rank)
     try:
         c.logpdf_batch(X, models, CF.NOISE_VAR, y)  # warmup: workspaces, task lists
@@ -549,16 +572,27 @@ def measure_config4(local_rank: int, torch, steps: int = 2):
             out, _ = c.logpdf_batch(X, models, CF.NOISE_VAR, y)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / steps
+        c.logpdf_batch(X, share8, CF.NOISE_VAR, y)  # warmup: the 8-model task list
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(2 * steps):
+            c.logpdf_batch(X, share8, CF.NOISE_VAR, y)
+        torch.cuda.synchronize()
+        dt8 = (time.perf_counter() - t0) / (2 * steps)
     finally:
         c.close()
         torch.cuda.empty_cache()
     flops = len(models) * (N ** 3 / 3.0 + N ** 2)
     tf = flops / dt / 1e12
+    rate64, rate8 = len(models) / dt, len(share8) / dt8
     return {"workload": f"BASELINE configs[4]: {len(models)} candidate formulas, N={N}, noise 0.1 (host inputs)",
-            "evals_per_s": len(models) / dt, "ms_per_step": dt * 1e3, "steps": steps,
+            "evals_per_s": rate64, "ms_per_step": dt * 1e3, "steps": steps,
             "n_finite": int(np.isfinite(out).sum()),
             "roofline": {"bound": "mfma", "kernel": "whole batch (64 x (N^3/3 + N^2))", "achieved": round(tf, 3),
-                         "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / PEAK_F64_TFLOPS, 4)}}
+                         "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / PEAK_F64_TFLOPS, 4)},
+            "share8": {"workload": f"one GPU's share of configs[4] on 8 GPUs: {len(share8)} formulas "
+                                   f"(replicas.shard rank 0), N={N}, one gaplac_logpdf_batch call",
+                       "evals_per_s": rate8, "ms_per_call": dt8 * 1e3, "ratio_to_64": rate8 / rate64}}
 
 
 def measure_config3_dist(rank: int, world: int, local_rank: int, torch, dist, steps: int = 3,

@@ -39,6 +39,7 @@ EXPORTED = (
     "gaplac_get_stats",
     "gaplac_reset_stats",
     "gaplac_plan_check",
+    "gaplac_plan_check_schedule",
     "gaplac_dist_create",
     "gaplac_dist_destroy",
     "gaplac_dist_last_error",
@@ -147,6 +148,7 @@ def load() -> ctypes.CDLL:
     lib.gaplac_reset_stats.argtypes = [c_void_p]
     _I32P, _I64P, _VPP = POINTER(c_int32), POINTER(c_int64), POINTER(c_void_p)
     lib.gaplac_plan_check.argtypes = [c_int64, c_int32, c_int64, c_int32, _I64P, _I64P, c_char_p, c_int64]
+    lib.gaplac_plan_check_schedule.argtypes = [c_int64, c_int32, c_int32, c_int32, c_int32, _I64P, c_char_p, c_int64]
     lib.gaplac_dist_create.argtypes = [c_int, c_int, c_int, c_int, _VPP]
     lib.gaplac_dist_destroy.argtypes = [c_void_p]
     lib.gaplac_dist_last_error.argtypes = [c_void_p]

@@ -858,7 +858,11 @@ int ensure_workspace(gaplac_ctx* ctx, int64_t N) {
     if ((rc = ensure(ctx, &ctx->A, &ctx->A_elems, (size_t)(Np + (int64_t)NB * ctx->xr_tiles) * Np))) return rc;
     if (ctx->xr_mode && !ctx->s_extra) {
         // created on first use only: a plain logpdf context keeps two streams, so the
-        // batch lanes (2 contexts) fit the 4 hardware queues a process gets by default
+        // batch lanes (2 contexts) fit the 4 hardware queues a process gets by default. A
+        // gradient / posterior context then holds four streams (s_main, s_panel, s_extra,
+        // s_xrest), all four hardware queues: another context or torch stream in the same
+        // process shares a queue with one of them and may serialise behind it (the
+        // measured 79.4 -> 78.0 ms of DESIGN.md §9 assumes no other streams are busy)
         int least = 0, greatest = 0;
         HIPCK(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
         HIPCK(ctx, hipStreamCreateWithPriority(&ctx->s_extra, hipStreamNonBlocking, least));
@@ -1268,7 +1272,14 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (ctx->tailk) ctx->tail_s = 80;  // the persistent tail (A/B at N = 16384)
     if (const char* s = std::getenv("GAPLAC_TAIL_S")) ctx->tail_s = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_TAIL_TRACE")) ctx->ttrace_path = s;  // diagnostics
-    if (const char* s = std::getenv("GAPLAC_TAIL_FAULT")) ctx->tail_fault = std::atoi(s);  // tests: forced expiry
+    if (const char* s = std::getenv("GAPLAC_TAIL_FAULT")) {  // tests only: forced expiry
+        ctx->tail_fault = std::atoi(s);
+        if (ctx->tail_fault >= 0)
+            std::fprintf(stderr,
+                         "gaplac: GAPLAC_TAIL_FAULT=%d is set (test hook): the persistent tail skips the diagonal "
+                         "block of that tail column and evaluations return GAPLAC_E_HIP\n",
+                         ctx->tail_fault);
+    }
     if (const char* s = std::getenv("GAPLAC_BATCH_W")) ctx->batch_w = std::max(1, std::min(TAIL_MAX_MODELS, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BATCH_LAG")) ctx->batch_lag = std::max(0, std::atoi(s));
     auto fail = [&](const char* what, hipError_t e) {
@@ -1860,6 +1871,114 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
     if (out_violations) *out_violations = g.violations;
     if (msg && msglen > 0) std::snprintf(msg, (size_t)msglen, "%s", g.first.c_str());
     return rc == GAPLAC_E_ARG && g.violations ? 0 : rc;
+}
+
+// Host-only accounting of the single-GPU schedule: a dry walk of one
+// evaluation of order N with the given deferral depth / band extension / cut-off, whose
+// launchers record every update (tile columns x panel columns) and every column's
+// factorisation in enqueue order (LaunchGuard::acct). Checks that every tile column gets
+// every earlier panel column exactly once, in increasing order, before its diagonal block
+// (or before the persistent tail that factors it), and that every update reads panel
+// columns already factored. 0, or GAPLAC_E_ARG with the first violation in msg.
+int gaplac_plan_check_schedule(int64_t N, int32_t spw, int32_t depth, int32_t pair_ext, int32_t pair_m,
+                               int64_t* out_records, char* msg, int64_t msglen) {
+    if (N < 1 || spw < 1 || spw > 8 || depth < 0 || depth > 8 || pair_ext < 0 || pair_ext > 1 || pair_m < 0)
+        return GAPLAC_E_ARG;
+    gaplac_ctx c;
+    c.dry = true;
+    c.spw = spw;
+    c.pair_depth = depth;
+    c.pair_ext = pair_ext;
+    c.pair_m = pair_m;
+    const int64_t Np = round_up(N + 1, NB);
+    const int nt = (int)(Np / NB);
+    double* const fake = reinterpret_cast<double*>((uintptr_t)1 << 44);
+    c.A = fake;
+    c.A_elems = (size_t)Np * (size_t)Np;
+    c.Dinv = fake;
+    c.tiles = reinterpret_cast<uint32_t*>(fake);
+    c.tile_off.assign((size_t)nt + 1, 0);
+    for (int m = 1; m <= nt; ++m) c.tile_off[(size_t)m] = c.tile_off[(size_t)m - 1] + (size_t)(m - 1) * m / 2;
+    c.tiles_nt = nt;
+    c.band_off.assign((size_t)nt + 1, 0);
+    {
+        size_t k = c.tile_off[(size_t)nt] + (size_t)nt * (nt + 1) / 2;
+        for (int m = 1; m <= nt; ++m) {
+            c.band_off[(size_t)m] = k;
+            const size_t w = (size_t)std::min(c.spw, m);
+            k += w * m - w * (w - 1) / 2;
+        }
+    }
+    c.tail_s = 80;
+    TermPack tp{};
+    tp.T = 1;
+    c.htp = &tp;
+    LaunchGuard g;
+    g.base = fake;
+    g.elems = (int64_t)c.A_elems;
+    g.dry = true;
+    std::vector<int> acct;
+    g.acct = &acct;
+    int rc;
+    {
+        GuardScope scope(&g);
+        rc = enqueue_eval(&c, N, 1, Np, nt);
+    }
+    c.htp = nullptr;
+    c.A = nullptr;
+    c.Dinv = nullptr;
+    c.tiles = nullptr;
+    std::string why;
+    char b[200];
+    if (rc) why = "the dry walk failed";
+    if (g.violations && why.empty()) why = g.first;
+    std::vector<int> next((size_t)nt, 0);       // next panel column tile column j must receive
+    std::vector<char> done((size_t)nt, 0);      // factored (or handed to the tail)
+    for (size_t i = 0; i + 5 <= acct.size() && why.empty(); i += 5) {
+        const int kind = acct[i], j0 = acct[i + 1], j1 = acct[i + 2], k0 = acct[i + 3], k1 = acct[i + 4];
+        if (kind == 0) {
+            for (int k = k0; k < k1 && why.empty(); ++k)
+                if (k < 0 || k >= nt || !done[(size_t)k]) {
+                    std::snprintf(b, sizeof b, "an update reads panel column %d before it is factored", k);
+                    why = b;
+                }
+            for (int j = j0; j < j1 && why.empty(); ++j) {
+                if (j < 0 || j >= nt || done[(size_t)j] || next[(size_t)j] != k0 || k1 > j) {
+                    std::snprintf(b, sizeof b, "tile column %d gets panel columns %d..%d (expected from %d%s)", j, k0,
+                                  k1 - 1, j >= 0 && j < nt ? next[(size_t)j] : -1,
+                                  j >= 0 && j < nt && done[(size_t)j] ? ", after its factorisation" : "");
+                    why = b;
+                } else {
+                    next[(size_t)j] = k1;
+                }
+            }
+        } else if (kind == 1) {
+            if (j0 < 0 || j0 >= nt) continue;
+            if (!done[(size_t)j0] && next[(size_t)j0] != j0) {
+                std::snprintf(b, sizeof b, "tile column %d factored with panel columns < %d only", j0,
+                              next[(size_t)j0]);
+                why = b;
+            }
+            done[(size_t)j0] = 1;
+        } else {
+            for (int j = j0; j < nt && why.empty(); ++j) {
+                if (done[(size_t)j] || next[(size_t)j] != j0) {
+                    std::snprintf(b, sizeof b, "the tail from %d starts with tile column %d at panel %d", j0, j,
+                                  next[(size_t)j]);
+                    why = b;
+                }
+                done[(size_t)j] = 1;
+            }
+        }
+    }
+    for (int j = 0; j < nt && why.empty(); ++j)
+        if (!done[(size_t)j]) {
+            std::snprintf(b, sizeof b, "tile column %d never factored", j);
+            why = b;
+        }
+    if (out_records) *out_records = (int64_t)(acct.size() / 5);
+    if (msg && msglen > 0) std::snprintf(msg, (size_t)msglen, "%s", why.c_str());
+    return why.empty() ? 0 : GAPLAC_E_ARG;
 }
 
 int gaplac_set_profiling(gaplac_ctx* ctx, int mode) {

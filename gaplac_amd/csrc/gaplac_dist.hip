@@ -99,6 +99,7 @@ struct gaplac_dist {
     hipEvent_t ev_recv[2][MAXC] = {}, ev_packed[2][MAXC] = {};
     hipEvent_t ev_step[2] = {}, ev_free_main[2] = {}, ev_free_panel[2] = {}, ev_free_comm[2] = {};
     hipEvent_t ev_upd[2] = {};  // replay: update(s) started (its UPD stamp written)
+    hipEvent_t ev_col[MAXC] = {};  // factor(s): column k of the SP final (its pack may start)
     int pair_m = 40;  // GAPLAC_PAIR_M: deferred updates while >= pair_m tile rows follow SP s+3
     // geometry of the current evaluation
     int64_t N = -1, Np = 0;
@@ -106,6 +107,8 @@ struct gaplac_dist {
     bool factored_any = false;
     std::vector<std::vector<DOp>> plan;
     int plan_nt = -1;
+    int held_step = -1;   // alone: the step whose ops after its mark wait for the next update
+    size_t held_from = 0;
     // device buffers
     double* C = nullptr;
     size_t C_elems = 0;
@@ -377,6 +380,22 @@ __global__ void release_kernel(unsigned long long* stamps, Release r) {
     stamps[r.out] = now;
 }
 
+// One 128-column block of a panel, rows .. rows-1 (a multiple of 128) from the column
+// storage into the panel buffer: 16-byte loads and stores, 512 rows per workgroup.
+__global__ __launch_bounds__(256) void pack_kernel(const double* __restrict__ src, int64_t lds,
+                                                   double* __restrict__ dst, int64_t ldd, int64_t rows) {
+    const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+    const int col = blockIdx.y;
+    if (r >= rows) return;
+    const double2 v = *reinterpret_cast<const double2*>(src + col * lds + r);
+    *reinterpret_cast<double2*>(dst + col * ldd + r) = v;
+}
+
+void launch_pack(hipStream_t s, const double* src, int64_t lds, double* dst, int64_t ldd, int64_t rows) {
+    if (rows <= 0 || !guard_launch("pack_kernel")) return;
+    pack_kernel<<<dim3((unsigned)((rows + 511) / 512), NB), dim3(256), 0, s>>>(src, lds, dst, ldd, rows);
+}
+
 int stamp(gaplac_dist* d, hipStream_t s, int slot) {
     if (!d->stamps) return 0;
     if (!guard_launch("stamp_kernel")) return 0;
@@ -401,8 +420,12 @@ int gaplac_dist_create(int device, int nranks, int rank, int spw, gaplac_dist** 
     d->nranks = nranks;
     d->rank = rank;
     d->W = spw;
-    d->cw = spw;
-    d->big_mode = nranks == 1 ? 2 : 1;  // one rank: the single-GPU rule
+    // defaults from the one-GPU replay of configs[3]: with several ranks,
+    // chunks of two tile columns, the chain alone, the large-launch kernel per rank; one
+    // rank keeps the single-GPU rules
+    d->cw = nranks > 1 ? std::min(2, spw) : spw;
+    d->alone = nranks > 1 ? 1 : 0;
+    d->big_mode = nranks == 1 ? 2 : 1;
     auto fail = [&](const char* what, hipError_t e) {
         std::fprintf(stderr, "gaplac_dist_create: %s: %s\n", what, hipGetErrorString(e));
         gaplac_dist_destroy(d);
@@ -425,6 +448,7 @@ int gaplac_dist_create(int device, int nranks, int rank, int spw, gaplac_dist** 
     if (const char* e = std::getenv("GAPLAC_DIST_BIG_MIN")) d->big_min = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("GAPLAC_DIST_ALONE")) d->alone = std::atoi(e) > 0;
     std::vector<hipEvent_t*> evs = {&d->ev_gram, &d->ev_panel_done};
+    for (int c = 0; c < MAXC; ++c) evs.push_back(&d->ev_col[c]);
     for (int b = 0; b < 2; ++b) {
         for (int c = 0; c < MAXC; ++c) {
             evs.push_back(&d->ev_recv[b][c]);
@@ -454,6 +478,7 @@ int gaplac_dist_destroy(gaplac_dist* d) {
     for (hipStream_t s : {d->s_main, d->s_panel, d->s_comm})
         if (s) (void)hipStreamSynchronize(s);
     std::vector<hipEvent_t> evs = {d->ev_gram, d->ev_panel_done};
+    for (int c = 0; c < MAXC; ++c) evs.push_back(d->ev_col[c]);
     for (int b = 0; b < 2; ++b) {
         for (int c = 0; c < MAXC; ++c) {
             evs.push_back(d->ev_recv[b][c]);
@@ -570,6 +595,7 @@ int gaplac_dist_begin(gaplac_dist* d, int64_t N, int32_t D, const double* X, int
     d->nsp = nsp;
     d->nloc = nloc;
     d->factored_any = false;
+    d->held_step = -1;
     if (d->plan_nt != nt) {
         d->plan = build_plan(nsp, nt, d->W, d->D, d->pair_m);
         std::string why;
@@ -628,10 +654,25 @@ int gaplac_dist_factor(gaplac_dist* d, int32_t s) {
     DCK(d, hipStreamWaitEvent(sp, d->ev_step[s & 1], 0));
     if (s > 0) {
         const int q = s - 1, nc = nchunks(d, q);
+        // alone: nothing of this rank runs beside the chain, so the lookahead takes the
+        // whole-tile band kernel (128x128 tiles, the SP's band list); otherwise the 64x64
+        // quadrant kernel, which fits beside resident bulk workgroups
+        const bool whole = d->alone && d->nranks > 1;
+        const size_t u = (size_t)(s / d->nranks);
         for (int c = 0; c < nc; ++c) {
-            if (!owns(d, q)) DCK(d, hipStreamWaitEvent(sp, d->ev_recv[q & 1][c], 0));
-            launch_col_update(sp, d->C, ldc, chunk_panel(d, q, c), d->nt, c0, lc0, w, chunk_cols(d, q, c) * NB,
-                              nullptr);
+            // this rank's own panel (one rank): packed on the comm stream
+            DCK(d, hipStreamWaitEvent(sp, owns(d, q) ? d->ev_packed[q & 1][c] : d->ev_recv[q & 1][c], 0));
+            if (whole && d->band_cnt[u] > 0) {
+                BulkArgs ba{d->C, d->Np, chunk_panel(d, q, c), d->tiles + d->band_off[u], d->band_cnt[u],
+                            chunk_cols(d, q, c) * NB, 0, 0, cmap(d)};
+                ba.max_r = d->nt - 1;
+                ba.max_c = d->nloc - 1;
+                ba.whole = 1;
+                launch_bulk(sp, ba, nullptr);
+            } else {
+                launch_col_update(sp, d->C, ldc, chunk_panel(d, q, c), d->nt, c0, lc0, w, chunk_cols(d, q, c) * NB,
+                                  nullptr);
+            }
         }
         // this rank's latest lookahead reading the group buffer (the receive of the
         // buffer's next group waits for it on the comm stream)
@@ -647,24 +688,26 @@ int gaplac_dist_factor(gaplac_dist* d, int32_t s) {
         if ((int64_t)c * NB < d->N)
             launch_potrf_diag(sp, Acol + (int64_t)c * NB, ldc, d->N, (int64_t)c * NB, Dk, d->dres, nullptr);
         launch_trsm(sp, Acol, ldc, d->nt, c, Dk, nullptr);
-        const int k = c - c0;  // column of the SP
+        // column k of the SP is final: pack it on the comm stream, beside the chain's next
+        // columns (the comm stream then broadcasts the chunk in order behind its packs)
+        const int k = c - c0;
         const int ch = k / d->cw;
-        if (k == w - 1 || (k + 1) % d->cw == 0) {  // the chunk's last column is final: pack it
-            if (ch == 0) {
-                // the packs overwrite group buffer group_buf(s): its previous group must be
-                // done with on s_main (ev_free_main; at a group's later panels implied by
-                // ev_step, which follows every update of steps <= s - 3) and on the comm
-                // stream (ev_free_comm: its broadcasts, this rank's own sends included); its
-                // lookahead readers are earlier on this stream
-                if (s % d->D == 0) DCK(d, hipStreamWaitEvent(sp, d->ev_free_main[group_buf(d, s)], 0));
-                DCK(d, hipStreamWaitEvent(sp, d->ev_free_comm[group_buf(d, s)], 0));
-            }
-            const int kc0 = chunk_col0(d, ch), ncol = chunk_cols(d, s, ch);
-            double* dst = const_cast<double*>(chunk_panel(d, s, ch).P) + (r0 - group_row0(d, s));
-            DCK(d, hipMemcpy2DAsync(dst, (size_t)ldp * 8, d->C + (int64_t)(lc0 + kc0) * NB * ldc + r0, (size_t)ldc * 8,
-                                    (size_t)(d->Np - r0) * 8, (size_t)ncol * NB, hipMemcpyDeviceToDevice, sp));
-            stamp(d, sp, st_pack(s, ch));
-            DCK(d, hipEventRecord(d->ev_packed[s & 1][ch], sp));
+        DCK(d, hipEventRecord(d->ev_col[k], sp));
+        if (k == 0 && s % d->D == 0) {
+            // the packs overwrite group buffer group_buf(s): its previous group's bulk
+            // updates must be done (at a group's later panels implied by ev_step, which
+            // follows every update of steps <= s - 3); its broadcasts are earlier on the
+            // comm stream, its lookaheads earlier on s_panel
+            DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_free_main[group_buf(d, s)], 0));
+        }
+        DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_col[k], 0));
+        launch_pack(d->s_comm, d->C + (int64_t)lc * NB * ldc + r0, ldc,
+                    const_cast<double*>(chunk_panel(d, s, ch).P) + (int64_t)(k - chunk_col0(d, ch)) * NB * ldp +
+                        (r0 - group_row0(d, s)),
+                    ldp, d->Np - r0);
+        if (k == w - 1 || (k + 1) % d->cw == 0) {  // the chunk's last column
+            stamp(d, d->s_comm, st_pack(s, ch));
+            DCK(d, hipEventRecord(d->ev_packed[s & 1][ch], d->s_comm));
         }
     }
     DCK(d, hipEventRecord(d->ev_panel_done, sp));
@@ -743,27 +786,14 @@ int gaplac_dist_comm_end(gaplac_dist* d, int32_t s) {
     return 0;
 }
 
-// Bulk trailing update of step s (s_main) following the step plan: SP s+2 first, then
-// ev_step, then the rest (a deferring step: SP s+3's band; otherwise the suffix).
-int gaplac_dist_update(gaplac_dist* d, int32_t s) {
-    if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "update: step %d out of range", s);
-    DCK(d, hipSetDevice(d->device));
-    const int last = nchunks(d, s) - 1;
-    // the owner reads its own packed panel (its broadcast may still be running); the
-    // others wait for the whole panel to arrive. Panels before s were waited for by the
-    // updates before this one on the same stream.
-    DCK(d, hipStreamWaitEvent(d->s_main, owns(d, s) ? d->ev_packed[s & 1][last] : d->ev_recv[s & 1][last], 0));
-    if (d->alone && d->nranks > 1 && s + 1 < d->nsp && owns(d, s + 1))
-        DCK(d, hipStreamWaitEvent(d->s_main, d->ev_panel_done, 0));  // factor(s+1), enqueued just before
-    stamp(d, d->s_main, st_upd(s));
-    if (d->stamps) DCK(d, hipEventRecord(d->ev_upd[s & 1], d->s_main));
+// The ops [b, e) of step p's plan on s_main (chain_beside: this rank's chain runs beside
+// them, so the large-launch kernel is not taken).
+static int run_ops(gaplac_dist* d, int p, size_t b, size_t e, bool chain_beside) {
     // owned-SP ordinal of the first owned SP >= g
     auto ord_from = [&](int g) {
         const int rel = g - d->rank;
         return rel <= 0 ? 0 : (rel + d->nranks - 1) / d->nranks;
     };
-    // this rank runs a chain beside the update when it owns SP s+1 (factor(s+1) runs now)
-    const bool chain_beside = s + 1 < d->nsp && owns(d, s + 1);
     auto launch = [&](const uint32_t* tiles, int cnt, const Panel& pn, int kd) -> int {
         if (cnt <= 0) return 0;
         BulkArgs ba{d->C, d->Np, pn, tiles, cnt, kd, 0, 0, cmap(d)};
@@ -781,10 +811,12 @@ int gaplac_dist_update(gaplac_dist* d, int32_t s) {
         return k;
     };
     int rc;
-    for (const DOp& op : d->plan[(size_t)s]) {
+    const std::vector<DOp>& ops = d->plan[(size_t)p];
+    for (size_t i = b; i < e; ++i) {
+        const DOp& op = ops[i];
         if (op.kind == OP_MARK) {
-            stamp(d, d->s_main, st_band(s));
-            DCK(d, hipEventRecord(d->ev_step[s & 1], d->s_main));
+            stamp(d, d->s_main, st_band(p));
+            DCK(d, hipEventRecord(d->ev_step[p & 1], d->s_main));
             continue;
         }
         const Panel pn = panel_of(d, op.pf);
@@ -799,10 +831,58 @@ int gaplac_dist_update(gaplac_dist* d, int32_t s) {
             if ((rc = launch(d->tiles + d->bulk_off[(size_t)u], d->bulk_cnt[(size_t)u], pn, kd))) return rc;
         }
     }
-    stamp(d, d->s_main, st_end(s));
-    // the group's last bulk reader: its last step (or the last step of all)
-    if (s % d->D == d->D - 1 || s + 1 >= d->nsp)
-        DCK(d, hipEventRecord(d->ev_free_main[group_buf(d, s)], d->s_main));
+    return 0;
+}
+
+// Step p's ops are all enqueued: its END stamp, and the group's last bulk reader (its last
+// step, or the last step of all) releases the group buffer.
+static int end_step(gaplac_dist* d, int p) {
+    stamp(d, d->s_main, st_end(p));
+    if (p % d->D == d->D - 1 || p + 1 >= d->nsp)
+        DCK(d, hipEventRecord(d->ev_free_main[group_buf(d, p)], d->s_main));
+    return 0;
+}
+
+// Bulk trailing update of step s (s_main) following the step plan: SP s+2 first, then
+// ev_step, then the rest (a deferring step: SP s+3's band; otherwise the suffix).
+// alone (a rank's chain gets the GPU to itself): the owner of SP s+1 starts update(s)
+// after factor(s+1), and the owner of SP s+2 holds the ops after update(s)'s mark back
+// until update(s+1) (after factor(s+2)): the chain of SP s+2, which starts at that mark,
+// then never shares the GPU with this rank's bulk updates.
+int gaplac_dist_update(gaplac_dist* d, int32_t s) {
+    if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "update: step %d out of range", s);
+    DCK(d, hipSetDevice(d->device));
+    const int last = nchunks(d, s) - 1;
+    // the owner reads its own packed panel (its broadcast may still be running); the
+    // others wait for the whole panel to arrive. Panels before s were waited for by the
+    // updates before this one on the same stream.
+    DCK(d, hipStreamWaitEvent(d->s_main, owns(d, s) ? d->ev_packed[s & 1][last] : d->ev_recv[s & 1][last], 0));
+    const bool alone = d->alone && d->nranks > 1;
+    const bool waits = alone && s + 1 < d->nsp && owns(d, s + 1);
+    if (waits) DCK(d, hipStreamWaitEvent(d->s_main, d->ev_panel_done, 0));  // factor(s+1), enqueued just before
+    int rc;
+    if (d->held_step >= 0) {  // update(s-1)'s ops after its mark (this rank's chain of SP s+1 is done)
+        const int p = d->held_step;
+        d->held_step = -1;
+        if (p != s - 1) return derr(d, GAPLAC_E_ARG, "update: held ops of step %d at step %d", p, s);
+        if ((rc = run_ops(d, p, d->held_from, d->plan[(size_t)p].size(), false)) || (rc = end_step(d, p))) return rc;
+    }
+    stamp(d, d->s_main, st_upd(s));
+    if (d->stamps) DCK(d, hipEventRecord(d->ev_upd[s & 1], d->s_main));
+    // this rank's chain runs beside the update when it owns SP s+1 and does not wait for it
+    const bool chain_beside = s + 1 < d->nsp && owns(d, s + 1) && !waits;
+    const std::vector<DOp>& ops = d->plan[(size_t)s];
+    size_t mark = 0;
+    while (mark < ops.size() && ops[mark].kind != OP_MARK) ++mark;
+    if ((rc = run_ops(d, s, 0, std::min(mark + 1, ops.size()), chain_beside))) return rc;
+    // (not with D = 1: factor(s+2) packs panel s+2 into panel s's buffer slot, which the held
+    // ops still read; with D >= 2 panel s+2 lands in the other group buffer or another slot)
+    if (alone && d->D >= 2 && s + 2 < d->nsp && owns(d, s + 2)) {
+        d->held_step = s;
+        d->held_from = mark + 1;
+    } else {
+        if ((rc = run_ops(d, s, mark + 1, ops.size(), chain_beside)) || (rc = end_step(d, s))) return rc;
+    }
     DCK(d, hipGetLastError());
     return 0;
 }
@@ -813,6 +893,7 @@ int gaplac_dist_update(gaplac_dist* d, int32_t s) {
 int gaplac_dist_finish(gaplac_dist* d, double* out_logdet, double* out_quad, int64_t* out_info) {
     if (!d) return GAPLAC_E_ARG;
     DCK(d, hipSetDevice(d->device));
+    if (d->held_step >= 0) return derr(d, GAPLAC_E_ARG, "finish: step %d's update is incomplete", d->held_step);
     if (d->factored_any) DCK(d, hipStreamWaitEvent(d->s_main, d->ev_panel_done, 0));
     {
         DistGuard guard(d);

@@ -156,7 +156,16 @@ struct LaunchGuard {
     int64_t launches = 0;
     int64_t violations = 0;
     std::string first;  // the first violation
+    // optional schedule accounting of a dry single-GPU walk (gaplac_plan_check_schedule):
+    // 5 ints per record {kind, j0, j1, k0, k1}: kind 0 = tile columns [j0, j1) updated
+    // (rows from their diagonal down) with panel columns [k0, k1); 1 = column j0 factored
+    // (diagonal block / TRSM); 2 = the persistent tail factors columns >= j0
+    std::vector<int>* acct = nullptr;
 };
+// record into the current guard's accounting (no-op without one)
+void acct_record(int kind, int j0, int j1, int k0, int k1);
+// panel column of a single-GPU panel pointer (its offset from the guard's base / (ld NB))
+int acct_panel_col(const double* P, int64_t ld);
 LaunchGuard*& current_guard();  // this thread's guard (nullptr: unchecked)
 struct GuardScope {
     LaunchGuard* prev;

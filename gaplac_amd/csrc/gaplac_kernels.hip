@@ -2861,6 +2861,19 @@ bool guard_launch(const char* what, const double* p, int64_t lo, int64_t hi) {
     return !g->dry;
 }
 
+void acct_record(int kind, int j0, int j1, int k0, int k1) {
+    LaunchGuard* g = current_guard();
+    if (!g || !g->acct) return;
+    for (int v : {kind, j0, j1, k0, k1}) g->acct->push_back(v);
+}
+
+int acct_panel_col(const double* P, int64_t ld) {
+    LaunchGuard* g = current_guard();
+    if (!g || !g->base || ld <= 0) return -1;
+    const int64_t off = (int64_t)(((intptr_t)P - (intptr_t)g->base) / (intptr_t)sizeof(double));
+    return (int)(off / (ld * NB));
+}
+
 bool guard_launch(const char* what) {
     (void)what;
     LaunchGuard* g = current_guard();
@@ -2936,11 +2949,13 @@ void launch_gram_list(hipStream_t s, double* C, int64_t ldc, int64_t N, const do
 
 void launch_potrf_diag(hipStream_t s, double* Ablk, int64_t lda, int64_t N, int64_t g0, double* Dinv,
                        EvalResult* res, KTime* kt) {
+    acct_record(1, (int)(g0 / NB), (int)(g0 / NB) + 1, 0, 0);
     if (!guard_launch("potrf_diag_kernel", Ablk, 0, tiles_end(lda, 0, 0))) return;
     potrf_diag_kernel<<<dim3(1), dim3(256), 0, s>>>(Ablk, lda, N, g0, Dinv, res, kt);
 }
 
 void launch_trsm(hipStream_t s, double* Acol, int64_t lda, int nt, int k, const double* Dinv, KTime* kt) {
+    acct_record(1, k, k + 1, 0, 0);
     const int n = nt - k - 1;
     if (n <= 0) return;
     if (!guard_launch("trsm_subst_kernel", Acol, 0, tiles_end(lda, nt - 1, 0))) return;
@@ -2988,6 +3003,10 @@ void launch_bulk(hipStream_t s, const BulkArgs& a, KTime* kt) {
     } else {
         max_r = max_c = tri_row(a.ntiles - 1);  // an m x m triangle list: entries < m
     }
+    if (a.rect_rows == 0 && a.bi0 == a.lj0 && a.cm.nranks == 1 && a.pn.row0 == 0) {
+        const int k0 = acct_panel_col(a.pn.P, a.pn.ld);
+        acct_record(0, a.lj0, a.lj0 + (int)max_c + 1, k0, k0 + a.kdepth / NB);
+    }
     if (!guard_launch("bulk update", a.C, 0, tiles_end(a.ldc, a.bi0 + max_r, a.lj0 + max_c))) return;
     const int grid = ((a.ntiles + 7) >> 3) << 3;
     if (syrk_is_small(a.ntiles) && !a.whole && !(a.tile_min > 0 && a.ntiles >= a.tile_min))
@@ -3006,6 +3025,10 @@ void launch_col_update(hipStream_t s, double* C, int64_t ldc, const Panel& pn, i
     if (m0 <= 0 || ncols <= 0) return;
     int tiles = 0;
     for (int c = 0; c < ncols && c < m0; ++c) tiles += m0 - c;
+    if (pn.row0 == 0 && jb == lj0) {
+        const int k0 = acct_panel_col(pn.P, pn.ld);
+        acct_record(0, jb, jb + std::min(ncols, m0), k0, k0 + kdepth / NB);
+    }
     if (!guard_launch("col_update_kernel", C, 0, tiles_end(ldc, nt - 1, lj0 + std::min(ncols, m0) - 1))) return;
     col_update_kernel<<<dim3((unsigned)(4 * tiles)), dim3(256), 0, s>>>(C, ldc, pn, jb, lj0, m0, kdepth, kt);
 }
@@ -3132,6 +3155,7 @@ void launch_lower_mv(hipStream_t s, const double* A, int64_t lda, int64_t N, con
 
 void launch_tail(hipStream_t s, const TailArgs& a, int grid, KTime* kt) {
     if (a.ntasks <= 0 || a.T <= 0) return;
+    if (a.nmodels == 1) acct_record(2, a.ts, a.ts + a.T, 0, 0);
     if (a.nmodels < 1 || a.nmodels > TAIL_MAX_MODELS ||
         !guard_launch("tail_kernel", a.A, 0,
                       (int64_t)(a.nmodels - 1) * a.a_stride + tiles_end(a.lda, a.ts + a.T + a.xrows - 1, a.ts + a.T - 1)))

@@ -234,6 +234,14 @@ int gaplac_reset_stats(gaplac_ctx* ctx);
  * Not in the reference (an internal guard). */
 int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* out_launches,
                       int64_t* out_violations, char* msg, int64_t msglen);
+/* Host-only accounting of the single-GPU schedule for order N (GAPLAC_SPW = spw,
+ * GAPLAC_PAIR_DEPTH = depth (0: auto), band extension pair_ext (0/1), GAPLAC_PAIR_M =
+ * pair_m): every tile column gets every earlier panel column exactly once, in order, before
+ * its factorisation, and every update reads factored panel columns. 0, or GAPLAC_E_ARG with
+ * the first violation in msg; *out_records: launches and factorisations recorded. Not in the
+ * reference (an internal guard). */
+int gaplac_plan_check_schedule(int64_t N, int32_t spw, int32_t depth, int32_t pair_ext, int32_t pair_m,
+                               int64_t* out_records, char* msg, int64_t msglen);
 
 /* ------------------------------------------------------------------------------------
  * Distributed evaluation (BASELINE configs[3]: N = 65536 over the GPUs of one node; one
@@ -290,7 +298,9 @@ int gaplac_dist_begin(gaplac_dist* d, int64_t N, int32_t D, const double* X, int
  * (1..spw), big = bulk kernel choice (0: never the large-launch kernel; 1: per rank,
  * launches of >= big_min tiles while this rank runs no chain; 2: by launch size, as on one
  * GPU — for ranks that share one device), alone = 1: a rank's bulk update waits while it
- * factors the next super-panel (the chain gets the whole GPU). */
+ * factors the next super-panel (the chain gets the whole GPU). Defaults with several ranks
+ * (the one-GPU replay's best at N = 65536 over 8): depth 2, chunk 2, big 1,
+ * alone 1; with one rank: chunk = spw, big 2, alone 0. */
 int gaplac_dist_configure(gaplac_dist* d, int32_t depth, int32_t chunk, int32_t big, int32_t big_min,
                           int32_t alone);
 int gaplac_dist_factor(gaplac_dist* d, int32_t s);   /* owner of super-panel s only */

@@ -18,8 +18,9 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("world,rank,depth,chunk,big", [(4, 1, 2, 1, 1), (4, 3, 4, 2, 1), (3, 0, 1, 4, 0)])
-def test_replay_rank_matches_loopback(world, rank, depth, chunk, big):
+@pytest.mark.parametrize("world,rank,depth,chunk,big,alone", [
+    (4, 1, 2, 1, 1, 1), (4, 3, 4, 2, 1, 0), (3, 0, 1, 4, 0, 1), (3, 2, 2, 2, 1, 1)])
+def test_replay_rank_matches_loopback(world, rank, depth, chunk, big, alone):
     import torch
     N = 9000
     rng = np.random.default_rng(17)
@@ -31,7 +32,7 @@ def test_replay_rank_matches_loopback(world, rank, depth, chunk, big):
     owners = [DI.DistRank(0, world, r, spw=4) for r in range(world)]
     DI.logpdf_dist_device(owners, DI.LoopbackTransport(), N, 1, dx.data_ptr(), N, terms, 0.1, dv.data_ptr())
     ld0, q0, info0 = owners[rank].finish()
-    rep = DI.DistRank(0, world, rank, spw=4, depth=depth, chunk=chunk, big=big)
+    rep = DI.DistRank(0, world, rank, spw=4, depth=depth, chunk=chunk, big=big, alone=alone)
     model = RP.ReplayModel(bw_GBps=50.0, lat_us=20.0)
     F = band = None
     for _ in range(2):

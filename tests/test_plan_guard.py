@@ -64,3 +64,32 @@ def test_bad_arguments():
     z = ctypes.c_int64()
     for args in ((0, 0, 0, 4), (10, 3, 0, 4), (10, 2, 0, 4), (10, 0, 0, 0), (10, 0, 0, 9)):
         assert lib.gaplac_plan_check(*args, ctypes.byref(z), ctypes.byref(z), None, 0) == _native.E_ARG
+
+
+def schedule(N, spw=4, depth=0, ext=1, pair_m=40):
+    lib = _native.load()
+    msg = ctypes.create_string_buffer(256)
+    n = ctypes.c_int64()
+    rc = lib.gaplac_plan_check_schedule(N, spw, depth, ext, pair_m, ctypes.byref(n), msg, 256)
+    return rc, n.value, msg.value.decode()
+
+
+@pytest.mark.parametrize("depth", [0, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("ext", [0, 1])
+def test_single_gpu_schedule_applies_every_panel_once_in_order(depth, ext):
+    """the deferred bulk updates at every depth (GAPLAC_PAIR_DEPTH 2..8, 0 =
+    auto) and with / without the band extension: a dry walk of the real schedule records
+    every update and factorisation, and every tile column gets every earlier panel column
+    exactly once, in order, before its diagonal block or the persistent tail."""
+    for N in (1, 127, 1000, 4096, 10239, 10240, 12000, 16384, 20000, 33000, 40000, 50000, 65536):
+        for spw, pair_m in ((4, 40), (4, 8), (2, 24), (3, 16)):
+            rc, n, msg = schedule(N, spw, depth, ext, pair_m)
+            assert rc == 0 and n >= 1, (N, spw, depth, ext, pair_m, msg)
+
+
+def test_schedule_records_cover_the_superpanel_phase():
+    # N = 65536: 513 tile columns, the last 80 in the persistent tail, the rest in
+    # super-panels: at least one factorisation record per non-tail column plus updates
+    rc, n, msg = schedule(65536)
+    assert rc == 0, msg
+    assert n > 2 * (513 - 80)
