@@ -73,6 +73,7 @@ struct gaplac_ctx {
                           //   (default 48 with the persistent tail, 32 without)
     int pair_ext = 1;     // 1 = a deferring step also updates the band after next (§3.2)
     int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
+    int la_tiles_m = 120;   // GAPLAC_LA_TILES_M: the lookahead of >= this many tile rows as whole tiles (0: never)
     int pair_m = 40;      // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
     int pair_depth = 0;   // GAPLAC_PAIR_DEPTH: super-panels per deferred bulk update (0: 4 from 256 tile
                           //   columns on, else 2; N = 65536 1439 -> 1427 ms, 16k 26.97 -> 27.14 ms at 3-4)
@@ -571,8 +572,22 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             else
                 HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_gram2, 0));  // rest of the Gram built
             const int c2 = spc[(size_t)p + 2];
-            launch_col_update(sp, ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nt, c1, c1, c2 - c1,
-                              kd, slot(ctx, 5, 0));
+            const int mla = nt - c1;
+            if (ctx->la_tiles_m > 0 && mla >= ctx->la_tiles_m && c2 - c1 == W && ctx->band_off.size() > (size_t)mla &&
+                !ctx->xr_mode) {
+                // the lookahead as whole 128x128 tiles (the band list of SP p+1's columns):
+                // less CU time than the quadrant kernel while the trailing matrix is large
+                BulkArgs ba{ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0},
+                            ctx->tiles + ctx->band_off[(size_t)mla], W * mla - W * (W - 1) / 2, kd, c1, c1,
+                            ColMap{1, 0, W}};
+                ba.max_r = mla - 1;
+                ba.max_c = W - 1;
+                ba.whole = 1;
+                launch_bulk(sp, ba, slot(ctx, 5, 0));
+            } else {
+                launch_col_update(sp, ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nt, c1, c1,
+                                  c2 - c1, kd, slot(ctx, 5, 0));
+            }
             if ((frc = factor_superpanel(ctx, sp, N, lda, nt, c1, c2))) return frc;
             HIPQ(ctx, hipEventRecord(ctx->ev_P[(p + 1) & 1], sp));
         }
@@ -1267,6 +1282,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_PAIR_M")) ctx->pair_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_PAIR_DEPTH")) ctx->pair_depth = std::max(2, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BAND_TILES_M")) ctx->band_tiles_m = std::max(1, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_LA_TILES_M")) ctx->la_tiles_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAILK")) ctx->tailk = s[0] != '0';
     if (ctx->tailk) ctx->tail_s = 80;  // the persistent tail (A/B at N = 16384)
