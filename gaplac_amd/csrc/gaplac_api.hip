@@ -73,6 +73,8 @@ struct gaplac_ctx {
                           //   (default 48 with the persistent tail, 32 without)
     int pair_ext = 1;     // 1 = a deferring step also updates the band after next (§3.2)
     int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
+    int grad_fused = 1;     // GAPLAC_GRAD_FUSED: -C^{-1} contracted inside cinv_contract_kernel (0: stored, then contracted)
+    bool grad_singletons = true;  // the gradient's formula has single-term groups only (the fused path's case)
     int la_tiles_m = 120;   // GAPLAC_LA_TILES_M: the lookahead of >= this many tile rows as whole tiles (0: never)
     int pair_m = 40;      // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
     int pair_depth = 0;   // GAPLAC_PAIR_DEPTH: super-panels per deferred bulk update (0: 4 from 256 tile
@@ -798,10 +800,39 @@ int enqueue_eval_body(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt)
     if (ctx->xr_mode == 2)
         launch_posterior(ctx->s_main, ctx->A, lda, Np, N, ctx->xr_M, ctx->dXs, ctx->xr_M, ctx->dtp, ctx->gpart,
                          ctx->pmean, ctx->pvar);
-    if (ctx->xr_mode == 1) {
+    if (ctx->xr_mode == 1 && ctx->grad_fused && ctx->grad_singletons) {
+        // alpha = Y z first (HBM-bound, ~0.2 ms alone), then M = -C^{-1} tile by tile contracted
+        // in place with every dC/dtheta (cinv_contract_kernel: the tile is never stored nor
+        // read back), then the fixed-order reduction, all on s_main
+        hipStream_t sm = ctx->s_main;
+        launch_zero_tail_cols(sm, ctx->A, lda, Np, N);
+        launch_copy_z(sm, ctx->A, lda, N, ctx->gz);
+        launch_alpha(sm, ctx->A, lda, Np, N, ctx->gz, ctx->gpart, ctx->galpha, ctx->gdv);
+        size_t e0 = 0;
+        const bool ev = ctx->prof_mode == 2;
+        if (ev) {
+            e0 = 2 * ctx->evpairs.size();
+            while (ctx->evpool.size() < e0 + 2) {
+                hipEvent_t e;
+                HIPQ(ctx, hipEventCreate(&e));
+                ctx->evpool.push_back(e);
+            }
+            HIPQ(ctx, hipEventRecord(ctx->evpool[e0], sm));
+        }
+        launch_cinv_contract(sm, ctx->A, lda, Np, N, ctx->dX, N, ctx->galpha, ctx->dtp, ctx->glist,
+                             ctx->glist_blocks, ctx->gpart, slot(ctx, 8, 0));
+        if (ev) {
+            HIPQ(ctx, hipEventRecord(ctx->evpool[e0 + 1], sm));
+            ctx->evpairs.push_back({e0, 0.0, 0.0, 8});
+        }
+        const int m = (int)((N + NB - 1) / NB);
+        launch_grad_reduce(sm, ctx->gpart, m * (m + 1) / 2, ctx->htp->T, ctx->gout);
+        HIPQ(ctx, hipMemcpyAsync(ctx->hgout, ctx->gout, sizeof(double) * (GAPLAC_MAX_TERMS + 1),
+                                  hipMemcpyDeviceToHost, sm));
+    } else if (ctx->xr_mode == 1) {
         // alpha = Y z on s_extra beside M = -C^{-1} over the factor storage on s_main (both only
         // read Y; z is copied out first, cinv may overwrite row N), then the contraction and
-        // the reduction on s_main once alpha is in
+        // the reduction on s_main once alpha is in (GAPLAC_GRAD_FUSED=0)
         hipStream_t sm = ctx->s_main;
         hipStream_t sx = ctx->serial ? sm : ctx->s_extra;
         launch_zero_tail_cols(sm, ctx->A, lda, Np, N);
@@ -1055,6 +1086,8 @@ int logpdf_grad_impl(gaplac_ctx* ctx, bool on_device, int64_t N, int32_t D, cons
         gp.gstart[t] = a;
         gp.gend[t] = b;
     }
+    ctx->grad_singletons = true;
+    for (int t = 0; t < T; ++t) ctx->grad_singletons = ctx->grad_singletons && gp.gend[t] - gp.gstart[t] == 1;
     HIPCK(ctx, hipSetDevice(ctx->device));
     if ((rc = on_device ? upload_device(ctx, N, D, X, ldx, v) : upload(ctx, N, D, X, ldx, v))) return rc;
     tp.noise = noise;
@@ -1283,6 +1316,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_PAIR_DEPTH")) ctx->pair_depth = std::max(2, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BAND_TILES_M")) ctx->band_tiles_m = std::max(1, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_LA_TILES_M")) ctx->la_tiles_m = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_GRAD_FUSED")) ctx->grad_fused = s[0] != '0';
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAILK")) ctx->tailk = s[0] != '0';
     if (ctx->tailk) ctx->tail_s = 80;  // the persistent tail (A/B at N = 16384)

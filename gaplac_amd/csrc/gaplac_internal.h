@@ -271,6 +271,12 @@ void launch_posterior(hipStream_t s, const double* A, int64_t lda, int64_t Np, i
 // ---- rand(FiniteGP): out = L z over the factor's lower triangle (partial: ceil(N/512) * N) ----
 void launch_lower_mv(hipStream_t s, const double* A, int64_t lda, int64_t N, const double* z, double* partial,
                      double* out);
+// The same tiles of M = -C^{-1} contracted in place (never stored) with every dC/dtheta:
+// partial as launch_grad_contract's; alpha must be final before the launch; formulas whose
+// groups are all single terms only.
+void launch_cinv_contract(hipStream_t s, const double* A, int64_t lda, int64_t Np, int64_t N, const double* X,
+                          int64_t ldx, const double* alpha, const TermPack* dtp, const uint32_t* list, int nblocks,
+                          double* partial, KTime* kt);
 // dparam[t] = 0.5 * sum over tiles (fixed order), t = 0..T (T = observation variance).
 void launch_grad_reduce(hipStream_t s, const double* partial, int ntiles, int T, double* out);
 // Workgroup -> tile list for launch_grad_tiles over the m x m triangle (XCD-balanced).

@@ -1984,6 +1984,157 @@ __global__ __launch_bounds__(256) void grad_contract_kernel(const double* __rest
     kt_end(kt);
 }
 
+// dC/dl of a SqExp / OU term (term_dk's arithmetic, the Gram kernel's table exp): no FMA
+// contraction, so equal coordinates give exactly u = 0
+__device__ __forceinline__ double dk_sqexp(double p, double xi, double xj, const double* tbl) {
+#pragma clang fp contract(off)
+    const double u = p * xi - p * xj;
+    const double u2 = u * u;
+    return exp_nonpos(-u2 * 0.5, tbl) * u2 * p;
+}
+__device__ __forceinline__ double dk_ou(double p, double xi, double xj, const double* tbl) {
+#pragma clang fp contract(off)
+    const double a = fabs(p * xi - p * xj);
+    return exp_nonpos(-a, tbl) * a * p;
+}
+
+// -C^{-1} tile (I, J) as cinv_tile_kernel computes it, contracted in place with every
+// dC/dtheta (grad_contract_kernel's sum over the tile) instead of being stored: the tile
+// never goes to HBM and is never read back. Formulas whose groups are all single terms (the
+// reference's lowering; product groups keep the two-kernel path). alpha must be final
+// before the launch. partial[b][t] for the tile's triangle index b = I (I + 1) / 2 + J,
+// t <= T. After the k-loop the accumulators become the weights wt (alpha_i alpha_j + M_ij)
+// in place (wt = 2 off the diagonal, 1 on it, 0 outside the lower triangle / past N); then
+// one pass per term over the 64 weights of a lane, each term kind a loop of its own (the
+// code stays small: a fully unrolled term x element nest overflowed the instruction cache).
+// The k-loop's LDS staging buffer holds the tile's coordinates, alpha and the exp table.
+__global__ __launch_bounds__(256, 2) void cinv_contract_kernel(const double* __restrict__ A, int64_t lda, int64_t Np,
+                                                               int64_t N, const double* __restrict__ X, int64_t ldx,
+                                                               const double* __restrict__ alpha,
+                                                               const TermPack* __restrict__ tpp,
+                                                               const uint32_t* __restrict__ list,
+                                                               double* __restrict__ partial, KTime* __restrict__ kt) {
+    kt_begin(kt);
+    const uint32_t e = list[blockIdx.x];
+    if (e != 0xffffffffu) {
+        const int I = (int)(e & 0xffffu), J = (int)(e >> 16);
+        const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+        const int wi = w & 1, wj = w >> 1;
+        const int fr = lane >> 4, fc = lane & 15;
+        const int64_t k0 = (int64_t)I * NB;
+        const double* Y = A + Np;
+        const bool active = !(I == J && wj > wi);
+        d4 acc[4][4];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int mj = 0; mj < 4; ++mj) acc[mi][mj] = d4{0.0, 0.0, 0.0, 0.0};
+        __shared__ MmaLds sm;
+        tile_mma_neg(Y + k0 * lda + (int64_t)I * NB, Y + k0 * lda + (int64_t)J * NB, lda, (int)(Np - k0), active,
+                     acc, sm);
+        // (tile_mma_neg ends on a barrier: the staging buffer is free)
+        const TermPack& tp = *tpp;
+        const int T = tp.T;
+        double* const xr = &sm[0][0][0][0];           // xr[t * 128 + r]
+        double* const xc = xr + GAPLAC_MAX_TERMS * NB;  // xc[t * 128 + c]
+        double* const ar = xc + GAPLAC_MAX_TERMS * NB;  // alpha of the rows, then of the columns
+        double* const ac = ar + NB;
+        double* const tbl = ac + NB;                    // exp table
+        double* const red = tbl + 256;                  // red[w * (T + 1) + t]
+        const int64_t r0 = (int64_t)I * NB, c0 = (int64_t)J * NB;
+        for (int idx = tid; idx < T * NB; idx += 256) {
+            const int t = idx / NB, q = idx % NB;
+            const bool x = tp.kind[t] != GAPLAC_NOISE;
+            const double* xcol = X + (int64_t)tp.col[t] * ldx;
+            xr[t * NB + q] = (x && r0 + q < N) ? xcol[r0 + q] : 0.0;
+            xc[t * NB + q] = (x && c0 + q < N) ? xcol[c0 + q] : 0.0;
+        }
+        if (tid < NB) {
+            ar[tid] = r0 + tid < N ? alpha[r0 + tid] : 0.0;
+            ac[tid] = c0 + tid < N ? alpha[c0 + tid] : 0.0;
+        }
+        tbl[tid] = kExp2Tbl256[tid];
+        __syncthreads();
+        // weights in place (inactive waves: all zero)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+            const int rr = 64 * wi + 16 * mi + fc;
+            const int64_t i = r0 + rr;
+            const double ai = ar[rr];
+#pragma unroll
+            for (int mj = 0; mj < 4; ++mj)
+#pragma unroll
+                for (int rg = 0; rg < 4; ++rg) {
+                    const int cc = 64 * wj + 16 * mj + fr + 4 * rg;
+                    const int64_t j = c0 + cc;
+                    const bool in = active && i < N && j < N && i >= j;
+                    const double wt = in ? (i == j ? 1.0 : 2.0) : 0.0;
+                    acc[mi][mj][rg] = wt * (ai * ac[cc] + acc[mi][mj][rg]);
+                }
+        }
+        // the diagonal elements of a diagonal tile (row rr == column cc)
+        auto diag_sum = [&]() {
+            double g = 0.0;
+            if (I == J) {
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int mj = 0; mj < 4; ++mj)
+#pragma unroll
+                        for (int rg = 0; rg < 4; ++rg)
+                            if (64 * wi + 16 * mi + fc == 64 * wj + 16 * mj + fr + 4 * rg) g += acc[mi][mj][rg];
+            }
+            return g;
+        };
+#pragma unroll 1
+        for (int t = 0; t <= T; ++t) {
+            double g = 0.0;
+            const int kind = t < T ? tp.kind[t] : GAPLAC_NOISE;
+            if (kind == GAPLAC_SQEXP) {
+                const double p = tp.p[t];
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi) {
+                    const double xi = xr[t * NB + 64 * wi + 16 * mi + fc];
+#pragma unroll
+                    for (int mj = 0; mj < 4; ++mj)
+#pragma unroll
+                        for (int rg = 0; rg < 4; ++rg)
+                            g += acc[mi][mj][rg] * dk_sqexp(p, xi, xc[t * NB + 64 * wj + 16 * mj + fr + 4 * rg], tbl);
+                }
+            } else if (kind == GAPLAC_OU) {
+                const double p = tp.p[t];
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi) {
+                    const double xi = xr[t * NB + 64 * wi + 16 * mi + fc];
+#pragma unroll
+                    for (int mj = 0; mj < 4; ++mj)
+#pragma unroll
+                        for (int rg = 0; rg < 4; ++rg)
+                            g += acc[mi][mj][rg] * dk_ou(p, xi, xc[t * NB + 64 * wj + 16 * mj + fr + 4 * rg], tbl);
+                }
+            } else if (kind == GAPLAC_LINEAR) {  // d/dc (x_i x_j + c) = 1
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int mj = 0; mj < 4; ++mj)
+#pragma unroll
+                        for (int rg = 0; rg < 4; ++rg) g += acc[mi][mj][rg];
+            } else if (kind == GAPLAC_NOISE) {  // a Noise term's variance, and (t = T) the observation noise
+                g = diag_sum();
+            }  // Cat: no parameter
+            const double x = wave_sum(g);
+            if (lane == 0) red[w * (T + 1) + t] = x;
+        }
+        __syncthreads();
+        if (tid <= T) {
+            const int64_t b = (int64_t)I * (I + 1) / 2 + J;
+            const int S = T + 1;
+            partial[b * S + tid] = (red[tid] + red[S + tid]) + (red[2 * S + tid] + red[3 * S + tid]);
+        }
+    }
+    kt_end(kt);
+}
+
 // out[t] = 1/2 sum_b partial[b][t], t = 0..T, fixed order.
 __global__ __launch_bounds__(256) void grad_reduce_kernel(const double* __restrict__ partial, int nb, int T,
                                                           double* __restrict__ out) {
@@ -3095,6 +3246,16 @@ void launch_grad_contract(hipStream_t s, const double* A, int64_t lda, int64_t N
     if (!guard_launch("grad_contract_kernel", A, 0, tiles_end(lda, m - 1, m - 1))) return;
     grad_contract_kernel<<<dim3((unsigned)tiles), dim3(256), 0, s>>>(A, lda, N, X, ldx, alpha, dtp, dgp, partial,
                                                                      kt);
+}
+
+void launch_cinv_contract(hipStream_t s, const double* A, int64_t lda, int64_t Np, int64_t N, const double* X,
+                          int64_t ldx, const double* alpha, const TermPack* dtp, const uint32_t* list, int nblocks,
+                          double* partial, KTime* kt) {
+    if (nblocks <= 0) return;
+    const int m = (int)((N + NB - 1) / NB);
+    if (!guard_launch("cinv_contract_kernel", A, 0, (Np - 1) * lda + Np + (int64_t)m * NB)) return;
+    cinv_contract_kernel<<<dim3((unsigned)nblocks), dim3(256), 0, s>>>(A, lda, Np, N, X, ldx, alpha, dtp, list,
+                                                                       partial, kt);
 }
 
 void launch_grad_reduce(hipStream_t s, const double* partial, int nb, int T, double* out) {
