@@ -1600,7 +1600,27 @@ int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D, 
     // Models in flight on up to batch_lanes lanes (lane 0 = this context): an order-8192
     // evaluation alone fills the chip only ~half the time (its panel chain is a
     // latency-bound critical path), so concurrent models fill the gaps.
-    const int nl = std::max(1, std::min(ctx->batch_lanes, nmodels));
+    int nl = std::max(1, std::min(ctx->batch_lanes, nmodels));
+    {
+        // every extra lane holds a whole evaluation workspace: keep the lanes that fit in the
+        // free device memory (the workspaces already held are reusable; 2 GiB kept free),
+        // down to this context alone, and say so clearly when not even that fits
+        const int64_t Np = round_up(N + 1, NB);
+        const size_t per = (size_t)Np * (size_t)Np * sizeof(double) + (size_t)(Np / NB) * DINV_PER_BLOCK * sizeof(double);
+        size_t freeb = 0, totalb = 0;
+        if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
+            size_t held = ctx->A_elems * sizeof(double);
+            for (size_t l = 0; l + 1 < (size_t)nl && l < ctx->lanes.size(); ++l) held += ctx->lanes[l]->A_elems * sizeof(double);
+            const size_t margin = (size_t)2 << 30;
+            const size_t budget = freeb + held > margin ? freeb + held - margin : 0;
+            const int fit = (int)std::min<size_t>((size_t)nl, budget / per);
+            if (fit < 1)
+                return set_err(ctx, GAPLAC_E_OOM,
+                               "batch: one evaluation workspace at N = %lld needs %zu bytes, %zu are free (%zu held)",
+                               (long long)N, per, freeb, held);
+            nl = fit;
+        }
+    }
     while ((int)ctx->lanes.size() < nl - 1) {
         gaplac_ctx* c = nullptr;
         if ((rc = gaplac_ctx_create(ctx->device, &c))) return set_err(ctx, rc, "batch lane creation failed");

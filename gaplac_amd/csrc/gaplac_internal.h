@@ -96,6 +96,9 @@ struct TailCtl {
     unsigned dprog[TAIL_TMAX];                // D(k): block columns (and inverses) 0 .. dprog-1 final
     unsigned sdone[TAIL_TMAX * TAIL_TMAX];    // S(i,k) finished ([i][k], relative tile indices)
     unsigned units[TAIL_TMAX * TAIL_TMAX];    // tile (i,j): update units applied per column (4; 10 on the diagonal)
+    // TRSM of the sub-diagonal tile (k+1, k): per 16-row group g, the 16-column blocks of L
+    // stored so far (0..8); the next diagonal tile's Q blocks consume them as they come
+    unsigned sprog[TAIL_TMAX][8];
 };
 struct TailArgs {
     double* A;

@@ -2357,6 +2357,12 @@ __host__ __device__ __forceinline__ int tail_deep_cols(int type, int q) {
     return type == TK_U ? (q == TAIL_UD ? 4 : q == TAIL_UD8 ? 8 : q == TAIL_UD2 ? 2 : 1) : 1;
 }
 
+// Progress of a sub-diagonal TRSM's 16-row group (its wave's stores of blocks < nb
+// complete: the caller has waited vmcnt past them), for the Q blocks behind it.
+__device__ __forceinline__ void tail_sprog(unsigned* sp, unsigned nb) {
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(sp, nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Stage L_kk's 28 strictly-lower 16x16 blocks and the 8 inverses in LDS for the tail's
 // TRSM: block (b, c), c < b, at p = b(b-1)/2 + c, Ls[p*256 + m*16 + j] = L(16b + j, 16c + m);
 // inverses at p = 28 + b. Half the block (tid >> 8) takes the even p, half the odd; every
@@ -2394,7 +2400,7 @@ __device__ __forceinline__ void tail_trsm_stage(double* Ls, const Gm<AUX>& gA, c
 // strictly-lower 16x16 blocks and the 8 inverses in LDS.
 template <int AUX>
 __device__ __forceinline__ void tail_trsm(double* smem, double* Acol, int64_t lda, int k, int bi, int h,
-                                          const double* Dk) {
+                                          const double* Dk, unsigned* sprog = nullptr) {
     double* Ls = smem;  // (TRSM_LBLK + NDB) x 256
     const int tid = otid(), wave = tid >> 6, lane = tid & 63;
     const int fr = lane >> 4, fc = lane & 15;
@@ -2439,6 +2445,14 @@ __device__ __forceinline__ void tail_trsm(double* smem, double* Acol, int64_t ld
         Y[b] = y;
 #pragma unroll
         for (int q = 0; q < 4; ++q) gA.st((uint32_t)((int64_t)(16 * b + fr + 4 * q) * lda + rowb + fc), y[q]);
+        if (sprog && b >= 2) {  // blocks < b-1 stored (blocks b-1 and b's stores may be in flight)
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            tail_sprog(&sprog[(rowb / 16) & 7], (unsigned)(b - 1));
+        }
+    }
+    if (sprog) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        tail_sprog(&sprog[(rowb / 16) & 7], (unsigned)NDB);
     }
 }
 
@@ -2452,7 +2466,7 @@ __device__ __forceinline__ void tail_trsm(double* smem, double* Acol, int64_t ld
 template <int AUX>
 __device__ __forceinline__ void tail_trsm_pipe(double* smem, unsigned* rowf, double* Acol, int64_t lda, int k, int bi,
                                                int h, const double* Dk, const unsigned* prog, const unsigned* ddone,
-                                               unsigned* err, unsigned* rerr) {
+                                               unsigned* err, unsigned* rerr, unsigned* sprog = nullptr) {
     double* Ls = smem;  // (TRSM_LBLK + NDB) x 256, as tail_trsm_stage lays it out
     const int tid = otid(), wave = tid >> 6, lane = tid & 63;
     const int fr = lane >> 4, fc = lane & 15;
@@ -2567,6 +2581,14 @@ __device__ __forceinline__ void tail_trsm_pipe(double* smem, unsigned* rowf, dou
         Y[b] = y;
 #pragma unroll
         for (int q = 0; q < 4; ++q) gA.st((uint32_t)((int64_t)(16 * b + fr + 4 * q) * lda + rowb + fc), y[q]);
+        if (sprog && b >= 2) {  // blocks < b-1 stored (blocks b-1 and b's stores may be in flight)
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            tail_sprog(&sprog[4 * h + wave], (unsigned)(b - 1));
+        }
+    }
+    if (sprog) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        tail_sprog(&sprog[4 * h + wave], (unsigned)NDB);
     }
 }
 
@@ -2641,26 +2663,57 @@ __device__ __forceinline__ void tail_update(const Gm<AUX>& gC, const Gm<AUX>& gP
 // Each accumulator starts from C and takes the k-steps in order: the same rounding as the
 // per-column chain kernels, so a matrix factored in the tail and through super-panels
 // (gradient / posterior workspaces) gives bitwise the same factor.
+// Pipelined behind the sub-diagonal TRSM (sprog: its per-16-row-group progress, round 5;
+// only the next diagonal tile's blocks, i = k + 1: a Q block of a later diagonal tile gets
+// sprog = nullptr and was dispatched after its TRSM finished):
+// the k-steps of column block b are loaded once both 16-row groups this wave reads have
+// stored block b, so the block's last MFMAs follow the TRSM's end instead of its publish.
+// Bounded like the TRSM's own row wait (2^23 polls); an expiry flags the evaluation.
 template <int AUX>
 __device__ __forceinline__ void tail_q32(const Gm<AUX>& gC, const Gm<AUX>& gP, int64_t lda, int row0, int ccol0,
-                                         int qrow0) {
+                                         int qrow0, const unsigned* sprog, int grow, unsigned* err, unsigned* rerr) {
     const int tid = otid(), wave = tid >> 6, lane = tid & 63;
     if (wave >= 4) return;
     const int fr = lane >> 4, fc = lane & 15;
     const int r0 = row0 + 16 * (wave & 1), c0 = ccol0 + 16 * (wave >> 1), q0 = qrow0 + 16 * (wave >> 1);
+    // 16-row groups (within the tile) of the P rows and the Q rows
+    const int ga = ((r0 - grow) >> 4) & 7, gb = ((q0 - grow) >> 4) & 7;
     d4 acc;
 #pragma unroll
     for (int rg = 0; rg < 4; ++rg) acc[rg] = gC.ld((uint32_t)((int64_t)(c0 + fr + 4 * rg) * lda + r0 + fc));
-    constexpr int KS = NB / 4;  // 32 k-steps
-    double fa[KS], fb[KS];
+    unsigned have = sprog ? 0u : (unsigned)NDB;  // blocks both groups have stored (no sprog: all, waited before)
 #pragma unroll
-    for (int st = 0; st < KS; ++st) {
-        const int64_t col = (int64_t)(4 * st + fr) * lda;
-        fb[st] = gP.ld((uint32_t)(col + r0 + fc));
-        fa[st] = gP.ld((uint32_t)(col + q0 + fc));
+    for (int b = 0; b < NDB; ++b) {
+        if (have <= (unsigned)b) {  // lane 0 polls (light on the TRSM's counters), the wave follows
+            if (lane == 0) {
+                bool got = false;
+                for (int it = 0; it < (1 << 23); ++it) {
+                    const unsigned x = tail_ld(&sprog[ga]), y = tail_ld(&sprog[gb]);
+                    have = x < y ? x : y;
+                    if (have > (unsigned)b) {
+                        got = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (!got) {
+                    have = (unsigned)NDB;  // expired: go on with what is there, flagged
+                    atomicOr(err, 1u);
+                    atomicOr(rerr, 2u);
+                }
+            }
+            have = (unsigned)__builtin_amdgcn_readfirstlane((int)have);
+        }
+        double fa[4], fb[4];
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            const int64_t col = (int64_t)(16 * b + 4 * st + fr) * lda;
+            fb[st] = gP.ld((uint32_t)(col + r0 + fc));
+            fa[st] = gP.ld((uint32_t)(col + q0 + fc));
+        }
+#pragma unroll
+        for (int st = 0; st < 4; ++st) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[st], fb[st], acc, 0, 0, 2);  // neg B
     }
-#pragma unroll
-    for (int st = 0; st < KS; ++st) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[st], fb[st], acc, 0, 0, 2);  // neg B
 #pragma unroll
     for (int rg = 0; rg < 4; ++rg) gC.st((uint32_t)((int64_t)(c0 + fr + 4 * rg) * lda + r0 + fc), acc[rg]);
 }
@@ -2681,7 +2734,9 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int
             const unsigned ups = i == j ? TAIL_NQ : 4u;
             const int nk = tail_deep_cols(type, q);  // panel columns k .. k+nk-1
             ok = tail_ld(&c->units[i * TAIL_TMAX + j]) >= ups * k;
-            for (int c2 = 0; c2 < nk && ok; ++c2)
+            // (a Q block of the next diagonal tile, i = k + 1, follows its TRSM's progress
+            // inside tail_q32; the other Q blocks wait for their TRSM to finish)
+            for (int c2 = 0; c2 < nk && ok && !(type == TK_Q && i == k + 1); ++c2)
                 ok = tail_ld(&c->sdone[i * TAIL_TMAX + k + c2]) >= 2u && tail_ld(&c->sdone[j * TAIL_TMAX + k + c2]) >= 2u;
         }
         if (ok) return true;
@@ -2727,10 +2782,12 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
                 potrf_diag2_body<GM_SC1>(smem, colk + (int64_t)gk * NB, a.lda, a.N, (int64_t)gk * NB,
                                          Dinv + (size_t)gk * DINV_PER_BLOCK, res, nullptr, &ctl->dprog[k]);
         } else if (type == TK_S && q == TAIL_S_WHOLE) {
-            tail_trsm<GM_SC1>(smem, colk, a.lda, gk, a.ts + i, q, Dinv + (size_t)gk * DINV_PER_BLOCK);
+            tail_trsm<GM_SC1>(smem, colk, a.lda, gk, a.ts + i, q, Dinv + (size_t)gk * DINV_PER_BLOCK,
+                              i == k + 1 ? ctl->sprog[k] : nullptr);
         } else if (type == TK_S) {
             tail_trsm_pipe<GM_SC1>(smem, s_rowf, colk, a.lda, gk, a.ts + i, q, Dinv + (size_t)gk * DINV_PER_BLOCK,
-                                   &ctl->dprog[k], &ctl->ddone[k], &ctl->err, &res->err);
+                                   &ctl->dprog[k], &ctl->ddone[k], &ctl->err, &res->err,
+                                   i == k + 1 ? ctl->sprog[k] : nullptr);
         } else {
             const int gi = a.ts + i, gj = a.ts + j;
             const Gm<GM_SC1> gC(A + (int64_t)gj * NB * a.lda), gP(colk);
@@ -2748,7 +2805,8 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
             } else {
                 // q = qa (qa + 1) / 2 + qb, qb <= qa: 32x32 block (qa, qb) of the diagonal tile
                 const int qa = q >= 6 ? 3 : q >= 3 ? 2 : q >= 1 ? 1 : 0, qb = q - qa * (qa + 1) / 2;
-                tail_q32<GM_SC1>(gC, gP, a.lda, gi * NB + 32 * qa, 32 * qb, gj * NB + 32 * qb);
+                tail_q32<GM_SC1>(gC, gP, a.lda, gi * NB + 32 * qa, 32 * qb, gj * NB + 32 * qb,
+                                 i == k + 1 ? ctl->sprog[k] : nullptr, gi * NB, &ctl->err, &res->err);
             }
         }
         // publish: every wave's stores complete, then one lane bumps the counter
