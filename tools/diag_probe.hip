@@ -1,8 +1,7 @@
 // Diagnostic: the diagonal-block kernel on an idle GPU. Checks it against a CPU Cholesky of
 // the same 128x128 block (L and the 16x16 inverses), prints its per-wave stamps per panel
-// (v1 = potrf_diag_kernel_body, v2 = potrf_diag2_body, v3 = potrf_diag3_body), checks the
-// variants against each other with padding inside the block and on a non-PD block, and
-// times the other chain kernels alone.
+// (the "v1" lines; the blocked 16x16-leaf variant that was "v2" was measured slower and
+// removed), and times the other chain kernels alone.
 #define GAPLAC_STAMPS 1
 #include "../gaplac_amd/csrc/gaplac_kernels.hip"
 #include <cmath>
@@ -17,54 +16,6 @@ __global__ __launch_bounds__(256) void diag_v1(double* Ag, int64_t lda, int64_t 
 __global__ __launch_bounds__(512) void diag_v2(double* Ag, int64_t lda, int64_t N, int64_t g0, double* Dinv, EvalResult* res) {
   __shared__ double smem[DIAG2_SMEM];
   potrf_diag2_body<0>(smem, Ag, lda, N, g0, Dinv, res);
-}
-template <int DBG = 0>
-__global__ __launch_bounds__(512) void diag_v3(double* Ag, int64_t lda, int64_t N, int64_t g0, double* Dinv, EvalResult* res) {
-  __shared__ double smem[DIAG3_SMEM];
-  potrf_diag3_body<0, DBG>(smem, Ag, lda, N, g0, Dinv, res);
-}
-// rows_gather / row_bcast semantics: out[4 * lane + k] = x of lane (k, lane & 15); out[256 + lane] = x of lane 5 of the row
-__global__ void gather_check(double* out) {
-  const int l = threadIdx.x;
-  double w[4];
-  rows_gather((double)(1000 + l), w);
-  for (int k = 0; k < 4; ++k) out[4 * l + k] = w[k];
-  out[256 + l] = row_bcast((double)(1000 + l), 5);
-}
-// the pivot sweep alone: one wave, 8 sweeps of the same SPD 16x16 block (cycles per sweep)
-__global__ __launch_bounds__(64) void pivot_alone(const double* A, double* out, unsigned long long* cyc) {
-  __shared__ double rec[1024];
-  const int lane = threadIdx.x;
-  double fin[4];
-  for (int rep = 0; rep < 8; ++rep) {
-    d4 acc;
-    for (int q = 0; q < 4; ++q) acc[q] = A[((lane >> 4) + 4 * q) * 16 + (lane & 15)];
-    __builtin_amdgcn_s_waitcnt(0);
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    diag3_pivot(acc, fin, rec, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-    if (lane == 0) cyc[rep] = t1 - t0;
-  }
-  __syncthreads();
-  double sum = 0;
-  for (int c = 0; c < 16; ++c) sum += rec[c * 64 + lane];  // keeps the record writes
-  for (int q = 0; q < 4; ++q) out[q * 64 + lane] = fin[q] + sum;
-}
-// the row-wave sweep alone: all 16 records published beforehand (cycles per sweep)
-__global__ __launch_bounds__(64) void rows_alone(double* out, unsigned long long* cyc, double* Dinv, EvalResult* res) {
-  __shared__ double sm[DIAG3_SMEM];
-  const int lane = threadIdx.x;
-  for (int i = lane; i < DIAG3_SMEM; i += 64) sm[i] = 0.001 * (i % 97) + (i < 1024 && (i % 65) == 0 ? 1.0 : 0.0);
-  __syncthreads();
-  for (int rep = 0; rep < 4; ++rep) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    diag3_rows<0>(sm + DIAG3_REC + NB + 8, sm, 0, 16, lane, 16, false, Dinv, nullptr, res, (unsigned*)(sm + DIAG3_REC + NB + 2));
-    __builtin_amdgcn_s_waitcnt(0);
-    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-    if (lane == 0) cyc[rep] = t1 - t0;
-  }
-  out[lane] = sm[DIAG3_REC + NB + 8 + lane];
 }
 int main() {
   const int nt = 4, Np = nt * NB;
@@ -99,59 +50,14 @@ int main() {
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
     if (v == 1) diag_v1<<<1, 256>>>(A, Np, N, 0, Dinv, res);
-    else if (v == 2) diag_v2<<<1, 512>>>(A, Np, N, 0, Dinv, res);
-    else diag_v3<0><<<1, 512>>>(A, Np, N, 0, Dinv, res);
+    else diag_v2<<<1, 512>>>(A, Np, N, 0, Dinv, res);
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(ms, e0, e1));
     CK(hipMemcpy(out.data(), A, out.size() * 8, hipMemcpyDeviceToHost));
     CK(hipMemcpy(dinv.data(), Dinv, dinv.size() * 8, hipMemcpyDeviceToHost));
     return 0;
   };
-  {
-    double* go; CK(hipMalloc(&go, 320 * 8));
-    gather_check<<<1, 64>>>(go);
-    std::vector<double> hg(320); CK(hipMemcpy(hg.data(), go, 320 * 8, hipMemcpyDeviceToHost));
-    int bad = 0;
-    for (int l = 0; l < 64; ++l) {
-      for (int k = 0; k < 4; ++k) bad += hg[4 * l + k] != 1000 + 16 * k + (l & 15);
-      bad += hg[256 + l] != 1000 + (l & ~15) + 5;
-    }
-    printf("gather/bcast check: %d mismatches\n", bad);
-    if (bad) return 1;
-  }
-  {
-    double *pa, *po; unsigned long long* pc;
-    CK(hipMalloc(&pa, 256 * 8)); CK(hipMalloc(&po, 256 * 8)); CK(hipMalloc(&pc, 8 * 8));
-    std::vector<double> blk(256);
-    for (int j = 0; j < 16; ++j) for (int i = 0; i < 16; ++i) blk[j * 16 + i] = h[(size_t)j * Np + i];
-    CK(hipMemcpy(pa, blk.data(), 256 * 8, hipMemcpyHostToDevice));
-    pivot_alone<<<1, 64>>>(pa, po, pc);
-    unsigned long long hc[8]; CK(hipMemcpy(hc, pc, 64, hipMemcpyDeviceToHost));
-    printf("pivot sweep alone (cycles):"); for (int i = 0; i < 8; ++i) printf(" %llu", hc[i]); printf("\n");
-    rows_alone<<<1, 64>>>(po, pc, Dinv, res);
-    CK(hipDeviceSynchronize());
-    CK(hipMemcpy(hc, pc, 32, hipMemcpyDeviceToHost));
-    printf("row sweep alone, records ready (cycles):"); for (int i = 0; i < 4; ++i) printf(" %llu", hc[i]); printf("\n");
-  }
-  {  // diag3 with roles switched off (timing only): per-panel pivot sweep cycles
-    CK(hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice));
-    auto sweeps = [&](const char* name, void (*k)(double*, int64_t, int64_t, int64_t, double*, EvalResult*)) -> int {
-      for (int rep = 0; rep < 2; ++rep) {
-        launch_init_result(0, res);
-        hipLaunchKernelGGL(k, dim3(1), dim3(512), 0, 0, A, (int64_t)Np, (int64_t)1 << 30, (int64_t)0, Dinv, res);
-        CK(hipDeviceSynchronize());
-      }
-      unsigned long long st[128]; CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof st));
-      printf("  v3 %-18s sweeps:", name);
-      for (int s = 0; s < 8; ++s) printf(" %5llu", st[2 + 2 * s] - st[1 + 2 * s]);
-      printf(" | total %llu | pure sweeps:", st[19] - st[20]);
-      for (int s = 0; s < 8; ++s) printf(" %5llu", st[89 + 2 * s] - st[88 + 2 * s]);
-      printf("\n");
-      return 0;
-    };
-    if (sweeps("all roles", diag_v3<0>) || sweeps("no stores", diag_v3<8>)) return 1;
-  }
-  for (int v = 1; v <= 3; ++v) {
+  for (int v = 1; v <= 2; ++v) {
     for (int rep = 0; rep < 4; ++rep) {
       float ms;
       if (run(v, h, 1 << 30, &ms)) return 1;
@@ -172,33 +78,7 @@ int main() {
         for (int i = 0; i < j; ++i) upper = std::fmax(upper, std::fabs(out[(size_t)j * Np + i]));
       printf("diag v%d: %.1f us (event)  max|L-Lcpu| %.2e  max|Dinv L - I| %.2e  upper %.1e  info %llx err %u\n", v, ms * 1e3,
              errL, errD, upper, (unsigned long long)hr.info, hr.err);
-      if (rep == 3 && v == 3) {
-        unsigned long long st[128]; CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof st));
-        printf("  v3 load %llu\n", st[0] - st[20]);
-        for (int s = 0; s < 8; ++s) {
-          const unsigned long long p = st[1 + 2 * s];
-          printf("  v3 s=%d: sweep %5llu  to next %5llu | rows w1 %5lld w2 %5lld | M w3 %5lld w5 %5lld w6 %5lld w7 %5lld w4 %5lld\n", s,
-                 st[2 + 2 * s] - p, (s < 7 ? st[3 + 2 * s] : st[17]) - st[2 + 2 * s],
-                 s <= 6 ? (long long)(st[24 + s] - p) : -1ll, s <= 2 ? (long long)(st[32 + s] - p) : -1ll,
-                 (long long)(st[48 + s] - p), (long long)(st[64 + s] - p), (long long)(st[72 + s] - p),
-                 (long long)(st[80 + s] - p), (long long)(st[56 + s] - p));
-        }
-        for (int s = 0; s < 8; ++s) {
-          const unsigned long long p = st[1 + 2 * s];
-          printf("  v3 s=%d: pivot sweep %5lld..%5lld | rows w1 start %5lld end %5lld | w2 start %5lld end %5lld\n", s,
-                 (long long)(st[88 + 2 * s] - p), (long long)(st[89 + 2 * s] - p),
-                 s <= 7 ? (long long)(st[104 + s] - p) : -1ll, s <= 6 ? (long long)(st[24 + s] - p) : -1ll,
-                 s <= 3 ? (long long)(st[112 + s] - p) : -1ll, s <= 2 ? (long long)(st[32 + s] - p) : -1ll);
-        }
-        {
-          const unsigned long long p = st[1 + 2 * 3];
-          printf("  v3 s=3 wave 3: prelude %lld..%lld | groups at %lld %lld %lld %lld | done %lld\n",
-                 (long long)(st[120] - p), (long long)(st[121] - p), (long long)(st[122] - p), (long long)(st[123] - p),
-                 (long long)(st[124] - p), (long long)(st[125] - p), (long long)(st[126] - p));
-        }
-        printf("  v3 last %llu total %llu cycles\n", st[19] - st[17], st[19] - st[20]);
-      }
-      if (rep == 3 && v <= 2) {  // per panel s, phase 2 of each wave (cycles, s_memtime)
+      if (rep == 3) {  // per panel s, phase 2 of each wave (cycles, s_memtime)
         unsigned long long st[128]; CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof st));
         printf("  v%d load %llu\n", v, st[0] - st[20]);
         for (int s = 0; s < 8; ++s) {
@@ -225,28 +105,29 @@ int main() {
     for (int j = 0; j < Np; ++j)
       for (int i = 0; i < Np; ++i)
         if ((i >= Npad || j >= Npad) && i != j) hp[(size_t)j * Np + i] = (i == Npad && j < Npad) ? 0.3 * std::sin(j) : 0.0;
-    std::vector<double> o[4], d[4];
-    EvalResult hv[4];
-    for (int v = 1; v <= 3; ++v) {
+    std::vector<double> o[3], d[3];
+    EvalResult hv[3];
+    for (int v = 1; v <= 2; ++v) {
       if (run(v, hp, Npad, &ms)) return 1;
       o[v] = out;
       d[v] = dinv;
       CK(hipMemcpy(&hv[v], res, sizeof hv[v], hipMemcpyDeviceToHost));
     }
-    for (int v = 2; v <= 3; ++v) {
-      double dl = 0, dd = 0, up = 0;
-      for (int j = 0; j < NB; ++j)
-        for (int i = 0; i < NB; ++i) {
-          if (i >= j) dl = std::fmax(dl, std::fabs(o[v][(size_t)j * Np + i] - o[1][(size_t)j * Np + i]));
-          else up = std::fmax(up, std::fabs(o[v][(size_t)j * Np + i]));
-        }
-      for (int k = 0; k < DINV_PER_BLOCK; ++k) dd = std::fmax(dd, std::fabs(d[v][k] - d[1][k]));
-      printf("padded N=%lld: max|L%d-L1| %.2e upper %.1e max|Dinv%d-Dinv1| %.2e | info %llx/%llx err %u\n", (long long)Npad, v, dl,
-             up, v, dd, (unsigned long long)hv[1].info, (unsigned long long)hv[v].info, hv[v].err);
+    double dl = 0, dd = 0;
+    for (int j = 0; j < NB; ++j)
+      for (int i = j; i < NB; ++i) {
+        dl = std::fmax(dl, std::fabs(o[2][(size_t)j * Np + i] - o[1][(size_t)j * Np + i]));
+
+      }
+    for (int k = 0; k < DINV_PER_BLOCK; ++k) {
+      dd = std::fmax(dd, std::fabs(d[2][k] - d[1][k]));
+
     }
+    printf("padded N=%lld: max|L2-L1| %.2e max|Dinv2-Dinv1| %.2e | info %llx/%llx err %u\n", (long long)Npad, dl, dd,
+           (unsigned long long)hv[1].info, (unsigned long long)hv[2].info, hv[2].err);
   }
   // non-PD: zero the block's (37,37) pivot region -> info must be 38 in both
-  for (int v = 1; v <= 3; ++v) {
+  for (int v = 1; v <= 2; ++v) {
     std::vector<double> hb = h;
     for (int i = 0; i < Np; ++i) { hb[(size_t)37 * Np + i] = 0; hb[(size_t)i * Np + 37] = 0; }
     float ms;
