@@ -76,6 +76,8 @@ struct gaplac_ctx {
     int grad_fused = 1;     // GAPLAC_GRAD_FUSED: -C^{-1} contracted inside cinv_contract_kernel (0: stored, then contracted)
     bool grad_singletons = true;  // the gradient's formula has single-term groups only (the fused path's case)
     int la_tiles_m = 120;   // GAPLAC_LA_TILES_M: the lookahead of >= this many tile rows as whole tiles (0: never)
+    int tail_subq = 0;      // GAPLAC_TAIL_SUBQ: near-diagonal tiles this many columns ahead updated as quadrants
+    int tail_subd = 1;      // GAPLAC_TAIL_SUBD: ... the tiles within this distance of the diagonal
     int pair_m = 40;      // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
     int pair_depth = 0;   // GAPLAC_PAIR_DEPTH: super-panels per deferred bulk update (0: 4 from 256 tile
                           //   columns on, else 2; N = 65536 1439 -> 1427 ms, 16k 26.97 -> 27.14 ms at 3-4)
@@ -693,13 +695,15 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             }
             if (ctx->dry) {  // gaplac_plan_check: the task list's dependency order
                 std::vector<uint32_t> host;
-                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X);
+                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X, ctx->tail_subq,
+                                 ctx->tail_subd);
                 std::string why;
                 if (!check_tail_tasks(T, host, &why, X)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
             }
             if ((ctx->ttasks_T != T || ctx->ttasks_X != X) && !ctx->dry) {
                 std::vector<uint32_t> host;
-                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X);
+                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X, ctx->tail_subq,
+                                 ctx->tail_subd);
                 int rc;
                 if ((rc = ensure(ctx, &ctx->ttasks, &ctx->ttasks_elems, host.size()))) return rc;
                 HIPCK(ctx, hipMemcpy(ctx->ttasks, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -1316,6 +1320,8 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_PAIR_DEPTH")) ctx->pair_depth = std::max(2, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BAND_TILES_M")) ctx->band_tiles_m = std::max(1, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_LA_TILES_M")) ctx->la_tiles_m = std::max(0, std::atoi(s));
+    if (const char* s = std::getenv("GAPLAC_TAIL_SUBQ")) ctx->tail_subq = std::max(0, std::min(8, std::atoi(s)));
+    if (const char* s = std::getenv("GAPLAC_TAIL_SUBD")) ctx->tail_subd = std::max(1, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_GRAD_FUSED")) ctx->grad_fused = s[0] != '0';
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAILK")) ctx->tailk = s[0] != '0';
@@ -1892,6 +1898,19 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
                         std::string why;
                         if (!check_tail_tasks(T, l, &why)) return why + " (gw " + std::to_string(gw) + ", near " +
                                                                   std::to_string(near) + ")";
+                    }
+            // single evaluations with sub-diagonal quadrant updates (GAPLAC_TAIL_SUBQ), with
+            // and without the posterior's extra rows
+            for (int T = 1; T <= TAIL_TMAX; ++T)
+                for (int sq : {1, 4, 8})
+                    for (int sd : {1, 2, 4})
+                    for (int X : {0, 2}) {
+                        if (T + X > TAIL_TMAX) continue;  // (the launch condition)
+                        std::vector<uint32_t> l;
+                        build_tail_tasks(T, l, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X, sq, sd);
+                        std::string why;
+                        if (!check_tail_tasks(T, l, &why, X))
+                            return why + " (sub_ahead " + std::to_string(sq) + ", sub_dist " + std::to_string(sd) + ")";
                     }
             // batched launches: each model's tasks, read out of the interleaved list, are
             // its single list in order (so each is a topological order of its own dataflow)

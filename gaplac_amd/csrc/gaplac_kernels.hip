@@ -2882,7 +2882,7 @@ void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<s
 // Single evaluations use GW = 4, NEAR = 4 (latency); batched launches fewer per-column
 // updates (throughput).
 void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart, int gw, int near,
-                      int quad_last, bool whole_trsm, int group, int xrows) {
+                      int quad_last, bool whole_trsm, int group, int xrows, int sub_ahead, int sub_dist) {
     group = group >= 4 ? 4 : group >= 2 ? 2 : 1;  // divides the deep width (4 or 8): groups stay in a block
     // deep width; near distance (>= 2: the next two diagonal tiles take per-column Q tasks)
     const int GW = gw == 8 ? 8 : 4, NEAR = std::max(2, near);
@@ -2965,6 +2965,12 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
         for (int j = g + 2; j < std::min(jfar, T); ++j)
             for (int i = j; i < T; ++i) {
                 if (i == g + 2 && j == g + 2) continue;  // the Q tasks above
+                if (i > j && i - j <= sub_dist && j <= g + 1 + sub_ahead && g >= T - quad_last) {
+                    // a near-diagonal tile a few columns ahead: quadrant tasks, so that its
+                    // update chain catches up after a deep update
+                    for (int q = 1; q <= 4; ++q) out.push_back(tail_enc(TK_U, q, g, i, j));
+                    continue;
+                }
                 if (grouped && (i == j ? j >= g1 + 3 : j >= g1 + 2)) {
                     if (g == g1) out.push_back(tail_enc(TK_U, qgroup, g0, i, j));
                     continue;
