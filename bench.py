@@ -126,8 +126,8 @@ def cpu_baseline(N: int, budget_s: float = 25.0):
 
 # PMC traffic of the dominant kernel (tools/profile_round.sh: FETCH_SIZE / WRITE_SIZE
 # passes over the same command, corrected per MI355X_MICROARCH.md; per launch).
-TRAFFIC_FILE = os.path.join("profiles", "r04final_traffic_syrk.json")
-TRAFFIC_FILE_CINV = os.path.join("profiles", "r04final_traffic_cinv.json")
+TRAFFIC_FILE = os.path.join("profiles", "r05final_traffic_syrk.json")
+TRAFFIC_FILE_CINV = os.path.join("profiles", "r05final_traffic_cinv.json")
 
 
 def load_traffic(name=TRAFFIC_FILE):
@@ -737,15 +737,17 @@ def main_grad(args):
     if st_ev["cinv_launches"] > 0 and st_ev["cinv_ms"] > 0:
         avg_s = st_ev["cinv_ms"] / st_ev["cinv_launches"] / 1e3
         ach = cinv_flops / avg_s / 1e12
-        roofline = {"bound": "mfma", "kernel": "cinv_tile_kernel (-C^{-1} = -L^{-T} L^{-1} lower tiles, fp64 MFMA 16x16x4)",
+        roofline = {"bound": "mfma",
+                    "kernel": "cinv_contract_kernel (-C^{-1} = -L^{-T} L^{-1} lower tiles on fp64 MFMA 16x16x4, each "
+                              "contracted with every dC/dtheta in place: never stored)",
                     "achieved": round(ach, 3), "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(ach / PEAK_F64_TFLOPS, 4), "traffic": load_traffic(TRAFFIC_FILE_CINV)[0],
                     "traffic_source": load_traffic(TRAFFIC_FILE_CINV)[1],
-                    # Y's upper triangle read once + M's lower triangle written once
-                    "traffic_algorithmic": 2 * 8.0 * Np * (Np + 1) / 2,
+                    # Y's upper triangle read once (the -C^{-1} tiles are not written)
+                    "traffic_algorithmic": 8.0 * Np * (Np + 1) / 2,
                     "flops_per_launch": cinv_flops, "avg_launch_ms": avg_s * 1e3,
                     "launches": st_ev["cinv_launches"],
-                    "timing": "hipEvents on s_main around every cinv_tile_kernel launch inside the timed region"}
+                    "timing": "hipEvents on s_main around every cinv_contract_kernel launch inside the timed region"}
     grad_flops = N ** 3  # potrf N^3/3 + identity rows (L^{-T}) N^3/3 + C^{-1} N^3/3
     tf = grad_flops * (value / world) / 1e12
     extra = {"whole_eval": {"flops_per_eval": grad_flops, "achieved_tflops_per_gpu": round(tf, 3),

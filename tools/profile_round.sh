@@ -14,6 +14,6 @@ python tools/pmc_traffic.py gpurun_out/$R/pmc_fetch gpurun_out/$R/pmc_write gpur
 python tools/pmc_traffic.py gpurun_out/$R/pmc_fetch gpurun_out/$R/pmc_write gpurun_out/$R/traffic_gram.json gram_queue_kernel || exit 5
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/$R/pmc_fetch_g -o run --output-format csv -- python bench.py --mode grad --steps 1 --warmup 1 --skip-cpu --no-extra --no-profile > gpurun_out/$R/pmc_fetch_g.log 2>&1 || exit 6
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/$R/pmc_write_g -o run --output-format csv -- python bench.py --mode grad --steps 1 --warmup 1 --skip-cpu --no-extra --no-profile > gpurun_out/$R/pmc_write_g.log 2>&1 || exit 7
-python tools/pmc_traffic.py gpurun_out/$R/pmc_fetch_g gpurun_out/$R/pmc_write_g gpurun_out/$R/traffic_cinv.json cinv_tile_kernel || exit 8
+python tools/pmc_traffic.py gpurun_out/$R/pmc_fetch_g gpurun_out/$R/pmc_write_g gpurun_out/$R/traffic_cinv.json cinv_contract_kernel || exit 8
 timeout -k 10 400 python bench.py > gpurun_out/$R/bench.json 2> gpurun_out/$R/bench.err || exit 9
 cat gpurun_out/$R/bench.json
