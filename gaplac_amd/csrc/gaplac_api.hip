@@ -718,7 +718,8 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
                                      : ctx->ttasks_n;
             if (!ctx->ttrace_path.empty() && !ctx->dry) {
                 int rc;
-                if ((rc = ensure(ctx, &ctx->ttrace, &ctx->ttrace_elems, 3 * (size_t)nts))) return rc;
+                if ((rc = ensure(ctx, &ctx->ttrace, &ctx->ttrace_elems, 3 * (size_t)nts + (size_t)TAIL_DSTAMPS * T)))
+                    return rc;
             }
             TailArgs ta{ctx->A, lda, N, ts, T, ctx->Dinv, ctx->dres, ctx->tctl, ctx->ttasks, nts,
                         ctx->ttrace_path.empty() ? nullptr : ctx->ttrace};
@@ -1010,6 +1011,18 @@ int eval_device(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp, EvalR
                 std::fprintf(f, "%zu %u %llu %llu %llu\n", i, tk[i], tr[3 * i], tr[3 * i + 1], tr[3 * i + 2]);
             std::fclose(f);
         }
+        // the diagonal blocks' phase times (potrf_diag2_body), one line per tile column
+        std::vector<unsigned long long> ds((size_t)TAIL_DSTAMPS * ctx->ttasks_T);
+        HIPCK(ctx, hipMemcpy(ds.data(), ctx->ttrace + 3 * (size_t)ctx->ttasks_n, ds.size() * 8, hipMemcpyDeviceToHost));
+        if (FILE* f = std::fopen((ctx->ttrace_path + ".d").c_str(), "a")) {
+            std::fprintf(f, "# N=%lld T=%d\n", (long long)N, ctx->ttasks_T);
+            for (int k = 0; k < ctx->ttasks_T; ++k) {
+                std::fprintf(f, "%d", k);
+                for (int i = 0; i < TAIL_DSTAMPS; ++i) std::fprintf(f, " %llu", ds[(size_t)TAIL_DSTAMPS * k + i]);
+                std::fprintf(f, "\n");
+            }
+            std::fclose(f);
+        }
     }
     if (prof) {
         rc = accumulate_slots(ctx, ctx->slots);
@@ -1223,7 +1236,9 @@ static int batch_tail_enqueue(gaplac_ctx* ctx, int64_t N, const std::vector<Term
         w.tasks_n = (int)all.size();
     }
     const bool trace = !ctx->ttrace_path.empty();  // diagnostics: launches one at a time
-    if (trace && (rc = ensure(ctx, &ctx->ttrace, &ctx->ttrace_elems, 3 * (size_t)w.tasks_n))) return rc;
+    // (+ the diagonal blocks' phase times, which a one-model launch records)
+    if (trace && (rc = ensure(ctx, &ctx->ttrace, &ctx->ttrace_elems, 3 * (size_t)w.tasks_n + (size_t)TAIL_DSTAMPS * nt)))
+        return rc;
     hipStream_t g = ctx->s_panel, s = ctx->s_main;
     for (int b = 0; b < B; ++b) w.htp[b] = packs[(size_t)(m0 + b)];
     // From the first enqueue on, a failure must not leave this call's work in flight (the

@@ -109,7 +109,9 @@ struct TailArgs {
     TailCtl* ctl;
     const uint32_t* tasks;
     int ntasks;
-    unsigned long long* trace;  // diagnostics (GAPLAC_TAIL_TRACE): per task dequeue / start / end times, or nullptr
+    unsigned long long* trace;  // diagnostics (GAPLAC_TAIL_TRACE): per task dequeue / start / end times, or nullptr;
+                                // single-model launches: then TAIL_DSTAMPS phase times per diagonal block at
+                                // trace + 3 ntasks + TAIL_DSTAMPS k (potrf_diag2_body)
     // several models in one launch (gaplac_logpdf_batch): task bits 27.. hold the model m,
     // whose matrix is A + m a_stride, inverses Dinv + m dinv_stride, result res + m,
     // counters ctl + m (ctl[0].head is the one dequeue counter)
@@ -121,6 +123,7 @@ struct TailArgs {
     int fault = -1;
     int xrows = 0;  // extra tile rows below the matrix factored along (tile rows ts+T .. ts+T+xrows-1)
 };
+constexpr int TAIL_DSTAMPS = 20;  // start, load in LDS, per panel s: phase 2 start / end, done
 constexpr int TAIL_MODEL_SHIFT = 27;
 constexpr int TAIL_MAX_MODELS = 32;
 // colstart (optional): index in out where the tasks of tile column g = 0 .. T-2 begin.

@@ -1117,11 +1117,17 @@ __device__ __forceinline__ void diag2_store_column(const double* Ab, double* Ag,
 template <int AUX>
 __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restrict__ Ag, int64_t lda, int64_t N,
                                                  int64_t g0, double* __restrict__ Dinv, EvalResult* __restrict__ res,
-                                                 double* Dl = nullptr, unsigned* prog = nullptr) {
+                                                 double* Dl = nullptr, unsigned* prog = nullptr,
+                                                 unsigned long long* dst = nullptr) {
     double* colbuf = smem;
     double* rdiag = colbuf + DIAG2_COLBUF;
     double* Ab = rdiag + NB;
     const int t = otid(), wave = t >> 6, lane = t & 63;
+    // diagnostics (tail trace): phase times on the 100 MHz clock, thread 0
+    auto dstamp = [&](int i) {
+        if (dst && t == 0) dst[i] = wall_clock64();
+    };
+    dstamp(0);
     // the chain first (wave-uniform branches: s_setprio takes an immediate)
     if (wave == 0) __builtin_amdgcn_s_setprio(3);
     else if (wave == 1) __builtin_amdgcn_s_setprio(2);
@@ -1165,6 +1171,7 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     STAMP(0);
+    dstamp(1);
     for (int s = 0; s < NDB; ++s) {
         if (s >= 1) {
             // phase 1: panel s-1 into block column s (the diagonal block first, on wave 0)
@@ -1179,6 +1186,7 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
             __syncthreads();
         }
         STAMP(1 + 2 * s);
+        dstamp(2 + 2 * s);
         // phase 2
         if (prog && s >= 2 && wave == 3 && lane == 0)  // columns and inverses 0 .. s-2 final
             __hip_atomic_store(prog, (unsigned)(s - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1220,6 +1228,7 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
         STAMPT(384, 64 + s);
         STAMPT(448, 72 + s);
         __syncthreads();
+        dstamp(3 + 2 * s);
     }
     if (wave == 3 && lane < 16) rdiag[16 * (NDB - 1) + lane] = colbuf[lane * 64 + lane];
     if (prog && wave >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1231,6 +1240,7 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
     STAMP(18);
     if (wave != 4) diag2_store_column<AUX>(Ab, Ag, lda, NDB - 1, wave < 4 ? t : t - 64, 448);
     STAMP(19);
+    dstamp(19);
 }
 // ---------------------------------------------------------------------------------
 // Diagonal block, round 5 (potrf_diag3_body): the same arithmetic contract as diag2
@@ -3239,7 +3249,10 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
                                              Dinv + (size_t)gk * DINV_PER_BLOCK, res, nullptr, &ctl->dprog[k]);
                 else
                     potrf_diag2_body<GM_SC1>(smem, colk + (int64_t)gk * NB, a.lda, a.N, (int64_t)gk * NB,
-                                             Dinv + (size_t)gk * DINV_PER_BLOCK, res, nullptr, &ctl->dprog[k]);
+                                             Dinv + (size_t)gk * DINV_PER_BLOCK, res, nullptr, &ctl->dprog[k],
+                                             a.trace && a.nmodels == 1
+                                                 ? a.trace + 3 * (size_t)a.ntasks + (size_t)TAIL_DSTAMPS * k
+                                                 : nullptr);
             }
         } else if (type == TK_S && q == TAIL_S_WHOLE) {
             tail_trsm<GM_SC1>(smem, colk, a.lda, gk, a.ts + i, q, Dinv + (size_t)gk * DINV_PER_BLOCK,
