@@ -139,9 +139,13 @@ constexpr int TAIL_MAX_MODELS = 32;
 // sub_ahead > 0: in the last quad_last columns the tiles (i, j) with 1 <= i - j <= sub_dist
 // of the next sub_ahead tile columns past g+1 are also updated as quadrant tasks (the
 // chains of per-column updates that the near-diagonal TRSMs wait for keep the pace).
+// crit_quads > 0: column g's updates of tiles (g+1+d, g+1), 1 <= d <= crit_quads, are
+// quadrant tasks in every column (not only the last quad_last).
+// diag_quads: the near diagonal tiles' per-column updates as three lower quadrant tasks.
 void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart = nullptr, int gw = 4,
                       int near = 4, int quad_last = TAIL_TMAX, bool whole_trsm = false, int group = 1,
-                      int xrows = 0, int sub_ahead = 0, int sub_dist = 1);
+                      int xrows = 0, int sub_ahead = 0, int sub_dist = 1, int crit_quads = 0,
+                      bool diag_quads = false);
 // B models' task lists interleaved (each model's own order kept, so the result is a
 // topological order per model). lag = 0: task by task, all models in step. lag > 0: a
 // software pipeline: model m runs lag * m tile columns behind model 0, and the tasks of the

@@ -2816,6 +2816,18 @@ constexpr int TAIL_UD2 = 7;    // U task q: a whole tile with the 2 columns k, k
 __host__ __device__ __forceinline__ int tail_deep_cols(int type, int q) {
     return type == TK_U ? (q == TAIL_UD ? 4 : q == TAIL_UD8 ? 8 : q == TAIL_UD2 ? 2 : 1) : 1;
 }
+// units an update task adds to its tile's counter (a tile column's update is 4 units off
+// the diagonal, TAIL_NQ = 10 on it). Quadrant tasks q = 1 .. 4 (qi = (q-1) >> 1, qj =
+// (q-1) & 1): 1 unit off the diagonal; on it only the lower three run, holding 3, 4 and 3
+// of the ten lower 32x32 blocks (q = 2, the upper quadrant, is never listed there).
+__host__ __device__ __forceinline__ unsigned tail_unit_add(int type, int q, int i, int j) {
+    const unsigned whole = i == j ? TAIL_NQ : 4u;
+    if (type == TK_Q) return 1u;
+    if (q == 0) return whole;
+    const int nk = tail_deep_cols(type, q);
+    if (nk > 1) return (unsigned)nk * whole;
+    return i != j ? 1u : q == 3 ? 4u : q == 2 ? 0u : 3u;
+}
 
 // Progress of a sub-diagonal TRSM's 16-row group (its wave's stores of blocks < nb
 // complete: the caller has waited vmcnt past them), for the Q blocks behind it.
@@ -3292,10 +3304,8 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
                 __hip_atomic_fetch_add(&ctl->sdone[i * TAIL_TMAX + k], q == TAIL_S_WHOLE ? 2u : 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             } else {
-                const unsigned whole = i == j ? TAIL_NQ : 4u;
-                const int nk = tail_deep_cols(type, q);
-                const unsigned add = type == TK_Q ? 1u : q == 0 ? whole : nk > 1 ? (unsigned)nk * whole : 1u;
-                __hip_atomic_fetch_add(&ctl->units[i * TAIL_TMAX + j], add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(&ctl->units[i * TAIL_TMAX + j], tail_unit_add(type, q, i, j), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
             }
             if (a.trace) a.trace[3 * tk + 2] = wall_clock64();
         }
@@ -3355,7 +3365,8 @@ void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<s
 // Single evaluations use GW = 4, NEAR = 4 (latency); batched launches fewer per-column
 // updates (throughput).
 void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart, int gw, int near,
-                      int quad_last, bool whole_trsm, int group, int xrows, int sub_ahead, int sub_dist) {
+                      int quad_last, bool whole_trsm, int group, int xrows, int sub_ahead, int sub_dist,
+                      int crit_quads, bool diag_quads) {
     group = group >= 4 ? 4 : group >= 2 ? 2 : 1;  // divides the deep width (4 or 8): groups stay in a block
     // deep width; near distance (>= 2: the next two diagonal tiles take per-column Q tasks)
     const int GW = gw == 8 ? 8 : 4, NEAR = std::max(2, near);
@@ -3377,7 +3388,9 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
     };
     auto Uq = [&](int i, int j, int k) {  // quadrants of off-diagonal tile (i, j) (or the whole tile)
         if (i < T) {
-            if (k < T - quad_last)
+            // (the next column's first crit_quads sub-diagonal tiles always in quadrants: the
+            // TRSM pipelined behind D(k+1) needs tile (k+2, k+1) within one D)
+            if (k < T - quad_last && !(j == k + 1 && i - j <= crit_quads))
                 out.push_back(tail_enc(TK_U, 0, k, i, j));
             else
                 for (int q = 1; q <= 4; ++q) out.push_back(tail_enc(TK_U, q, k, i, j));
@@ -3448,6 +3461,13 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
                     if (g == g1) out.push_back(tail_enc(TK_U, qgroup, g0, i, j));
                     continue;
                 }
+                if (diag_quads && i == j) {
+                    // a diagonal tile's per-column update as its three lower quadrants: the
+                    // tile's serial chain of K = 128 updates keeps ahead of the diagonal
+                    // blocks (one whole-tile task is ~24 us of a ~31 us column)
+                    for (int q : {1, 3, 4}) out.push_back(tail_enc(TK_U, q, g, i, j));
+                    continue;
+                }
                 out.push_back(tail_enc(TK_U, 0, g, i, j));
             }
         for (uint32_t e : later[(size_t)g]) out.push_back(e);
@@ -3502,7 +3522,9 @@ bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why
             for (int c = 0; c < nk; ++c)
                 if (sdone[(size_t)i * T + k + c] < 2u || sdone[(size_t)j * T + k + c] < 2u)
                     return fail(n, "update before its panel TRSMs");
-            const unsigned add = type == TK_Q ? 1u : q == 0 ? whole : nk > 1 ? (unsigned)nk * whole : 1u;
+            if (type == TK_U && nk == 1 && q != 0 && (q > 4 || (i == j && q == 2)))
+                return fail(n, "an update quadrant that does not exist (or the diagonal tile's upper one)");
+            const unsigned add = tail_unit_add(type, q, i, j);
             // a whole-column step must start exactly at column k (no column skipped or repeated)
             if ((type == TK_U && (q == 0 || nk > 1)) && units[(size_t)i * T + j] != whole * (unsigned)k)
                 return fail(n, "update repeats or skips a column");
