@@ -80,6 +80,7 @@ struct gaplac_ctx {
     int tail_subd = 1;      // GAPLAC_TAIL_SUBD: ... the tiles within this distance of the diagonal
     int tail_critq = 0;     // GAPLAC_TAIL_CRITQ: the next tile column's first this many sub-diagonal tiles as quadrants
     bool tail_diagq = false;  // GAPLAC_TAIL_DIAGQ: near diagonal tiles' per-column updates as three quadrant tasks
+    bool tail_fuseq = false;  // GAPLAC_TAIL_FUSEQ: each diagonal block applies its tile's last update itself
     int pair_m = 40;      // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
     int pair_depth = 0;   // GAPLAC_PAIR_DEPTH: super-panels per deferred bulk update (0: 4 from 256 tile
                           //   columns on, else 2; N = 65536 1439 -> 1427 ms, 16k 26.97 -> 27.14 ms at 3-4)
@@ -698,14 +699,14 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             if (ctx->dry) {  // gaplac_plan_check: the task list's dependency order
                 std::vector<uint32_t> host;
                 build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X, ctx->tail_subq,
-                                 ctx->tail_subd, ctx->tail_critq, ctx->tail_diagq);
+                                 ctx->tail_subd, ctx->tail_critq, ctx->tail_diagq, ctx->tail_fuseq);
                 std::string why;
                 if (!check_tail_tasks(T, host, &why, X)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
             }
             if ((ctx->ttasks_T != T || ctx->ttasks_X != X) && !ctx->dry) {
                 std::vector<uint32_t> host;
                 build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X, ctx->tail_subq,
-                                 ctx->tail_subd, ctx->tail_critq, ctx->tail_diagq);
+                                 ctx->tail_subd, ctx->tail_critq, ctx->tail_diagq, ctx->tail_fuseq);
                 int rc;
                 if ((rc = ensure(ctx, &ctx->ttasks, &ctx->ttasks_elems, host.size()))) return rc;
                 HIPCK(ctx, hipMemcpy(ctx->ttasks, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -1341,6 +1342,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_TAIL_SUBD")) ctx->tail_subd = std::max(1, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAIL_CRITQ")) ctx->tail_critq = std::max(0, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAIL_DIAGQ")) ctx->tail_diagq = s[0] != '0';
+    if (const char* s = std::getenv("GAPLAC_TAIL_FUSEQ")) ctx->tail_fuseq = s[0] != '0';
     if (const char* s = std::getenv("GAPLAC_GRAD_FUSED")) ctx->grad_fused = s[0] != '0';
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAILK")) ctx->tailk = s[0] != '0';
@@ -1925,16 +1927,19 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
                     for (int sd : {1, 2, 4})
                     for (int cq : {0, 2})
                     for (int dq : {0, 1})
+                    for (int fq : {0, 1})
                     for (int X : {0, 2}) {
                         if ((sq == 0 && sd != 1) || (cq != 0 && sq != 0 && sd != 2)) continue;  // (bounded sweep)
+                        if (fq && (sd == 4 || (cq != 0 && dq == 0))) continue;
                         if (T + X > TAIL_TMAX) continue;  // (the launch condition)
                         std::vector<uint32_t> l;
                         build_tail_tasks(T, l, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X, sq, sd, cq,
-                                         dq != 0);
+                                         dq != 0, fq != 0);
                         std::string why;
                         if (!check_tail_tasks(T, l, &why, X))
                             return why + " (sub_ahead " + std::to_string(sq) + ", sub_dist " + std::to_string(sd) +
-                                   ", crit_quads " + std::to_string(cq) + ", diag_quads " + std::to_string(dq) + ")";
+                                   ", crit_quads " + std::to_string(cq) + ", diag_quads " + std::to_string(dq) +
+                                   ", fuse_q " + std::to_string(fq) + ")";
                     }
             // batched launches: each model's tasks, read out of the interleaved list, are
             // its single list in order (so each is a topological order of its own dataflow)

@@ -142,10 +142,12 @@ constexpr int TAIL_MAX_MODELS = 32;
 // crit_quads > 0: column g's updates of tiles (g+1+d, g+1), 1 <= d <= crit_quads, are
 // quadrant tasks in every column (not only the last quad_last).
 // diag_quads: the near diagonal tiles' per-column updates as three lower quadrant tasks.
+// fuse_q: no Q blocks for the next diagonal tile; D(g+1) (task q = 1) applies column g's
+// update to its tile in LDS, pipelined behind S(g+1, g) (diag2_fused_load).
 void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart = nullptr, int gw = 4,
                       int near = 4, int quad_last = TAIL_TMAX, bool whole_trsm = false, int group = 1,
                       int xrows = 0, int sub_ahead = 0, int sub_dist = 1, int crit_quads = 0,
-                      bool diag_quads = false);
+                      bool diag_quads = false, bool fuse_q = false);
 // B models' task lists interleaved (each model's own order kept, so the result is a
 // topological order per model). lag = 0: task by task, all models in step. lag > 0: a
 // software pipeline: model m runs lag * m tile columns behind model 0, and the tasks of the

@@ -1114,11 +1114,103 @@ __device__ __forceinline__ void diag2_store_column(const double* Ab, double* Ag,
 // 512 threads: wave 0 = A (the pivot chain), wave 1 = B (rows 64+ of panels 0-3), waves 2-7
 // the trailing updates, the stores of finished block columns and (wave 7) the inverses.
 // Waves w and w + 4 share a SIMD, so every SIMD's matrix pipe takes trailing work.
+// Fused next-diagonal update (tail D task q = 1, GAPLAC_TAIL_FUSEQ): the diagonal block
+// itself applies the previous tile column's update C -= L L^T (L = tile (k, k-1), written
+// by the TRSM pipelined behind D(k-1)) into LDS instead of ten Q tasks storing the tile and
+// the block loading it back. Each of the 36 lower 16x16 blocks takes exactly tail_q32's
+// MFMA sequence (accumulator from C, k-steps 4 at a time in order), so the factor is
+// bitwise the Q path's. Block m = wave + 8 s; the k-steps of column block b once every
+// 16-row group of the TRSM has stored block b (sprog), bounded like tail_q32's poll.
 template <int AUX>
+__device__ __forceinline__ void diag2_fused_load(double* Ab, const double* Ag, const double* P, int64_t lda,
+                                                 const unsigned* sprog, unsigned* err, unsigned* rerr) {
+    const int t = otid(), wave = t >> 6, lane = t & 63, fr = lane >> 4, fc = lane & 15;
+    const Gm<AUX> gC(Ag), gP(P);
+    constexpr int NS = (NPK + 7) / 8;  // 5 blocks per wave at most
+    int bI[NS], bJ[NS];
+    d4 acc[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const int m = wave + 8 * s;
+        int I = 0;
+        while ((I + 1) * (I + 2) / 2 <= m) ++I;
+        bI[s] = I;
+        bJ[s] = m - I * (I + 1) / 2;
+        if (m < NPK) {
+#pragma unroll
+            for (int rg = 0; rg < 4; ++rg)
+                acc[s][rg] = gC.ld((uint32_t)((int64_t)(16 * bJ[s] + fr + 4 * rg) * lda + 16 * bI[s] + fc));
+        }
+    }
+    // column block b of L staged once per workgroup (16 columns x 128 rows, coalesced), the
+    // fragments then read from LDS: ~9x fewer handed-off loads than per-block fragments
+    double* stg = Ab + NPK * 256;
+    unsigned have = 0;
+#pragma unroll 1
+    for (int b = 0; b < NDB; ++b) {
+        if (t == 0 && have <= (unsigned)b) {  // one lane polls; the barrier below releases the rest
+            bool got = false;
+            for (int it = 0; it < (1 << 23); ++it) {
+                unsigned mn = __hip_atomic_load(&sprog[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                for (int g = 1; g < NDB; ++g) {
+                    const unsigned x = __hip_atomic_load(&sprog[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    mn = x < mn ? x : mn;
+                }
+                have = mn;
+                if (have > (unsigned)b) {
+                    got = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (!got) {
+                have = (unsigned)NDB;  // expired: go on with what is there, flagged
+                atomicOr(err, 1u);
+                atomicOr(rerr, 2u);
+            }
+        }
+        __syncthreads();  // (also: every wave is done reading the previous block's staging)
+        {
+            double x[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int e = t + 512 * i;
+                x[i] = gP.ld((uint32_t)((int64_t)(16 * b + (e >> 7)) * lda + (e & 127)));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) stg[t + 512 * i] = x[i];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (wave + 8 * s < NPK) {
+                double fa[4], fb[4];
+#pragma unroll
+                for (int st = 0; st < 4; ++st) {
+                    const int col = (4 * st + fr) * 128;
+                    fb[st] = stg[col + 16 * bI[s] + fc];
+                    fa[st] = stg[col + 16 * bJ[s] + fc];
+                }
+#pragma unroll
+                for (int st = 0; st < 4; ++st)
+                    acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[st], fb[st], acc[s], 0, 0, 2);  // neg B
+            }
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+        if (wave + 8 * s < NPK)
+#pragma unroll
+            for (int rg = 0; rg < 4; ++rg) Ab[bidx(bI[s], bJ[s]) * 256 + (fr + 4 * rg) * 16 + fc] = acc[s][rg];
+}
+
+template <int AUX, bool FUSED = false>
 __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restrict__ Ag, int64_t lda, int64_t N,
                                                  int64_t g0, double* __restrict__ Dinv, EvalResult* __restrict__ res,
                                                  double* Dl = nullptr, unsigned* prog = nullptr,
-                                                 unsigned long long* dst = nullptr) {
+                                                 unsigned long long* dst = nullptr, const double* fP = nullptr,
+                                                 const unsigned* fsprog = nullptr, unsigned* ferr = nullptr) {
     double* colbuf = smem;
     double* rdiag = colbuf + DIAG2_COLBUF;
     double* Ab = rdiag + NB;
@@ -1137,7 +1229,9 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
     // waves 2-7, written to LDS while panel 0 is swept.
     double2 rest[10];
     const int tt = t - 128;  // waves 2-7: 0 .. 383
-    {
+    if constexpr (FUSED) {
+        diag2_fused_load<AUX>(Ab, Ag, fP, lda, fsprog, ferr, &res->err);
+    } else {
         const Gm<AUX> g(Ag);
         double2 col0[2];
 #pragma unroll
@@ -1195,7 +1289,7 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
         } else if (wave == 1 && s < 4) {
             diag2_sweep_b(Ab, colbuf, s, lane, res);
         } else {
-            if (s == 0 && wave >= 2) {  // the rest of the block into LDS
+            if (!FUSED && s == 0 && wave >= 2) {  // the rest of the block into LDS
 #pragma unroll
                 for (int i = 0; i < 10; ++i) {
                     const int q = tt + 384 * i;
@@ -3197,8 +3291,8 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int
     const unsigned long long t0 = wall_clock64();
     for (unsigned it = 1;; ++it) {
         bool ok;
-        if (type == TK_D) {
-            ok = tail_ld(&c->units[k * TAIL_TMAX + k]) >= TAIL_NQ * k;
+        if (type == TK_D) {  // (q = 1: applies column k-1's update itself, behind its TRSM)
+            ok = tail_ld(&c->units[k * TAIL_TMAX + k]) >= TAIL_NQ * (unsigned)(q == 1 ? k - 1 : k);
         } else if (type == TK_S) {  // the block itself; D(k)'s progress inside tail_trsm_pipe
             ok = tail_ld(&c->units[i * TAIL_TMAX + k]) >= 4u * k;
             if (q == TAIL_S_WHOLE && ok) ok = tail_ld(&c->ddone[k]) != 0u;  // not pipelined: D(k) done
@@ -3224,7 +3318,8 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int
 #define GAPLAC_DIAG3 0
 #endif
 __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict__ kt) {
-    __shared__ double smem[GAPLAC_DIAG3 ? DIAG3_SMEM : DIAG2_SMEM];
+    // (diag2 + the fused update's 16 x 128 staging, diag2_fused_load)
+    __shared__ double smem[GAPLAC_DIAG3 && DIAG3_SMEM > DIAG2_SMEM + 16 * NB ? DIAG3_SMEM : DIAG2_SMEM + 16 * NB];
     __shared__ unsigned s_task;
     __shared__ unsigned s_rowf[NDB];
     kt_begin(kt);
@@ -3256,7 +3351,15 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         if (faulted) {
         } else if (type == TK_D) {
             if ((int64_t)gk * NB < a.N) {
-                if (GAPLAC_DIAG3)
+                if (q == 1)
+                    potrf_diag2_body<GM_SC1, true>(smem, colk + (int64_t)gk * NB, a.lda, a.N, (int64_t)gk * NB,
+                                                   Dinv + (size_t)gk * DINV_PER_BLOCK, res, nullptr, &ctl->dprog[k],
+                                                   a.trace && a.nmodels == 1
+                                                       ? a.trace + 3 * (size_t)a.ntasks + (size_t)TAIL_DSTAMPS * k
+                                                       : nullptr,
+                                                   A + (int64_t)(gk - 1) * NB * a.lda + (int64_t)gk * NB,
+                                                   ctl->sprog[k - 1], &ctl->err);
+                else if (GAPLAC_DIAG3)
                     potrf_diag3_body<GM_SC1>(smem, colk + (int64_t)gk * NB, a.lda, a.N, (int64_t)gk * NB,
                                              Dinv + (size_t)gk * DINV_PER_BLOCK, res, nullptr, &ctl->dprog[k]);
                 else
@@ -3299,6 +3402,9 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         __syncthreads();
         if (threadIdx.x == 0 && !faulted) {
             if (type == TK_D) {
+                if (q == 1)  // (the column k-1 update it applied: the tile's count stays complete)
+                    __hip_atomic_fetch_add(&ctl->units[k * TAIL_TMAX + k], TAIL_NQ, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_fetch_add(&ctl->ddone[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else if (type == TK_S) {  // two halves per tile (or one whole-tile task): done at 2
                 __hip_atomic_fetch_add(&ctl->sdone[i * TAIL_TMAX + k], q == TAIL_S_WHOLE ? 2u : 1u, __ATOMIC_RELAXED,
@@ -3366,7 +3472,7 @@ void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<s
 // updates (throughput).
 void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart, int gw, int near,
                       int quad_last, bool whole_trsm, int group, int xrows, int sub_ahead, int sub_dist,
-                      int crit_quads, bool diag_quads) {
+                      int crit_quads, bool diag_quads, bool fuse_q) {
     group = group >= 4 ? 4 : group >= 2 ? 2 : 1;  // divides the deep width (4 or 8): groups stay in a block
     // deep width; near distance (>= 2: the next two diagonal tiles take per-column Q tasks)
     const int GW = gw == 8 ? 8 : 4, NEAR = std::max(2, near);
@@ -3432,9 +3538,9 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
         const int b = g / GW;
         const int jfar = deep_block(b) ? far_from(b) : T;  // per-column updates below this tile column
         S(g + 2, g);
-        Qs(g + 1, g);
+        if (!fuse_q) Qs(g + 1, g);  // (fuse_q: D(g+1) applies column g's update itself)
         Uq(g + 2, g + 1, g);
-        out.push_back(tail_enc(TK_D, 0, g + 1, 0, 0));
+        out.push_back(tail_enc(TK_D, fuse_q ? 1 : 0, g + 1, 0, 0));
         S(g + 2, g + 1);
         Qs(g + 2, g);
         S(g + 3, g);
@@ -3509,6 +3615,12 @@ bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why
         if (k >= T || i >= R || j >= T || (i >= T && (type == TK_D || type == TK_Q)))
             return fail(n, "task outside the tile range");
         if (type == TK_D) {
+            if (q > 1 || (q == 1 && k == 0)) return fail(n, "a diagonal block task of an unknown kind");
+            if (q == 1) {  // fused: column k-1's update applied by the block itself, behind S(k, k-1)
+                if (units[(size_t)k * T + k] != TAIL_NQ * (unsigned)(k - 1)) return fail(n, "D before its tile is updated");
+                if (sdone[(size_t)k * T + k - 1] != 2u) return fail(n, "fused D before its TRSM is dequeued");
+                units[(size_t)k * T + k] += TAIL_NQ;
+            }
             if (units[(size_t)k * T + k] != TAIL_NQ * (unsigned)k) return fail(n, "D before its tile is updated");
             ddone[(size_t)k] += 1;
         } else if (type == TK_S) {
