@@ -81,6 +81,10 @@ struct gaplac_ctx {
     int tail_critq = 0;     // GAPLAC_TAIL_CRITQ: the next tile column's first this many sub-diagonal tiles as quadrants
     bool tail_diagq = false;  // GAPLAC_TAIL_DIAGQ: near diagonal tiles' per-column updates as three quadrant tasks
     bool tail_fuseq = false;  // GAPLAC_TAIL_FUSEQ: each diagonal block applies its tile's last update itself
+    // GAPLAC_TAIL_SIM: the single-evaluation tail list ordered by a simulated schedule
+    // (sim_order_tail_tasks); -1 = for tails of fewer than 80 tile columns (measured: T = 33
+    // -4.4%, T = 65 -1.3%, T = 80 +0.3%), 0 never, 1 always
+    int tail_sim = -1;
     int pair_m = 40;      // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
     int pair_depth = 0;   // GAPLAC_PAIR_DEPTH: super-panels per deferred bulk update (0: 4 from 256 tile
                           //   columns on, else 2; N = 65536 1439 -> 1427 ms, 16k 26.97 -> 27.14 ms at 3-4)
@@ -707,6 +711,8 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
                 std::vector<uint32_t> host;
                 build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X, ctx->tail_subq,
                                  ctx->tail_subd, ctx->tail_critq, ctx->tail_diagq, ctx->tail_fuseq);
+                if ((ctx->tail_sim > 0 || (ctx->tail_sim < 0 && T < 80)) && X == 0)
+                    sim_order_tail_tasks(T, host, std::max(1, ctx->ncu / std::max(1, ctx->tail_share)));
                 int rc;
                 if ((rc = ensure(ctx, &ctx->ttasks, &ctx->ttasks_elems, host.size()))) return rc;
                 HIPCK(ctx, hipMemcpy(ctx->ttasks, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -1343,6 +1349,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_TAIL_CRITQ")) ctx->tail_critq = std::max(0, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAIL_DIAGQ")) ctx->tail_diagq = s[0] != '0';
     if (const char* s = std::getenv("GAPLAC_TAIL_FUSEQ")) ctx->tail_fuseq = s[0] != '0';
+    if (const char* s = std::getenv("GAPLAC_TAIL_SIM")) ctx->tail_sim = s[0] == '0' ? 0 : 1;
     if (const char* s = std::getenv("GAPLAC_GRAD_FUSED")) ctx->grad_fused = s[0] != '0';
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAILK")) ctx->tailk = s[0] != '0';
@@ -1941,6 +1948,17 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
                                    ", crit_quads " + std::to_string(cq) + ", diag_quads " + std::to_string(dq) +
                                    ", fuse_q " + std::to_string(fq) + ")";
                     }
+            // the simulated order (GAPLAC_TAIL_SIM) must come out reordered and checked
+            for (int T : {2, 9, 33, 80, 128})
+                for (int fq : {0, 1}) {
+                    std::vector<uint32_t> l;
+                    build_tail_tasks(T, l, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, 0, 0, 1, 0, false,
+                                     fq != 0);
+                    const int st = sim_order_tail_tasks(T, l, 256);
+                    if (st != 0)
+                        return "simulated tail order (T = " + std::to_string(T) + ", fuse_q " + std::to_string(fq) +
+                               ") " + (st == 1 ? "stalled" : "failed the dependency check");
+                }
             // batched launches: each model's tasks, read out of the interleaved list, are
             // its single list in order (so each is a topological order of its own dataflow)
             for (int T : {1, 2, 9, 33, 65, 80})

@@ -148,6 +148,11 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
                       int near = 4, int quad_last = TAIL_TMAX, bool whole_trsm = false, int group = 1,
                       int xrows = 0, int sub_ahead = 0, int sub_dist = 1, int crit_quads = 0,
                       bool diag_quads = false, bool fuse_q = false);
+// The list (no extra rows) reordered by a simulated schedule on `workers` workgroups
+// (longest path to the end first, measured task durations); kept as built if the result
+// fails check_tail_tasks. Returns 0 when reordered, 1 if the simulation stalled, 2 if the
+// order failed the check (both: list unchanged).
+int sim_order_tail_tasks(int T, std::vector<uint32_t>& list, int workers);
 // B models' task lists interleaved (each model's own order kept, so the result is a
 // topological order per model). lag = 0: task by task, all models in step. lag > 0: a
 // software pipeline: model m runs lag * m tile columns behind model 0, and the tasks of the

@@ -19,6 +19,8 @@
 #include <math.h>
 
 #include <algorithm>
+#include <functional>
+#include <queue>
 #include <type_traits>
 #include <cstdio>
 #include <cstdlib>
@@ -3592,6 +3594,141 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
         xcol(g);
     }
     xcol(T - 1);
+}
+
+// Reorder a single evaluation's list (no extra rows) by a simulated schedule: the tasks'
+// dependencies as tail_wait has them (the TRSMs pipelined behind their diagonal block and
+// the next diagonal tile's Q blocks behind their TRSM), durations as measured in the N =
+// 4096 task traces, `workers` persistent workgroups, and among ready
+// tasks the one with the longest path to the end first. Sorted by simulated start (ties:
+// list order) the list stays a topological order: every task starts no earlier than what
+// it waits for.
+int sim_order_tail_tasks(int T, std::vector<uint32_t>& list, int workers) {
+    const int n = (int)list.size();
+    if (n == 0 || workers < 1) return 1;
+    struct Tk {
+        int type, q, k, i, j, nk;
+        double dur;
+    };
+    std::vector<Tk> tk((size_t)n);
+    for (int x = 0; x < n; ++x) {
+        const uint32_t e = list[(size_t)x];
+        Tk& t = tk[(size_t)x];
+        t.type = (int)(e & 3u), t.q = (int)((e >> 2) & 15u), t.k = (int)((e >> 6) & 127u);
+        t.i = (int)((e >> 13) & 127u), t.j = (int)((e >> 20) & 127u);
+        t.nk = tail_deep_cols(t.type, t.q);
+        t.dur = t.type == TK_D ? 24.5 : t.type == TK_S ? 12.0 : t.type == TK_Q ? 5.0
+              : t.nk > 1 ? 19.0 * t.nk : t.q == 0 ? 25.0 : 8.4;
+    }
+    // predecessors; pipelined ones (S behind D, the next tile's Q behind its TRSM) marked
+    std::vector<std::vector<int>> pred((size_t)n), succ((size_t)n);
+    std::vector<std::vector<int>> pipe((size_t)n);  // the pipelined producers, if any
+    std::vector<int> dof((size_t)T, -1);
+    std::vector<std::vector<int>> sof((size_t)T * T);
+    struct Tile {
+        int col = -1;
+        std::vector<int> group, prev;
+    };
+    std::vector<Tile> tile((size_t)T * T);
+    for (int x = 0; x < n; ++x) {
+        const Tk& t = tk[(size_t)x];
+        std::vector<int>& p = pred[(size_t)x];
+        if (t.type == TK_D) {
+            const Tile& tl = tile[(size_t)t.k * T + t.k];
+            p = tl.group;
+            if (t.q == 1 && t.k >= 1)
+                pipe[(size_t)x] = sof[(size_t)t.k * T + t.k - 1];
+            dof[(size_t)t.k] = x;
+        } else if (t.type == TK_S) {
+            p = tile[(size_t)t.i * T + t.k].group;
+            if (dof[(size_t)t.k] >= 0) pipe[(size_t)x].push_back(dof[(size_t)t.k]);
+            sof[(size_t)t.i * T + t.k].push_back(x);
+        } else {
+            Tile& tl = tile[(size_t)t.i * T + t.j];
+            const int col = t.k + t.nk - 1;
+            if (col > tl.col) {
+                tl.prev = tl.group;
+                tl.group.clear();
+                tl.col = col;
+            }
+            p = tl.prev;
+            const bool piped = t.type == TK_Q && t.i == t.k + 1;
+            for (int c = 0; c < t.nk; ++c) {
+                for (int s : sof[(size_t)t.i * T + t.k + c]) {
+                    if (piped)
+                        pipe[(size_t)x].push_back(s);
+                    else
+                        p.push_back(s);
+                }
+                if (t.i != t.j)
+                    for (int s : sof[(size_t)t.j * T + t.k + c]) p.push_back(s);
+            }
+            tl.group.push_back(x);
+        }
+        for (int y : pipe[(size_t)x]) p.push_back(y);
+        for (int y : p) succ[(size_t)y].push_back(x);
+    }
+    // longest path to the end (a pipelined consumer adds only its part after the producer)
+    auto piped_on = [&](int s, int x) {
+        for (int y : pipe[(size_t)s])
+            if (y == x) return true;
+        return false;
+    };
+    std::vector<double> rank((size_t)n, 0.0);
+    for (int x = n - 1; x >= 0; --x) {
+        double m = 0.0;
+        for (int s : succ[(size_t)x]) m = std::max(m, rank[(size_t)s] - (piped_on(s, x) ? tk[(size_t)s].dur - 3.5 : 0.0));
+        rank[(size_t)x] = tk[(size_t)x].dur + m;
+    }
+    // event simulation: a task is ready when its plain predecessors have finished and its
+    // pipelined producer has started; it then ends at max(start + dur, producer end + 3.5)
+    std::vector<int> wait((size_t)n, 0);
+    std::vector<double> start((size_t)n, -1.0), fin((size_t)n, 0.0);
+    for (int x = 0; x < n; ++x) wait[(size_t)x] = (int)pred[(size_t)x].size();
+    using Ev = std::pair<double, int>;  // (time, task): finish events
+    std::priority_queue<Ev, std::vector<Ev>, std::greater<Ev>> ends;
+    auto cmp = [&](int a, int b) { return rank[(size_t)a] != rank[(size_t)b] ? rank[(size_t)a] < rank[(size_t)b] : a > b; };
+    std::priority_queue<int, std::vector<int>, decltype(cmp)> ready(cmp);
+    // a pipelined consumer's dependency on its producer is released at the producer's start
+    auto release = [&](int y) {
+        if (--wait[(size_t)y] == 0) ready.push(y);
+    };
+    for (int x = 0; x < n; ++x)
+        if (wait[(size_t)x] == 0) ready.push(x);
+    int free_w = workers, done = 0;
+    double now = 0.0;
+    while (done < n) {
+        while (free_w > 0 && !ready.empty()) {
+            const int x = ready.top();
+            ready.pop();
+            start[(size_t)x] = now;
+            double f = now + tk[(size_t)x].dur;
+            for (int y : pipe[(size_t)x]) f = std::max(f, fin[(size_t)y] + 3.5);
+            fin[(size_t)x] = f;
+            --free_w;
+            ends.push({f, x});
+            for (int s : succ[(size_t)x])
+                if (piped_on(s, x)) release(s);
+        }
+        if (ends.empty()) break;  // (cannot happen for a topological list)
+        const Ev ev = ends.top();
+        ends.pop();
+        now = ev.first;
+        ++free_w;
+        ++done;
+        for (int s : succ[(size_t)ev.second])
+            if (!piped_on(s, ev.second)) release(s);
+    }
+    if (done < n) return 1;  // keep the list as built
+    std::vector<int> ord((size_t)n);
+    for (int x = 0; x < n; ++x) ord[(size_t)x] = x;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return start[(size_t)a] < start[(size_t)b]; });
+    std::vector<uint32_t> out((size_t)n);
+    for (int x = 0; x < n; ++x) out[(size_t)x] = list[(size_t)ord[(size_t)x]];
+    std::string why;
+    if (!check_tail_tasks(T, out, &why, 0)) return 2;  // keep the list as built
+    list.swap(out);
+    return 0;
 }
 
 // Host check of a task list (gaplac_plan_check's dry walk): run the tasks one at a time in
