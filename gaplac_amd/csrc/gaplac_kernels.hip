@@ -3596,6 +3596,14 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
     xcol(T - 1);
 }
 
+// simulation constants (build switches for A/Bs): the pipelined consumer's part after its
+// producer ends (us), and the share of the grid the simulation schedules (percent)
+#ifndef GAPLAC_SIM_PIPE
+#define GAPLAC_SIM_PIPE 3.5
+#endif
+#ifndef GAPLAC_SIM_WPCT
+#define GAPLAC_SIM_WPCT 100
+#endif
 // Reorder a single evaluation's list (no extra rows) by a simulated schedule: the tasks'
 // dependencies as tail_wait has them (the TRSMs pipelined behind their diagonal block and
 // the next diagonal tile's Q blocks behind their TRSM), durations as measured in the N =
@@ -3616,6 +3624,7 @@ int sim_order_tail_tasks(int T, std::vector<uint32_t>& list, int workers) {
         Tk& t = tk[(size_t)x];
         t.type = (int)(e & 3u), t.q = (int)((e >> 2) & 15u), t.k = (int)((e >> 6) & 127u);
         t.i = (int)((e >> 13) & 127u), t.j = (int)((e >> 20) & 127u);
+        if (t.k >= T || t.i >= T || t.j >= T || (e >> TAIL_MODEL_SHIFT) != 0u) return 1;  // (extra rows, models)
         t.nk = tail_deep_cols(t.type, t.q);
         t.dur = t.type == TK_D ? 24.5 : t.type == TK_S ? 12.0 : t.type == TK_Q ? 5.0
               : t.nk > 1 ? 19.0 * t.nk : t.q == 0 ? 25.0 : 8.4;
@@ -3677,11 +3686,11 @@ int sim_order_tail_tasks(int T, std::vector<uint32_t>& list, int workers) {
     std::vector<double> rank((size_t)n, 0.0);
     for (int x = n - 1; x >= 0; --x) {
         double m = 0.0;
-        for (int s : succ[(size_t)x]) m = std::max(m, rank[(size_t)s] - (piped_on(s, x) ? tk[(size_t)s].dur - 3.5 : 0.0));
+        for (int s : succ[(size_t)x]) m = std::max(m, rank[(size_t)s] - (piped_on(s, x) ? tk[(size_t)s].dur - GAPLAC_SIM_PIPE : 0.0));
         rank[(size_t)x] = tk[(size_t)x].dur + m;
     }
     // event simulation: a task is ready when its plain predecessors have finished and its
-    // pipelined producer has started; it then ends at max(start + dur, producer end + 3.5)
+    // pipelined producer has started; it then ends at max(start + dur, producer end + GAPLAC_SIM_PIPE)
     std::vector<int> wait((size_t)n, 0);
     std::vector<double> start((size_t)n, -1.0), fin((size_t)n, 0.0);
     for (int x = 0; x < n; ++x) wait[(size_t)x] = (int)pred[(size_t)x].size();
@@ -3695,7 +3704,7 @@ int sim_order_tail_tasks(int T, std::vector<uint32_t>& list, int workers) {
     };
     for (int x = 0; x < n; ++x)
         if (wait[(size_t)x] == 0) ready.push(x);
-    int free_w = workers, done = 0;
+    int free_w = std::max(1, workers * GAPLAC_SIM_WPCT / 100), done = 0;
     double now = 0.0;
     while (done < n) {
         while (free_w > 0 && !ready.empty()) {
@@ -3703,7 +3712,7 @@ int sim_order_tail_tasks(int T, std::vector<uint32_t>& list, int workers) {
             ready.pop();
             start[(size_t)x] = now;
             double f = now + tk[(size_t)x].dur;
-            for (int y : pipe[(size_t)x]) f = std::max(f, fin[(size_t)y] + 3.5);
+            for (int y : pipe[(size_t)x]) f = std::max(f, fin[(size_t)y] + GAPLAC_SIM_PIPE);
             fin[(size_t)x] = f;
             --free_w;
             ends.push({f, x});
