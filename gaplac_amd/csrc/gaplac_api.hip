@@ -78,7 +78,8 @@ struct gaplac_ctx {
     int la_tiles_m = 120;   // GAPLAC_LA_TILES_M: the lookahead of >= this many tile rows as whole tiles (0: never)
     int tail_subq = 0;      // GAPLAC_TAIL_SUBQ: near-diagonal tiles this many columns ahead updated as quadrants
     int tail_subd = 1;      // GAPLAC_TAIL_SUBD: ... the tiles within this distance of the diagonal
-    int tail_critq = 0;     // GAPLAC_TAIL_CRITQ: the next tile column's first this many sub-diagonal tiles as quadrants
+    int tail_critq = -1;    // GAPLAC_TAIL_CRITQ: the next tile column's first this many sub-diagonal tiles as
+                            // quadrants; -1 = 1 with the simulated order, else 0 (N = 4096: -0.7%)
     bool tail_diagq = false;  // GAPLAC_TAIL_DIAGQ: near diagonal tiles' per-column updates as three quadrant tasks
     bool tail_fuseq = false;  // GAPLAC_TAIL_FUSEQ: each diagonal block applies its tile's last update itself
     // GAPLAC_TAIL_SIM: the single-evaluation tail list ordered by a simulated schedule
@@ -703,15 +704,21 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             if (ctx->dry) {  // gaplac_plan_check: the task list's dependency order
                 std::vector<uint32_t> host;
                 build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X, ctx->tail_subq,
-                                 ctx->tail_subd, ctx->tail_critq, ctx->tail_diagq, ctx->tail_fuseq);
+                                 ctx->tail_subd,
+                                 ctx->tail_critq >= 0                                                   ? ctx->tail_critq
+                                 : ((ctx->tail_sim > 0 || (ctx->tail_sim < 0 && T < 80)) && X == 0) ? 1
+                                                                                                     : 0,
+                                 ctx->tail_diagq, ctx->tail_fuseq);
                 std::string why;
                 if (!check_tail_tasks(T, host, &why, X)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
             }
             if ((ctx->ttasks_T != T || ctx->ttasks_X != X) && !ctx->dry) {
                 std::vector<uint32_t> host;
+                const bool sim = (ctx->tail_sim > 0 || (ctx->tail_sim < 0 && T < 80)) && X == 0;
                 build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X, ctx->tail_subq,
-                                 ctx->tail_subd, ctx->tail_critq, ctx->tail_diagq, ctx->tail_fuseq);
-                if ((ctx->tail_sim > 0 || (ctx->tail_sim < 0 && T < 80)) && X == 0)
+                                 ctx->tail_subd, ctx->tail_critq >= 0 ? ctx->tail_critq : sim ? 1 : 0, ctx->tail_diagq,
+                                 ctx->tail_fuseq);
+                if (sim)
                     sim_order_tail_tasks(T, host, std::max(1, ctx->ncu / std::max(1, ctx->tail_share)));
                 int rc;
                 if ((rc = ensure(ctx, &ctx->ttasks, &ctx->ttasks_elems, host.size()))) return rc;
@@ -1346,7 +1353,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_LA_TILES_M")) ctx->la_tiles_m = std::max(0, std::atoi(s));
     if (const char* s = std::getenv("GAPLAC_TAIL_SUBQ")) ctx->tail_subq = std::max(0, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_TAIL_SUBD")) ctx->tail_subd = std::max(1, std::min(8, std::atoi(s)));
-    if (const char* s = std::getenv("GAPLAC_TAIL_CRITQ")) ctx->tail_critq = std::max(0, std::min(8, std::atoi(s)));
+    if (const char* s = std::getenv("GAPLAC_TAIL_CRITQ")) ctx->tail_critq = std::max(0, std::min(8, std::atoi(s)));  // (explicit)
     if (const char* s = std::getenv("GAPLAC_TAIL_DIAGQ")) ctx->tail_diagq = s[0] != '0';
     if (const char* s = std::getenv("GAPLAC_TAIL_FUSEQ")) ctx->tail_fuseq = s[0] != '0';
     if (const char* s = std::getenv("GAPLAC_TAIL_SIM")) ctx->tail_sim = s[0] == '0' ? 0 : 1;
