@@ -534,6 +534,11 @@ static bool pair_defer(const gaplac_ctx* ctx, const std::vector<int>& spc, int n
            p + 3 + ctx->pair_ext <= nsp && nt - spc[(size_t)p + 3 + ctx->pair_ext] >= ctx->pair_m;
 }
 
+// Latency-shaped (quadrant) columns of a single evaluation's tail: with the simulated
+// order a tail of at most 40 tile columns takes them in every column (N = 4096: -2%; at T =
+// 65 all columns cost +4%, 40 of them +1.5%), else the last GAPLAC_QUAD_LAST.
+static int tail_quad_last(bool sim, int T) { return sim && T <= 40 ? TAIL_TMAX : GAPLAC_QUAD_LAST; }
+
 int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     hipStream_t sm = ctx->s_main;
     hipStream_t sp = ctx->serial ? sm : ctx->s_panel;
@@ -703,19 +708,17 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             }
             if (ctx->dry) {  // gaplac_plan_check: the task list's dependency order
                 std::vector<uint32_t> host;
-                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X, ctx->tail_subq,
-                                 ctx->tail_subd,
-                                 ctx->tail_critq >= 0                                                   ? ctx->tail_critq
-                                 : ((ctx->tail_sim > 0 || (ctx->tail_sim < 0 && T < 80)) && X == 0) ? 1
-                                                                                                     : 0,
-                                 ctx->tail_diagq, ctx->tail_fuseq);
+                const bool sim = (ctx->tail_sim > 0 || (ctx->tail_sim < 0 && T < 80)) && X == 0;
+                build_tail_tasks(T, host, nullptr, 4, 4, tail_quad_last(sim, T), false, GAPLAC_SINGLE_GROUP, X, ctx->tail_subq,
+                                 ctx->tail_subd, ctx->tail_critq >= 0 ? ctx->tail_critq : sim ? 1 : 0, ctx->tail_diagq,
+                                 ctx->tail_fuseq);
                 std::string why;
                 if (!check_tail_tasks(T, host, &why, X)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
             }
             if ((ctx->ttasks_T != T || ctx->ttasks_X != X) && !ctx->dry) {
                 std::vector<uint32_t> host;
                 const bool sim = (ctx->tail_sim > 0 || (ctx->tail_sim < 0 && T < 80)) && X == 0;
-                build_tail_tasks(T, host, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X, ctx->tail_subq,
+                build_tail_tasks(T, host, nullptr, 4, 4, tail_quad_last(sim, T), false, GAPLAC_SINGLE_GROUP, X, ctx->tail_subq,
                                  ctx->tail_subd, ctx->tail_critq >= 0 ? ctx->tail_critq : sim ? 1 : 0, ctx->tail_diagq,
                                  ctx->tail_fuseq);
                 if (sim)
@@ -1957,10 +1960,10 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
                     }
             // the simulated order (GAPLAC_TAIL_SIM) must come out reordered and checked
             for (int T : {2, 9, 33, 80, 128})
-                for (int fq : {0, 1}) {
+                for (int fq : {0, 1})
+                for (int ql : {GAPLAC_QUAD_LAST, TAIL_TMAX}) {
                     std::vector<uint32_t> l;
-                    build_tail_tasks(T, l, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, 0, 0, 1, 0, false,
-                                     fq != 0);
+                    build_tail_tasks(T, l, nullptr, 4, 4, ql, false, GAPLAC_SINGLE_GROUP, 0, 0, 1, 1, false, fq != 0);
                     const int st = sim_order_tail_tasks(T, l, 256);
                     if (st != 0)
                         return "simulated tail order (T = " + std::to_string(T) + ", fuse_q " + std::to_string(fq) +
