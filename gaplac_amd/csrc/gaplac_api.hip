@@ -75,19 +75,13 @@ struct gaplac_ctx {
     int band_tiles_m = 64;  // GAPLAC_BAND_TILES_M: bands of >= this many tile rows as whole tiles
     int grad_fused = 1;     // GAPLAC_GRAD_FUSED: -C^{-1} contracted inside cinv_contract_kernel (0: stored, then contracted)
     bool grad_singletons = true;  // the gradient's formula has single-term groups only (the fused path's case)
-    int la_tiles_m = 120;   // GAPLAC_LA_TILES_M: the lookahead of >= this many tile rows as whole tiles (0: never)
-    int tail_subq = 0;      // GAPLAC_TAIL_SUBQ: near-diagonal tiles this many columns ahead updated as quadrants
-    int tail_subd = 1;      // GAPLAC_TAIL_SUBD: ... the tiles within this distance of the diagonal
-    int tail_critq = -1;    // GAPLAC_TAIL_CRITQ: the next tile column's first this many sub-diagonal tiles as
-                            // quadrants; -1 = 1 with the simulated order, else 0 (N = 4096: -0.7%)
-    bool tail_diagq = false;  // GAPLAC_TAIL_DIAGQ: near diagonal tiles' per-column updates as three quadrant tasks
-    bool tail_fuseq = false;  // GAPLAC_TAIL_FUSEQ: each diagonal block applies its tile's last update itself
+    int la_tiles_m = 120;   // the lookahead of >= this many tile rows as whole tiles (0: never)
     // GAPLAC_TAIL_SIM: the single-evaluation tail list ordered by a simulated schedule
     // (sim_order_tail_tasks); -1 = for tails of fewer than 80 tile columns (measured: T = 33
     // -4.4%, T = 65 -1.3%, T = 80 +0.3%), 0 never, 1 always
     int tail_sim = -1;
     int pair_m = 40;      // GAPLAC_PAIR_M: paired bulk updates while >= this many tile rows follow the band
-    int pair_depth = 0;   // GAPLAC_PAIR_DEPTH: super-panels per deferred bulk update (0: 4 from 256 tile
+    int pair_depth = 0;   // (plan checks only) super-panels per deferred bulk update (0: 4 from 256 tile
                           //   columns on, else 2; N = 65536 1439 -> 1427 ms, 16k 26.97 -> 27.14 ms at 3-4)
     int ncu = 256;        // compute units of the device
     bool tailk = true;    // GAPLAC_TAILK: the serial tail as one persistent dataflow launch (tail_kernel)
@@ -709,18 +703,14 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             if (ctx->dry) {  // gaplac_plan_check: the task list's dependency order
                 std::vector<uint32_t> host;
                 const bool sim = (ctx->tail_sim > 0 || (ctx->tail_sim < 0 && T < 80)) && X == 0;
-                build_tail_tasks(T, host, nullptr, 4, 4, tail_quad_last(sim, T), false, GAPLAC_SINGLE_GROUP, X, ctx->tail_subq,
-                                 ctx->tail_subd, ctx->tail_critq >= 0 ? ctx->tail_critq : sim ? 1 : 0, ctx->tail_diagq,
-                                 ctx->tail_fuseq);
+                build_tail_tasks(T, host, nullptr, 4, 4, tail_quad_last(sim, T), false, GAPLAC_SINGLE_GROUP, X, sim ? 1 : 0);
                 std::string why;
                 if (!check_tail_tasks(T, host, &why, X)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
             }
             if ((ctx->ttasks_T != T || ctx->ttasks_X != X) && !ctx->dry) {
                 std::vector<uint32_t> host;
                 const bool sim = (ctx->tail_sim > 0 || (ctx->tail_sim < 0 && T < 80)) && X == 0;
-                build_tail_tasks(T, host, nullptr, 4, 4, tail_quad_last(sim, T), false, GAPLAC_SINGLE_GROUP, X, ctx->tail_subq,
-                                 ctx->tail_subd, ctx->tail_critq >= 0 ? ctx->tail_critq : sim ? 1 : 0, ctx->tail_diagq,
-                                 ctx->tail_fuseq);
+                build_tail_tasks(T, host, nullptr, 4, 4, tail_quad_last(sim, T), false, GAPLAC_SINGLE_GROUP, X, sim ? 1 : 0);
                 if (sim)
                     sim_order_tail_tasks(T, host, std::max(1, ctx->ncu / std::max(1, ctx->tail_share)));
                 int rc;
@@ -1351,14 +1341,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     if (const char* s = std::getenv("GAPLAC_SERIAL")) ctx->serial = s[0] == '1';
     if (const char* s = std::getenv("GAPLAC_SPW")) ctx->spw = std::max(1, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_PAIR_M")) ctx->pair_m = std::max(0, std::atoi(s));
-    if (const char* s = std::getenv("GAPLAC_PAIR_DEPTH")) ctx->pair_depth = std::max(2, std::min(8, std::atoi(s)));
     if (const char* s = std::getenv("GAPLAC_BAND_TILES_M")) ctx->band_tiles_m = std::max(1, std::atoi(s));
-    if (const char* s = std::getenv("GAPLAC_LA_TILES_M")) ctx->la_tiles_m = std::max(0, std::atoi(s));
-    if (const char* s = std::getenv("GAPLAC_TAIL_SUBQ")) ctx->tail_subq = std::max(0, std::min(8, std::atoi(s)));
-    if (const char* s = std::getenv("GAPLAC_TAIL_SUBD")) ctx->tail_subd = std::max(1, std::min(8, std::atoi(s)));
-    if (const char* s = std::getenv("GAPLAC_TAIL_CRITQ")) ctx->tail_critq = std::max(0, std::min(8, std::atoi(s)));  // (explicit)
-    if (const char* s = std::getenv("GAPLAC_TAIL_DIAGQ")) ctx->tail_diagq = s[0] != '0';
-    if (const char* s = std::getenv("GAPLAC_TAIL_FUSEQ")) ctx->tail_fuseq = s[0] != '0';
     if (const char* s = std::getenv("GAPLAC_TAIL_SIM")) ctx->tail_sim = s[0] == '0' ? 0 : 1;
     if (const char* s = std::getenv("GAPLAC_GRAD_FUSED")) ctx->grad_fused = s[0] != '0';
     if (const char* s = std::getenv("GAPLAC_BATCH_LANES")) ctx->batch_lanes = std::max(1, std::min(16, std::atoi(s)));
@@ -1646,23 +1629,23 @@ int gaplac_logpdf_batch(gaplac_ctx* ctx, int32_t nmodels, int64_t N, int32_t D, 
     // latency-bound critical path), so concurrent models fill the gaps.
     int nl = std::max(1, std::min(ctx->batch_lanes, nmodels));
     {
-        // every extra lane holds a whole evaluation workspace: keep the lanes that fit in the
-        // free device memory (the workspaces already held are reusable; 2 GiB kept free),
-        // down to this context alone, and say so clearly when not even that fits
+        // every extra lane holds a whole evaluation workspace: keep the extra lanes that fit
+        // in the free device memory beside this context's own workspace (the workspaces
+        // already held are reusable; 2 GiB kept free for everything else). Lane 0 is this
+        // context: it is never refused here (as a single gaplac_logpdf call would not be);
+        // if even its workspace does not fit, ensure_workspace reports the real OOM.
         const int64_t Np = round_up(N + 1, NB);
         const size_t per = (size_t)Np * (size_t)Np * sizeof(double) + (size_t)(Np / NB) * DINV_PER_BLOCK * sizeof(double);
         size_t freeb = 0, totalb = 0;
-        if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
-            size_t held = ctx->A_elems * sizeof(double);
+        if (nl > 1 && hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
+            const size_t own = ctx->A_elems * sizeof(double);
+            size_t held = 0;
             for (size_t l = 0; l + 1 < (size_t)nl && l < ctx->lanes.size(); ++l) held += ctx->lanes[l]->A_elems * sizeof(double);
             const size_t margin = (size_t)2 << 30;
-            const size_t budget = freeb + held > margin ? freeb + held - margin : 0;
-            const int fit = (int)std::min<size_t>((size_t)nl, budget / per);
-            if (fit < 1)
-                return set_err(ctx, GAPLAC_E_OOM,
-                               "batch: one evaluation workspace at N = %lld needs %zu bytes, %zu are free (%zu held)",
-                               (long long)N, per, freeb, held);
-            nl = fit;
+            const size_t own_need = own >= per ? 0 : per - own;  // lane 0's workspace still to allocate
+            const size_t avail = freeb + held;
+            const size_t budget = avail > margin + own_need ? avail - margin - own_need : 0;
+            nl = 1 + (int)std::min<size_t>((size_t)(nl - 1), budget / per);
         }
     }
     while ((int)ctx->lanes.size() < nl - 1) {
@@ -1937,36 +1920,28 @@ int gaplac_plan_check(int64_t N, int32_t mode, int64_t M, int32_t spw, int64_t* 
                         if (!check_tail_tasks(T, l, &why)) return why + " (gw " + std::to_string(gw) + ", near " +
                                                                   std::to_string(near) + ")";
                     }
-            // single evaluations with sub-diagonal quadrant updates (GAPLAC_TAIL_SUBQ), with
-            // and without the posterior's extra rows
+            // single evaluations with the critical sub-diagonal quadrants, with and without the
+            // posterior's extra rows
             for (int T = 1; T <= TAIL_TMAX; ++T)
-                for (int sq : {0, 1, 4, 8})
-                    for (int sd : {1, 2, 4})
-                    for (int cq : {0, 2})
-                    for (int dq : {0, 1})
-                    for (int fq : {0, 1})
-                    for (int X : {0, 2}) {
-                        if ((sq == 0 && sd != 1) || (cq != 0 && sq != 0 && sd != 2)) continue;  // (bounded sweep)
-                        if (fq && (sd == 4 || (cq != 0 && dq == 0))) continue;
-                        if (T + X > TAIL_TMAX) continue;  // (the launch condition)
-                        std::vector<uint32_t> l;
-                        build_tail_tasks(T, l, nullptr, 4, 4, GAPLAC_QUAD_LAST, false, GAPLAC_SINGLE_GROUP, X, sq, sd, cq,
-                                         dq != 0, fq != 0);
-                        std::string why;
-                        if (!check_tail_tasks(T, l, &why, X))
-                            return why + " (sub_ahead " + std::to_string(sq) + ", sub_dist " + std::to_string(sd) +
-                                   ", crit_quads " + std::to_string(cq) + ", diag_quads " + std::to_string(dq) +
-                                   ", fuse_q " + std::to_string(fq) + ")";
-                    }
+                for (int ql : {GAPLAC_QUAD_LAST, TAIL_TMAX})
+                    for (int cq : {0, 1, 2})
+                        for (int X : {0, 2}) {
+                            if (T + X > TAIL_TMAX) continue;  // (the launch condition)
+                            std::vector<uint32_t> l;
+                            build_tail_tasks(T, l, nullptr, 4, 4, ql, false, GAPLAC_SINGLE_GROUP, X, cq);
+                            std::string why;
+                            if (!check_tail_tasks(T, l, &why, X))
+                                return why + " (quad_last " + std::to_string(ql) + ", crit_quads " + std::to_string(cq) +
+                                       ", extra rows " + std::to_string(X) + ")";
+                        }
             // the simulated order (GAPLAC_TAIL_SIM) must come out reordered and checked
-            for (int T : {2, 9, 33, 80, 128})
-                for (int fq : {0, 1})
+            for (int T : {2, 9, 33, 65, 80, 128})
                 for (int ql : {GAPLAC_QUAD_LAST, TAIL_TMAX}) {
                     std::vector<uint32_t> l;
-                    build_tail_tasks(T, l, nullptr, 4, 4, ql, false, GAPLAC_SINGLE_GROUP, 0, 0, 1, 1, false, fq != 0);
+                    build_tail_tasks(T, l, nullptr, 4, 4, ql, false, GAPLAC_SINGLE_GROUP, 0, 1);
                     const int st = sim_order_tail_tasks(T, l, 256);
                     if (st != 0)
-                        return "simulated tail order (T = " + std::to_string(T) + ", fuse_q " + std::to_string(fq) +
+                        return "simulated tail order (T = " + std::to_string(T) + ", quad_last " + std::to_string(ql) +
                                ") " + (st == 1 ? "stalled" : "failed the dependency check");
                 }
             // batched launches: each model's tasks, read out of the interleaved list, are

@@ -89,15 +89,16 @@ struct gaplac_dist {
     int D = 2;         // GAPLAC_DIST_DEPTH: panels per deferral group
     int cw = 4;        // GAPLAC_DIST_CHUNK: tile columns per broadcast chunk
     int big_mode = 1;  // GAPLAC_DIST_BIG: 0 never, 1 per rank (no chain beside the launch), 2 by launch size
-    int big_min = 2048;  // GAPLAC_DIST_BIG_MIN: tiles of a launch for the per-rank choice
+    int big_min = 2048;  // (gaplac_dist_configure) tiles of a launch for the per-rank choice
     int alone = 0;     // GAPLAC_DIST_ALONE: the owner of SP s+1 starts update(s) after its chain
     hipStream_t s_main = nullptr, s_panel = nullptr, s_comm = nullptr;
     hipEvent_t ev_gram = nullptr, ev_panel_done = nullptr;
     // ev_recv / ev_packed per panel parity and chunk; ev_step[s & 1]: update(s) brought SP
-    // s+2 up to date; ev_free_main / ev_free_panel / ev_free_comm per group buffer: its last
-    // bulk update / lookahead / broadcast of the buffer's current group done
+    // s+2 up to date; ev_free_main / ev_free_panel per group buffer: its last bulk update /
+    // lookahead of the buffer's current group done (the broadcasts that refill a buffer are
+    // ordered behind the earlier ones by the comm stream itself, so they need no event)
     hipEvent_t ev_recv[2][MAXC] = {}, ev_packed[2][MAXC] = {};
-    hipEvent_t ev_step[2] = {}, ev_free_main[2] = {}, ev_free_panel[2] = {}, ev_free_comm[2] = {};
+    hipEvent_t ev_step[2] = {}, ev_free_main[2] = {}, ev_free_panel[2] = {};
     hipEvent_t ev_upd[2] = {};  // replay: update(s) started (its UPD stamp written)
     hipEvent_t ev_col[MAXC] = {};  // factor(s): column k of the SP final (its pack may start)
     int pair_m = 40;  // GAPLAC_PAIR_M: deferred updates while >= pair_m tile rows follow SP s+3
@@ -445,7 +446,6 @@ int gaplac_dist_create(int device, int nranks, int rank, int spw, gaplac_dist** 
     if (const char* e = std::getenv("GAPLAC_DIST_DEPTH")) d->D = std::max(1, std::min(8, std::atoi(e)));
     if (const char* e = std::getenv("GAPLAC_DIST_CHUNK")) d->cw = std::max(1, std::min(spw, std::atoi(e)));
     if (const char* e = std::getenv("GAPLAC_DIST_BIG")) d->big_mode = std::max(0, std::min(2, std::atoi(e)));
-    if (const char* e = std::getenv("GAPLAC_DIST_BIG_MIN")) d->big_min = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("GAPLAC_DIST_ALONE")) d->alone = std::atoi(e) > 0;
     std::vector<hipEvent_t*> evs = {&d->ev_gram, &d->ev_panel_done};
     for (int c = 0; c < MAXC; ++c) evs.push_back(&d->ev_col[c]);
@@ -454,7 +454,7 @@ int gaplac_dist_create(int device, int nranks, int rank, int spw, gaplac_dist** 
             evs.push_back(&d->ev_recv[b][c]);
             evs.push_back(&d->ev_packed[b][c]);
         }
-        for (hipEvent_t* ev : {&d->ev_step[b], &d->ev_free_main[b], &d->ev_free_panel[b], &d->ev_free_comm[b],
+        for (hipEvent_t* ev : {&d->ev_step[b], &d->ev_free_main[b], &d->ev_free_panel[b],
                                &d->ev_upd[b]})
             evs.push_back(ev);
     }
@@ -484,7 +484,7 @@ int gaplac_dist_destroy(gaplac_dist* d) {
             evs.push_back(d->ev_recv[b][c]);
             evs.push_back(d->ev_packed[b][c]);
         }
-        for (hipEvent_t ev : {d->ev_step[b], d->ev_free_main[b], d->ev_free_panel[b], d->ev_free_comm[b], d->ev_upd[b]})
+        for (hipEvent_t ev : {d->ev_step[b], d->ev_free_main[b], d->ev_free_panel[b], d->ev_upd[b]})
             evs.push_back(ev);
     }
     for (hipEvent_t ev : evs)
@@ -773,7 +773,6 @@ int gaplac_dist_comm_end_chunk(gaplac_dist* d, int32_t s, int32_t c) {
         return derr(d, GAPLAC_E_ARG, "comm_end: step %d chunk %d out of range", s, c);
     DCK(d, hipSetDevice(d->device));
     DCK(d, hipEventRecord(d->ev_recv[s & 1][c], d->s_comm));
-    if (c == nchunks(d, s) - 1) DCK(d, hipEventRecord(d->ev_free_comm[group_buf(d, s)], d->s_comm));
     return 0;
 }
 

@@ -136,18 +136,11 @@ constexpr int TAIL_MAX_MODELS = 32;
 // task (K = 128 group) where the chain allows.
 // xrows > 0: xrows extra tile rows below the matrix (relative rows T .. T+xrows-1, the
 // posterior's cross-covariance rows) factored along: whole-tile TRSMs and updates only.
-// sub_ahead > 0: in the last quad_last columns the tiles (i, j) with 1 <= i - j <= sub_dist
-// of the next sub_ahead tile columns past g+1 are also updated as quadrant tasks (the
-// chains of per-column updates that the near-diagonal TRSMs wait for keep the pace).
 // crit_quads > 0: column g's updates of tiles (g+1+d, g+1), 1 <= d <= crit_quads, are
 // quadrant tasks in every column (not only the last quad_last).
-// diag_quads: the near diagonal tiles' per-column updates as three lower quadrant tasks.
-// fuse_q: no Q blocks for the next diagonal tile; D(g+1) (task q = 1) applies column g's
-// update to its tile in LDS, pipelined behind S(g+1, g) (diag2_fused_load).
 void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart = nullptr, int gw = 4,
                       int near = 4, int quad_last = TAIL_TMAX, bool whole_trsm = false, int group = 1,
-                      int xrows = 0, int sub_ahead = 0, int sub_dist = 1, int crit_quads = 0,
-                      bool diag_quads = false, bool fuse_q = false);
+                      int xrows = 0, int crit_quads = 0);
 // The list (no extra rows) reordered by a simulated schedule on `workers` workgroups
 // (longest path to the end first, measured task durations); kept as built if the result
 // fails check_tail_tasks. Returns 0 when reordered, 1 if the simulation stalled, 2 if the

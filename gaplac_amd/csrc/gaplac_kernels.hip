@@ -1116,103 +1116,11 @@ __device__ __forceinline__ void diag2_store_column(const double* Ab, double* Ag,
 // 512 threads: wave 0 = A (the pivot chain), wave 1 = B (rows 64+ of panels 0-3), waves 2-7
 // the trailing updates, the stores of finished block columns and (wave 7) the inverses.
 // Waves w and w + 4 share a SIMD, so every SIMD's matrix pipe takes trailing work.
-// Fused next-diagonal update (tail D task q = 1, GAPLAC_TAIL_FUSEQ): the diagonal block
-// itself applies the previous tile column's update C -= L L^T (L = tile (k, k-1), written
-// by the TRSM pipelined behind D(k-1)) into LDS instead of ten Q tasks storing the tile and
-// the block loading it back. Each of the 36 lower 16x16 blocks takes exactly tail_q32's
-// MFMA sequence (accumulator from C, k-steps 4 at a time in order), so the factor is
-// bitwise the Q path's. Block m = wave + 8 s; the k-steps of column block b once every
-// 16-row group of the TRSM has stored block b (sprog), bounded like tail_q32's poll.
 template <int AUX>
-__device__ __forceinline__ void diag2_fused_load(double* Ab, const double* Ag, const double* P, int64_t lda,
-                                                 const unsigned* sprog, unsigned* err, unsigned* rerr) {
-    const int t = otid(), wave = t >> 6, lane = t & 63, fr = lane >> 4, fc = lane & 15;
-    const Gm<AUX> gC(Ag), gP(P);
-    constexpr int NS = (NPK + 7) / 8;  // 5 blocks per wave at most
-    int bI[NS], bJ[NS];
-    d4 acc[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-        const int m = wave + 8 * s;
-        int I = 0;
-        while ((I + 1) * (I + 2) / 2 <= m) ++I;
-        bI[s] = I;
-        bJ[s] = m - I * (I + 1) / 2;
-        if (m < NPK) {
-#pragma unroll
-            for (int rg = 0; rg < 4; ++rg)
-                acc[s][rg] = gC.ld((uint32_t)((int64_t)(16 * bJ[s] + fr + 4 * rg) * lda + 16 * bI[s] + fc));
-        }
-    }
-    // column block b of L staged once per workgroup (16 columns x 128 rows, coalesced), the
-    // fragments then read from LDS: ~9x fewer handed-off loads than per-block fragments
-    double* stg = Ab + NPK * 256;
-    unsigned have = 0;
-#pragma unroll 1
-    for (int b = 0; b < NDB; ++b) {
-        if (t == 0 && have <= (unsigned)b) {  // one lane polls; the barrier below releases the rest
-            bool got = false;
-            for (int it = 0; it < (1 << 23); ++it) {
-                unsigned mn = __hip_atomic_load(&sprog[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-                for (int g = 1; g < NDB; ++g) {
-                    const unsigned x = __hip_atomic_load(&sprog[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    mn = x < mn ? x : mn;
-                }
-                have = mn;
-                if (have > (unsigned)b) {
-                    got = true;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            if (!got) {
-                have = (unsigned)NDB;  // expired: go on with what is there, flagged
-                atomicOr(err, 1u);
-                atomicOr(rerr, 2u);
-            }
-        }
-        __syncthreads();  // (also: every wave is done reading the previous block's staging)
-        {
-            double x[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int e = t + 512 * i;
-                x[i] = gP.ld((uint32_t)((int64_t)(16 * b + (e >> 7)) * lda + (e & 127)));
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) stg[t + 512 * i] = x[i];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            if (wave + 8 * s < NPK) {
-                double fa[4], fb[4];
-#pragma unroll
-                for (int st = 0; st < 4; ++st) {
-                    const int col = (4 * st + fr) * 128;
-                    fb[st] = stg[col + 16 * bI[s] + fc];
-                    fa[st] = stg[col + 16 * bJ[s] + fc];
-                }
-#pragma unroll
-                for (int st = 0; st < 4; ++st)
-                    acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[st], fb[st], acc[s], 0, 0, 2);  // neg B
-            }
-        }
-    }
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-        if (wave + 8 * s < NPK)
-#pragma unroll
-            for (int rg = 0; rg < 4; ++rg) Ab[bidx(bI[s], bJ[s]) * 256 + (fr + 4 * rg) * 16 + fc] = acc[s][rg];
-}
-
-template <int AUX, bool FUSED = false>
 __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restrict__ Ag, int64_t lda, int64_t N,
                                                  int64_t g0, double* __restrict__ Dinv, EvalResult* __restrict__ res,
                                                  double* Dl = nullptr, unsigned* prog = nullptr,
-                                                 unsigned long long* dst = nullptr, const double* fP = nullptr,
-                                                 const unsigned* fsprog = nullptr, unsigned* ferr = nullptr) {
+                                                 unsigned long long* dst = nullptr) {
     double* colbuf = smem;
     double* rdiag = colbuf + DIAG2_COLBUF;
     double* Ab = rdiag + NB;
@@ -1231,9 +1139,7 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
     // waves 2-7, written to LDS while panel 0 is swept.
     double2 rest[10];
     const int tt = t - 128;  // waves 2-7: 0 .. 383
-    if constexpr (FUSED) {
-        diag2_fused_load<AUX>(Ab, Ag, fP, lda, fsprog, ferr, &res->err);
-    } else {
+    {
         const Gm<AUX> g(Ag);
         double2 col0[2];
 #pragma unroll
@@ -1291,7 +1197,7 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
         } else if (wave == 1 && s < 4) {
             diag2_sweep_b(Ab, colbuf, s, lane, res);
         } else {
-            if (!FUSED && s == 0 && wave >= 2) {  // the rest of the block into LDS
+            if (s == 0 && wave >= 2) {  // the rest of the block into LDS
 #pragma unroll
                 for (int i = 0; i < 10; ++i) {
                     const int q = tt + 384 * i;
@@ -1337,456 +1243,6 @@ __device__ __forceinline__ void potrf_diag2_body(double* smem, double* __restric
     if (wave != 4) diag2_store_column<AUX>(Ab, Ag, lda, NDB - 1, wave < 4 ? t : t - 64, 448);
     STAMP(19);
     dstamp(19);
-}
-// ---------------------------------------------------------------------------------
-// Diagonal block, round 5 (potrf_diag3_body): the same arithmetic contract as diag2
-// (pivots of padding columns 1, info = first pivot <= 0, L in the lower triangle with zeros
-// above, the eight 16x16 inverses), with the pivot wave's issue count halved:
-//
-// Pivot wave (wave 0): ONLY the 16x16 diagonal block of panel s, kept in the f64 MFMA
-// accumulator layout (lane (qc, i) = (lane >> 4, lane & 15) holds element (i, 4m + qc)
-// in slot m). The block is factored in four groups of 4 columns:
-//   - the group's 4 columns of every row are replicated over the four 16-lane rows
-//     (w[0..3], an all-gather by v_permlane16/32_swap), so the values the pivot chain
-//     needs (L(c+1, c), the next pivot, L(4g+k', c)) are DPP row broadcasts
-//     (v_mov_b64 row_newbcast), no v_readlane and no LDS round trip;
-//   - pivot chain per column: rsq -> 1/sqrt(p) (one third-order step, as diag2) ->
-//     L(c+1, c) = a rd -> next pivot = b - L(c+1, c)^2;
-//   - the rank-4 update of the later groups is ONE v_mfma_f64_16x16x4f64 on the group's
-//     final columns (the MFMA operand of lane (qc, i) is L(i, 4g+qc): the accumulator slot).
-// ~25 instructions per column against diag2's ~50; the sweep 2.6-3.1k cycles per panel in
-// situ against 4.4-4.8k (tools/diag_probe.hip). Each column is published
-// as a 64-lane record (L(i, c) for i > c, rd in slot c as the flag, the pivot in slot 16+c).
-// Row waves (waves 1, 2): rows 16s+16 .. 127 of panel s, one row per lane, consuming the
-// records (one slot per lane + DPP broadcasts, two records in flight); 16 spare lanes
-// compute the panel's 16x16 inverse from unit rows by the same recurrence.
-// Block-column updates: waves 3 and 7 accumulate column s+1's blocks over the panels k < s
-// during panel s (left-looking, MFMA); after the panel's one barrier the pivot wave adds
-// panel s to its next diagonal block and the free waves to the blocks below (one each).
-// The pivot <= 0 test reads the records one panel later, off the pivot wave.
-// ---------------------------------------------------------------------------------
-constexpr int DIAG3_REC = 2 * 16 * 64;                          // records of even / odd panels
-constexpr int DIAG3_SMEM = DIAG3_REC + NB + 8 + NPK * 256;      // records, rdiag, counters, Ab
-static_assert(DIAG3_SMEM >= DIAG2_SMEM, "tail_kernel's LDS covers both diagonal kernels");
-
-// lane r of every 16-lane row to the whole row (r folds to a constant in the unrolled sweep)
-__device__ __forceinline__ double row_bcast(double x, int r) {
-    const long long v = __double_as_longlong(x);
-    long long o = v;
-    switch (r) {
-#define D3_RB(n)                                                   \
-    case n:                                                        \
-        o = __builtin_amdgcn_mov_dpp(v, 0x150 + n, 0xf, 0xf, false); \
-        break;
-        D3_RB(0) D3_RB(1) D3_RB(2) D3_RB(3) D3_RB(4) D3_RB(5) D3_RB(6) D3_RB(7)
-        D3_RB(8) D3_RB(9) D3_RB(10) D3_RB(11) D3_RB(12) D3_RB(13) D3_RB(14) D3_RB(15)
-#undef D3_RB
-        default: break;
-    }
-    return __longlong_as_double(o);
-}
-
-// w[k] = x of lane (k, lane & 15): the four 16-lane rows' values, in every row
-__device__ __forceinline__ void rows_gather(double x, double (&w)[4]) {
-    const long long v = __double_as_longlong(x);
-    const unsigned lo = (unsigned)v, hi = (unsigned)((unsigned long long)v >> 32);
-    const auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // rows 0 0 2 2 | 1 1 3 3
-    const auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-    const auto l02 = __builtin_amdgcn_permlane32_swap(l16[0], l16[0], false, false);  // rows 0 | 2
-    const auto l13 = __builtin_amdgcn_permlane32_swap(l16[1], l16[1], false, false);  // rows 1 | 3
-    const auto h02 = __builtin_amdgcn_permlane32_swap(h16[0], h16[0], false, false);
-    const auto h13 = __builtin_amdgcn_permlane32_swap(h16[1], h16[1], false, false);
-    auto mk = [](unsigned a, unsigned b) {
-        return __longlong_as_double((long long)(((unsigned long long)b << 32) | (unsigned long long)a));
-    };
-    w[0] = mk(l02[0], h02[0]);
-    w[1] = mk(l13[0], h13[0]);
-    w[2] = mk(l02[1], h02[1]);
-    w[3] = mk(l13[1], h13[1]);
-}
-
-// accumulator-layout views of a 16x16 column-major block of Ab (dblk_update's layout)
-__device__ __forceinline__ d4 dacc_load(const double* Ab, int I, int J, int lane) {
-    const double* C = Ab + bidx(I, J) * 256;
-    const int fr = lane >> 4, fc = lane & 15;
-    d4 acc;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = C[(fr + 4 * q) * 16 + fc];
-    return acc;
-}
-__device__ __forceinline__ void dacc_store(double* Ab, int I, int J, int lane, const d4& acc) {
-    double* C = Ab + bidx(I, J) * 256;
-    const int fr = lane >> 4, fc = lane & 15;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) C[(fr + 4 * q) * 16 + fc] = acc[q];
-}
-// acc -= L_Ik L_Jk^T
-__device__ __forceinline__ void dacc_sub(d4& acc, const double* Ab, int I, int J, int k, int lane) {
-    const double* LI = Ab + bidx(I, k) * 256;
-    const double* LJ = Ab + bidx(J, k) * 256;
-    const int fr = lane >> 4, fc = lane & 15;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(LJ[(4 * kk + fr) * 16 + fc], LI[(4 * kk + fr) * 16 + fc], acc, 0, 0,
-                                                   1);  // neg A
-}
-
-// The pivot wave's sweep of panel s. acc: the updated diagonal block (accumulator layout,
-// padding pivots already replaced); fin[g]: the final L of group g in the same layout
-// (zeros above the diagonal); rec: this panel's records.
-__device__ __forceinline__ void diag3_pivot(d4& acc, double (&fin)[4], double* rec, int lane) {
-    asm volatile("" : "+v"(lane));
-    const int qc = lane >> 4, i = lane & 15;
-    double w[4];
-    rows_gather(acc[0], w);
-    double piv = row_bcast(w[0], 0);
-    double k375 = 0.375;  // kept in a VGPR (not an inline constant)
-    PIN(k375);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int c = 4 * g + k;
-            // off the chain first: the unscaled column values the chain and the near
-            // updates need, broadcast from their rows
-            double a1 = 0.0, bb = 0.0, xs[4];
-            if (k < 3) {
-                a1 = row_bcast(w[k], c + 1);      // A'(c+1, c)
-                bb = row_bcast(w[k + 1], c + 1);  // pivot c+1 before column c
-            }
-#pragma unroll
-            for (int k2 = k + 2; k2 < 4; ++k2) xs[k2] = row_bcast(w[k], 4 * g + k2);
-            const double y = __builtin_amdgcn_rsq(piv);
-            const double t = piv * y;
-            const double e = fma(-t, y, 1.0);
-            const double cc = fma(e, k375, 0.5);
-            const double ye = y * e;
-            const double rd = fma(ye, cc, y);  // 1/sqrt(p), <= 1 ulp
-            const double pv = piv;
-            w[k] = w[k] * rd;  // L(i, c) below the diagonal, sqrt(p) on it
-            // the record: L(i, c) in slots i > c, rd in slot c (the flag), the pivot in
-            // slot 16 + c (tested for <= 0 one panel later, off this wave)
-            rec[c * 64 + lane] = lane == c ? rd : (lane == 16 + c ? pv : w[k]);
-            SB();  // the record goes out now (the row waves follow it), not with the group's
-            if (k < 3) {
-                const double al = a1 * rd;  // L(c+1, c)
-                piv = fma(-al, al, bb);     // bitwise the value row c+1's lanes hold after the update
-                w[k + 1] = fma(-w[k], al, w[k + 1]);
-#pragma unroll
-                for (int k2 = k + 2; k2 < 4; ++k2) w[k2] = fma(-w[k], xs[k2] * rd, w[k2]);  // L(4g+k2, c)
-            }
-        }
-        const double f = qc == 0 ? w[0] : qc == 1 ? w[1] : qc == 2 ? w[2] : w[3];
-        fin[g] = i >= 4 * g + qc ? f : 0.0;
-        if (g < 3) {
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(fin[g], fin[g], acc, 0, 0, 1);  // later groups -= L_g L_g^T
-            rows_gather(acc[g + 1], w);
-            piv = row_bcast(w[0], 4 * g + 4);
-        }
-    }
-}
-
-// Rows row0 + lane (one per lane, row < 128) of panel s: consume the pivot wave's records.
-// Each lane reads ONE slot of record c (slot lane & 15: a 16-lane row holds the whole
-// record) and the values are broadcast inside the row by DPP (row_newbcast), so a record
-// costs the LDS 512 bytes per wave instead of 16 x 512 (every lane reading every slot).
-// Record c+1 is read while column c is updated. A 16-lane row's slots are read in one
-// LDS cycle and the record is one 16-lane write, so a row that sees the flag (slot c) set
-// sees the record; the wave goes on when every row does (else: sleep, read again).
-// Lanes 48-63 of the wave named by invw are never live rows (rows >= 128): they start
-// from the unit row e_j (j = lane - 48) and the same recurrence leaves column j of L_ss^-1
-// in them, written to Dinv (and Dl) -- the panel's 16x16 inverse, off every other wave.
-// Padding columns (>= npiv) use rd = 1 (diag2's unit pivots; their rows below are zeros).
-// Every finished group of 4 columns goes to LDS at once, counted in *gprog (4 s + g + 1).
-template <int AUX>
-__device__ __forceinline__ void diag3_rows(double* Ab, const double* rec, int s, int row0, int lane, int npiv,
-                                           bool invw, double* __restrict__ Dinv, double* Dl, EvalResult* res,
-                                           unsigned* gprog) {
-    asm volatile("" : "+v"(lane));
-    const int row = row0 + lane;
-    const bool live = row < NB;
-    const bool inv = invw && lane >= 48;  // the caller guarantees row >= NB there
-    double* blk = Ab + bidx(live ? (row >> 4) : NDB - 1, s) * 256;
-    const int rr = row & 15;
-    const double* slot = rec + (lane & 15);
-    double v[16];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) v[c] = blk[c * 16 + rr];  // every lane's address is valid: no branches
-#pragma unroll
-    for (int c = 0; c < 16; ++c) v[c] = inv ? (c == lane - 48 ? 1.0 : 0.0) : v[c];
-    bool timeout = false;
-    // records c and c+1 in flight while column c-1 is updated
-    double x = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    double xn = __hip_atomic_load(slot + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        // the flag: slot c of each 16-lane row (lanes c, 16+c, 32+c, 48+c)
-        // (the test is straight-line code: a loop header here would make the compiler wait
-        // for the record prefetched behind this one as well)
-        const unsigned long long fmask = 0x0001000100010001ull << c;
-        if (__builtin_expect((__builtin_amdgcn_ballot_w64(x == -1.0) & fmask) != 0, 0)) {
-            int it = 0;
-            do {
-                x = __hip_atomic_load(slot + c * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            } while ((__builtin_amdgcn_ballot_w64(x == -1.0) & fmask) && ++it < (1 << 22));
-            if (__builtin_amdgcn_ballot_w64(x == -1.0) & fmask) timeout = true;  // results flagged, not trusted
-        }
-        double xnn = 0.0;
-        if (c + 2 < 16) xnn = __hip_atomic_load(slot + (c + 2) * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        double bx[16];  // the record's values, broadcast before l is known
-#pragma unroll
-        for (int c2 = c; c2 < 16; ++c2) bx[c2] = row_bcast(x, c2);
-        const double l = v[c] * (c >= npiv ? 1.0 : bx[c]);
-        v[c] = l;
-#pragma unroll
-        for (int c2 = c + 1; c2 < 16; ++c2) v[c2] = fma(-l, bx[c2], v[c2]);
-        // column c's updates happen here, not sunk below the next column's wait
-#pragma unroll
-        for (int c2 = c; c2 < 16; ++c2) PIN(v[c2]);
-        if (c + 1 < 16) PIN(xn);  // the next record is tested after these updates
-        if ((c & 3) == 3) {
-            // columns c-3 .. c are final: into LDS, then the group count (LDS is in order
-            // within a wave: the M waves that see the count see the columns)
-            if (live) {
-#pragma unroll
-                for (int c2 = c - 3; c2 <= c; ++c2) blk[c2 * 16 + rr] = v[c2];
-            }
-            asm volatile("" ::: "memory");
-            if (gprog && lane == 0)
-                __hip_atomic_store(gprog, (unsigned)(4 * s + (c >> 2) + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        x = xn;
-        xn = xnn;
-    }
-    if (timeout && lane == 0) atomicOr(&res->err, 1u);
-    if (inv) {
-        const int j = lane - 48;
-        const Gm<AUX> g(Dinv);
-#pragma unroll
-        for (int r2 = 0; r2 < 16; r2 += 2) g.st2((uint32_t)(s * 256 + j * 16 + r2), make_double2(v[r2], v[r2 + 1]));
-        if (Dl) {
-#pragma unroll
-            for (int r2 = 0; r2 < 16; r2 += 2)
-                *reinterpret_cast<double2*>(&Dl[s * 256 + j * 16 + r2]) = make_double2(v[r2], v[r2 + 1]);
-        }
-    }
-}
-
-// Blocks (I0, J) and (I1, J) (I1 < 0: none) -= sum over panels k < kend of L_Ik L_Jk^T,
-// in LDS. Two accumulators interleaved, L_Jk shared, panel k+1's operands loaded while
-// panel k's MFMAs run.
-__device__ __forceinline__ void diag3_accum(double* Ab, int I0, int I1, int J, int kend, int lane) {
-    const int fr = lane >> 4, fc = lane & 15, off = fr * 16 + fc;
-    const bool two = I1 >= 0;
-    d4 a0 = dacc_load(Ab, I0, J, lane), a1 = {0.0, 0.0, 0.0, 0.0};
-    if (two) a1 = dacc_load(Ab, I1, J, lane);
-    double lj[4], l0[4], l1[4];
-    auto ld = [&](int k, double (&xj)[4], double (&x0)[4], double (&x1)[4]) {
-        const double* LJ = Ab + bidx(J, k) * 256 + off;
-        const double* L0 = Ab + bidx(I0, k) * 256 + off;
-        const double* L1 = Ab + bidx(two ? I1 : I0, k) * 256 + off;
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            xj[kk] = LJ[64 * kk];
-            x0[kk] = L0[64 * kk];
-            x1[kk] = two ? L1[64 * kk] : 0.0;
-        }
-    };
-    ld(0, lj, l0, l1);
-    for (int k = 0; k < kend; ++k) {
-        double nj[4], n0[4], n1[4];
-        if (k + 1 < kend) ld(k + 1, nj, n0, n1);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(lj[kk], l0[kk], a0, 0, 0, 1);  // neg A
-            if (two) a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(lj[kk], l1[kk], a1, 0, 0, 1);
-        }
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            lj[kk] = nj[kk];
-            l0[kk] = n0[kk];
-            l1[kk] = n1[kk];
-        }
-    }
-    dacc_store(Ab, I0, J, lane, a0);
-    if (two) dacc_store(Ab, I1, J, lane, a1);
-}
-
-// Panel (columns col0 .. col0+15) done: OpenBLAS potf2's test (the reference's dpotrf,
-// 0.3.20) on its pivots -- ajj <= 0 only, so a NaN pivot is not reported and propagates to
-// a NaN logpdf, as in the reference; padding columns (>= N) excluded. Then, if reset, the
-// record's flags go back to -1 for the panel after next (same parity).
-__device__ __forceinline__ void diag3_panel_info(double* rq, int64_t col0, int64_t N, int lane, EvalResult* res,
-                                                 bool reset) {
-    double pv = 1.0;
-    if (lane < 16) pv = rq[lane * 64 + 16 + lane];
-    const unsigned long long badm = __ballot(lane < 16 && col0 + lane < N && pv <= 0.0);
-    if (badm && lane == 0) atomicMin(&res->info, (unsigned long long)(col0 + __builtin_ctzll(badm) + 1));
-    if (reset && lane < 16) rq[lane * 65] = -1.0;
-}
-
-// Row waves: wave 1 (rows 16s+16 .. 16s+79; its lanes 48-63 invert from panel 4 on) and
-// wave 2 (rows 16s+80 .. 16s+143 up to panel 3; lanes 48-63 invert up to panel 3).
-__device__ __forceinline__ bool diag3_rowwave(int wave, int s) { return wave == 1 || (wave == 2 && s <= 3); }
-// The waves that store panel s-1's block column during panel s: 3 5 6 7 4, and 2 once it
-// has no rows; index and count.
-__device__ __forceinline__ int diag3_sindex(int wave, int s) {
-    return wave == 3 ? 0 : wave == 5 ? 1 : wave == 6 ? 2 : wave == 7 ? 3 : wave == 4 ? 4 : (wave == 2 && s >= 4) ? 5 : -1;
-}
-__device__ __forceinline__ int diag3_scount(int s) { return 5 + (s >= 4); }
-// blocks of column t+1 written after panel t (rows t+2 .. 7), summed over t < s
-__device__ __forceinline__ unsigned diag3_ready_target(int s) { return (unsigned)(6 * s - s * (s - 1) / 2); }
-
-// 512 threads, DIAG3_SMEM doubles of LDS (smem); Dl / prog as potrf_diag2_body.
-template <int AUX>
-__device__ __forceinline__ void potrf_diag3_body(double* smem, double* __restrict__ Ag, int64_t lda, int64_t N,
-                                                 int64_t g0, double* __restrict__ Dinv, EvalResult* __restrict__ res,
-                                                 double* Dl = nullptr, unsigned* prog = nullptr) {
-    double* rec = smem;
-    double* rdiag = rec + DIAG3_REC;  // (unused: the inverse comes from the records)
-    unsigned* ready = reinterpret_cast<unsigned*>(rdiag + NB);  // blocks of the next column written
-    double* Ab = rdiag + NB + 8;
-    const int t = otid(), wave = t >> 6, lane = t & 63;
-    if (wave == 0) __builtin_amdgcn_s_setprio(3);
-    else if (wave <= 2) __builtin_amdgcn_s_setprio(2);
-    else __builtin_amdgcn_s_setprio(1);
-    STAMP(20);
-    // Load: block column 0 by everyone (panel 0 needs it), the other 28 blocks by waves 3-7,
-    // written to LDS while panel 0 is swept (diag2's scheme).
-    double2 rest[12];
-    const int tt = t - 192;  // waves 3-7: 0 .. 319
-    {
-        const Gm<AUX> g(Ag);
-        double2 col0[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int q = t + 512 * i, I = q >> 7, pr = q & 127, c = pr >> 3, r = 2 * (pr & 7);
-            col0[i] = g.ld2((uint32_t)((int64_t)c * lda + 16 * I + r));
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int q = t + 512 * i, I = q >> 7, pr = q & 127;
-            *reinterpret_cast<double2*>(&Ab[bidx(I, 0) * 256 + 2 * pr]) = col0[i];
-        }
-        if (wave >= 3) {
-#pragma unroll
-            for (int i = 0; i < 12; ++i) {
-                const int q = tt + 320 * i;
-                if (q < 28 * 128) {
-                    int I, J;
-                    diag2_block_of(q >> 7, I, J);
-                    const int pr = q & 127, c = pr >> 3, r = 2 * (pr & 7);
-                    rest[i] = g.ld2((uint32_t)((int64_t)(16 * J + c) * lda + 16 * I + r));
-                }
-            }
-        }
-    }
-    if (wave == 3 && lane < 32) rec[(lane >> 4) * 1024 + (lane & 15) * 65] = -1.0;  // both parities' flags
-    if (wave == 3 && lane == 0) *ready = 0u;
-    // a barrier that does not wait for the other blocks' loads (__syncthreads would)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    STAMP(0);
-    d4 acc;  // pivot wave: the diagonal block; the post-barrier step: a block below it
-    double fin[4];
-    const int64_t g0N = N - g0;
-    if (wave == 0) acc = dacc_load(Ab, 0, 0, lane);
-    if (wave >= 3) {  // the rest of the block into LDS while panel 0 is swept (before the loop:
-                      // these registers must not stay live through it)
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-            const int q = tt + 320 * i;
-            if (q < 28 * 128) {
-                int I, J;
-                diag2_block_of(q >> 7, I, J);
-                *reinterpret_cast<double2*>(&Ab[bidx(I, J) * 256 + 2 * (q & 127)]) = rest[i];
-            }
-        }
-    }
-    for (int s = 0; s < NDB; ++s) {
-        const int R0 = 16 * s;
-        double* rp = rec + (s & 1) * 1024;
-        const int64_t np64 = g0N - R0;
-        const int npiv = (int)(np64 < 0 ? 0 : (np64 > 16 ? 16 : np64));  // columns >= npiv: padding
-        STAMP(1 + 2 * s);
-        if (wave == 0) {
-            // padding columns (>= N): unit pivots; column N itself (the augmented row's)
-            // gets a huge pivot so that the rows below it divide to exact zeros, and is
-            // written as 1 (its rd is taken as 1 everywhere else)
-            const int qc = lane >> 4, i = lane & 15;
-            if (npiv < 16) {
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const int col = 4 * m + qc;
-                    if (i == col && col >= npiv) acc[m] = (int64_t)col == np64 ? 0x1p1000 : 1.0;
-                }
-            }
-            diag3_pivot(acc, fin, rp, lane);
-            double* D = Ab + bidx(s, s) * 256;
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const int col = 4 * m + qc;
-                D[col * 16 + i] = (i == col && col >= npiv) ? 1.0 : fin[m];
-            }
-            STAMP(2 + 2 * s);
-        } else if (diag3_rowwave(wave, s)) {
-            // rows 16s+16 .. 127: wait for this column's blocks (the post-barrier step)
-            const unsigned tgt = diag3_ready_target(s);
-            unsigned have = __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            for (int it = 0; have < tgt && it < (1 << 22); ++it)
-                have = __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (have < tgt && lane == 0) atomicOr(&res->err, 1u);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            // the inverse lanes: wave 2's up to panel 3, wave 1's from panel 4 (rows >= 128)
-            const bool invw = (wave == 2) == (s <= 3);
-            diag3_rows<AUX>(Ab, rp, s, R0 + 16 + 64 * (wave - 1), lane, npiv, invw, Dinv, Dl, res, nullptr);
-        } else {
-            if (s >= 1) {
-                const int e = diag3_sindex(wave, s);
-                diag2_store_column<AUX>(Ab, Ag, lda, s - 1, e * 64 + lane, diag3_scount(s) * 64);
-                if (wave == 7) diag3_panel_info(rec + ((s - 1) & 1) * 1024, g0 + 16 * (s - 1), N, lane, res, true);
-            }
-            // left-looking on waves 3 and 7: column s+1's blocks over panels k < s (pairs
-            // I, I+2), back into LDS
-            if (s >= 1 && s + 1 < NDB && (wave == 3 || wave == 7)) {
-                const int J = s + 1;
-                for (int I = J + (wave == 7); I < NDB; I += 4) diag3_accum(Ab, I, I + 2 < NDB ? I + 2 : -1, J, s, lane);
-            }
-        }
-        if (prog && wave >= 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        // block column s is final in LDS; columns and inverses < s in global
-        if (prog && s >= 1 && wave == 3 && lane == 0)
-            __hip_atomic_store(prog, (unsigned)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (s + 1 < NDB) {
-            const int J = s + 1;
-            if (wave == 0) {
-                acc = dacc_load(Ab, J, J, lane);  // column J's diagonal block over panels < s
-                dacc_sub(acc, Ab, J, J, s, lane);
-            } else if (!diag3_rowwave(wave, s + 1)) {
-                // panel s into column J's blocks below the diagonal, one block per free wave:
-                // 4 5 6 3 7, and 2 once it has no rows
-                const int e = wave == 4 ? 0 : wave == 5 ? 1 : wave == 6 ? 2 : wave == 3 ? 3 : wave == 7 ? 4 : 5;
-                const int ne = diag3_rowwave(2, s + 1) ? 5 : 6;
-                unsigned nmine = 0;
-                for (int I = J + 1 + e; I < NDB; I += ne) {
-                    d4 a = dacc_load(Ab, I, J, lane);
-                    dacc_sub(a, Ab, I, J, s, lane);
-                    dacc_store(Ab, I, J, lane, a);
-                    ++nmine;
-                }
-                // LDS is in order within a wave: the blocks land before the count
-                asm volatile("" ::: "memory");
-                if (nmine && lane == 0) __hip_atomic_fetch_add(ready, nmine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        }
-    }
-    STAMP(17);
-    if (wave == 7) diag3_panel_info(rec + 1024, g0 + 16 * (NDB - 1), N, lane, res, false);
-    diag2_store_column<AUX>(Ab, Ag, lda, NDB - 1, t, 512);  // the last block column
-    STAMP(19);
 }
 #undef SB
 #undef PIN
@@ -2563,7 +2019,11 @@ __device__ __forceinline__ double dk_ou(double p, double xi, double xj, const do
 // in place (wt = 2 off the diagonal, 1 on it, 0 outside the lower triangle / past N); then
 // one pass per term over the 64 weights of a lane, each term kind a loop of its own (the
 // code stays small: a fully unrolled term x element nest overflowed the instruction cache).
-// The k-loop's LDS staging buffer holds the tile's coordinates, alpha and the exp table.
+// The k-loop's LDS staging buffer holds the tile's coordinates, alpha and the exp table
+// (checked for every GAPLAC_KB: with KB = 8 they fill it exactly); the per-wave sums have
+// their own small array.
+static_assert(sizeof(MmaLds) >= (2 * GAPLAC_MAX_TERMS * NB + 2 * NB + 256) * sizeof(double),
+              "cinv_contract_kernel's coordinates, alpha and exp table must fit the staging LDS");
 __global__ __launch_bounds__(256, 2) void cinv_contract_kernel(const double* __restrict__ A, int64_t lda, int64_t Np,
                                                                int64_t N, const double* __restrict__ X, int64_t ldx,
                                                                const double* __restrict__ alpha,
@@ -2596,7 +2056,7 @@ __global__ __launch_bounds__(256, 2) void cinv_contract_kernel(const double* __r
         double* const ar = xc + GAPLAC_MAX_TERMS * NB;  // alpha of the rows, then of the columns
         double* const ac = ar + NB;
         double* const tbl = ac + NB;                    // exp table
-        double* const red = tbl + 256;                  // red[w * (T + 1) + t]
+        __shared__ double red[4 * (GAPLAC_MAX_TERMS + 1)];  // red[w * (T + 1) + t]
         const int64_t r0 = (int64_t)I * NB, c0 = (int64_t)J * NB;
         for (int idx = tid; idx < T * NB; idx += 256) {
             const int t = idx / NB, q = idx % NB;
@@ -3293,8 +2753,8 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int
     const unsigned long long t0 = wall_clock64();
     for (unsigned it = 1;; ++it) {
         bool ok;
-        if (type == TK_D) {  // (q = 1: applies column k-1's update itself, behind its TRSM)
-            ok = tail_ld(&c->units[k * TAIL_TMAX + k]) >= TAIL_NQ * (unsigned)(q == 1 ? k - 1 : k);
+        if (type == TK_D) {
+            ok = tail_ld(&c->units[k * TAIL_TMAX + k]) >= TAIL_NQ * (unsigned)k;
         } else if (type == TK_S) {  // the block itself; D(k)'s progress inside tail_trsm_pipe
             ok = tail_ld(&c->units[i * TAIL_TMAX + k]) >= 4u * k;
             if (q == TAIL_S_WHOLE && ok) ok = tail_ld(&c->ddone[k]) != 0u;  // not pipelined: D(k) done
@@ -3314,14 +2774,11 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int
     }
 }
 
-// The tail's diagonal blocks: the round-3 potrf_diag2_body (0) or potrf_diag3_body (1, a
-// build switch: N = 4096 / 8192 -0.5%, select +0.3% slower).
-#ifndef GAPLAC_DIAG3
-#define GAPLAC_DIAG3 0
-#endif
+// The tail's diagonal blocks run potrf_diag2_body (round 3); its LDS also holds the TRSM's
+// staged L_kk and inverses (tail_trsm_stage: 36 x 256 doubles).
+static_assert(DIAG2_SMEM >= (TRSM_LBLK + NDB) * 256, "tail_kernel LDS too small for the TRSM staging");
 __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict__ kt) {
-    // (diag2 + the fused update's 16 x 128 staging, diag2_fused_load)
-    __shared__ double smem[GAPLAC_DIAG3 && DIAG3_SMEM > DIAG2_SMEM + 16 * NB ? DIAG3_SMEM : DIAG2_SMEM + 16 * NB];
+    __shared__ double smem[DIAG2_SMEM];
     __shared__ unsigned s_task;
     __shared__ unsigned s_rowf[NDB];
     kt_begin(kt);
@@ -3353,23 +2810,11 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         if (faulted) {
         } else if (type == TK_D) {
             if ((int64_t)gk * NB < a.N) {
-                if (q == 1)
-                    potrf_diag2_body<GM_SC1, true>(smem, colk + (int64_t)gk * NB, a.lda, a.N, (int64_t)gk * NB,
-                                                   Dinv + (size_t)gk * DINV_PER_BLOCK, res, nullptr, &ctl->dprog[k],
-                                                   a.trace && a.nmodels == 1
-                                                       ? a.trace + 3 * (size_t)a.ntasks + (size_t)TAIL_DSTAMPS * k
-                                                       : nullptr,
-                                                   A + (int64_t)(gk - 1) * NB * a.lda + (int64_t)gk * NB,
-                                                   ctl->sprog[k - 1], &ctl->err);
-                else if (GAPLAC_DIAG3)
-                    potrf_diag3_body<GM_SC1>(smem, colk + (int64_t)gk * NB, a.lda, a.N, (int64_t)gk * NB,
-                                             Dinv + (size_t)gk * DINV_PER_BLOCK, res, nullptr, &ctl->dprog[k]);
-                else
-                    potrf_diag2_body<GM_SC1>(smem, colk + (int64_t)gk * NB, a.lda, a.N, (int64_t)gk * NB,
-                                             Dinv + (size_t)gk * DINV_PER_BLOCK, res, nullptr, &ctl->dprog[k],
-                                             a.trace && a.nmodels == 1
-                                                 ? a.trace + 3 * (size_t)a.ntasks + (size_t)TAIL_DSTAMPS * k
-                                                 : nullptr);
+                potrf_diag2_body<GM_SC1>(smem, colk + (int64_t)gk * NB, a.lda, a.N, (int64_t)gk * NB,
+                                         Dinv + (size_t)gk * DINV_PER_BLOCK, res, nullptr, &ctl->dprog[k],
+                                         a.trace && a.nmodels == 1
+                                             ? a.trace + 3 * (size_t)a.ntasks + (size_t)TAIL_DSTAMPS * k
+                                             : nullptr);
             }
         } else if (type == TK_S && q == TAIL_S_WHOLE) {
             tail_trsm<GM_SC1>(smem, colk, a.lda, gk, a.ts + i, q, Dinv + (size_t)gk * DINV_PER_BLOCK,
@@ -3404,9 +2849,6 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         __syncthreads();
         if (threadIdx.x == 0 && !faulted) {
             if (type == TK_D) {
-                if (q == 1)  // (the column k-1 update it applied: the tile's count stays complete)
-                    __hip_atomic_fetch_add(&ctl->units[k * TAIL_TMAX + k], TAIL_NQ, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_fetch_add(&ctl->ddone[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else if (type == TK_S) {  // two halves per tile (or one whole-tile task): done at 2
                 __hip_atomic_fetch_add(&ctl->sdone[i * TAIL_TMAX + k], q == TAIL_S_WHOLE ? 2u : 1u, __ATOMIC_RELAXED,
@@ -3473,8 +2915,7 @@ void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<s
 // Single evaluations use GW = 4, NEAR = 4 (latency); batched launches fewer per-column
 // updates (throughput).
 void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* colstart, int gw, int near,
-                      int quad_last, bool whole_trsm, int group, int xrows, int sub_ahead, int sub_dist,
-                      int crit_quads, bool diag_quads, bool fuse_q) {
+                      int quad_last, bool whole_trsm, int group, int xrows, int crit_quads) {
     group = group >= 4 ? 4 : group >= 2 ? 2 : 1;  // divides the deep width (4 or 8): groups stay in a block
     // deep width; near distance (>= 2: the next two diagonal tiles take per-column Q tasks)
     const int GW = gw == 8 ? 8 : 4, NEAR = std::max(2, near);
@@ -3540,9 +2981,9 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
         const int b = g / GW;
         const int jfar = deep_block(b) ? far_from(b) : T;  // per-column updates below this tile column
         S(g + 2, g);
-        if (!fuse_q) Qs(g + 1, g);  // (fuse_q: D(g+1) applies column g's update itself)
+        Qs(g + 1, g);
         Uq(g + 2, g + 1, g);
-        out.push_back(tail_enc(TK_D, fuse_q ? 1 : 0, g + 1, 0, 0));
+        out.push_back(tail_enc(TK_D, 0, g + 1, 0, 0));
         S(g + 2, g + 1);
         Qs(g + 2, g);
         S(g + 3, g);
@@ -3559,21 +3000,8 @@ void build_tail_tasks(int T, std::vector<uint32_t>& out, std::vector<size_t>* co
         for (int j = g + 2; j < std::min(jfar, T); ++j)
             for (int i = j; i < T; ++i) {
                 if (i == g + 2 && j == g + 2) continue;  // the Q tasks above
-                if (i > j && i - j <= sub_dist && j <= g + 1 + sub_ahead && g >= T - quad_last) {
-                    // a near-diagonal tile a few columns ahead: quadrant tasks, so that its
-                    // update chain catches up after a deep update
-                    for (int q = 1; q <= 4; ++q) out.push_back(tail_enc(TK_U, q, g, i, j));
-                    continue;
-                }
                 if (grouped && (i == j ? j >= g1 + 3 : j >= g1 + 2)) {
                     if (g == g1) out.push_back(tail_enc(TK_U, qgroup, g0, i, j));
-                    continue;
-                }
-                if (diag_quads && i == j) {
-                    // a diagonal tile's per-column update as its three lower quadrants: the
-                    // tile's serial chain of K = 128 updates keeps ahead of the diagonal
-                    // blocks (one whole-tile task is ~24 us of a ~31 us column)
-                    for (int q : {1, 3, 4}) out.push_back(tail_enc(TK_U, q, g, i, j));
                     continue;
                 }
                 out.push_back(tail_enc(TK_U, 0, g, i, j));
@@ -3645,8 +3073,6 @@ int sim_order_tail_tasks(int T, std::vector<uint32_t>& list, int workers) {
         if (t.type == TK_D) {
             const Tile& tl = tile[(size_t)t.k * T + t.k];
             p = tl.group;
-            if (t.q == 1 && t.k >= 1)
-                pipe[(size_t)x] = sof[(size_t)t.k * T + t.k - 1];
             dof[(size_t)t.k] = x;
         } else if (t.type == TK_S) {
             p = tile[(size_t)t.i * T + t.k].group;
@@ -3761,12 +3187,7 @@ bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why
         if (k >= T || i >= R || j >= T || (i >= T && (type == TK_D || type == TK_Q)))
             return fail(n, "task outside the tile range");
         if (type == TK_D) {
-            if (q > 1 || (q == 1 && k == 0)) return fail(n, "a diagonal block task of an unknown kind");
-            if (q == 1) {  // fused: column k-1's update applied by the block itself, behind S(k, k-1)
-                if (units[(size_t)k * T + k] != TAIL_NQ * (unsigned)(k - 1)) return fail(n, "D before its tile is updated");
-                if (sdone[(size_t)k * T + k - 1] != 2u) return fail(n, "fused D before its TRSM is dequeued");
-                units[(size_t)k * T + k] += TAIL_NQ;
-            }
+            if (q != 0) return fail(n, "a diagonal block task of an unknown kind");
             if (units[(size_t)k * T + k] != TAIL_NQ * (unsigned)k) return fail(n, "D before its tile is updated");
             ddone[(size_t)k] += 1;
         } else if (type == TK_S) {

@@ -273,11 +273,19 @@ class TorchTransport:
 class LoopbackTransport:
     """All ranks of the job in this process, on one device: broadcast = D2D copies on the
     receivers' comm streams, ordered after the root's pack; the root's comm stream then
-    waits for every copy, so its buffer is not re-packed before the copies have read it."""
+    waits for every copy, so its buffer is not re-packed before the copies have read it.
+
+    keep_options: leave each rank's schedule options as configured (the multi-rank
+    defaults: chain alone, per-rank bulk kernel) instead of the single-GPU choices the
+    shared device would favour; for correctness checks of those options across ranks that
+    exchange panels (they only add waits inside a rank, so they are valid on one device)."""
+
+    def __init__(self, keep_options: bool = False):
+        self.keep_options = keep_options
 
     def prepare(self, ranks: Sequence, N: int):
         for r in ranks:
-            if len(ranks) > 1 and hasattr(r, "configure"):
+            if len(ranks) > 1 and hasattr(r, "configure") and not self.keep_options:
                 r.configure(big=2, alone=0)  # the ranks share one device: the single-GPU choices
             r.use_torch_panel_buffers(N)
 

@@ -191,3 +191,21 @@ def test_gloo_world2_processes_share_one_gpu():
     rl = R.logpdf(X, terms, 0.1, v)[0]
     for rank, lp, err in got:
         assert abs(lp - rl) <= 1e-12 * abs(rl)
+
+
+@pytest.mark.parametrize("world,spw,N,big", [(4, 2, 12000, 1), (4, 2, 12000, 0), (8, 2, 9000, 1)])
+def test_loopback_multirank_defaults_match_single_gpu(world, spw, N, big):
+    """the P > 1 defaults (chain alone with held post-mark ops, depth 2, chunk 2,
+    the per-rank bulk kernel choice) across ranks that really exchange panels: every rank
+    keeps its options (LoopbackTransport(keep_options=True)); against the single-GPU path
+    at 1e-11, twice through the same workspaces."""
+    X, terms, v = _case(N, seed=N + world)
+    with Context(0) as ctx:
+        ref = ctx.logpdf(X, terms, 0.1, v)
+    ranks = [DI.DistRank(0, world, r, spw=spw, depth=2, chunk=2, big=big, alone=1) for r in range(world)]
+    tr = DI.LoopbackTransport(keep_options=True)
+    for _ in range(2):
+        got = DI.logpdf_dist(ranks, tr, X, terms, 0.1, v)
+        assert abs(got - ref) <= 1e-11 * abs(ref)
+    for r in ranks:
+        r.close()

@@ -1,7 +1,7 @@
 // Diagnostic: the diagonal-block kernel on an idle GPU. Checks it against a CPU Cholesky of
 // the same 128x128 block (L and the 16x16 inverses), prints its per-wave stamps per panel
-// (v1 = potrf_diag_kernel_body, the super-panel chain's; v2 = potrf_diag2_body, round 3;
-// v3 = potrf_diag3_body, the tail's since round 5), checks v2 and v3 against v1 with padding
+// (v1 = potrf_diag_kernel_body, the super-panel chain's; v2 = potrf_diag2_body, the tail's;
+// round 5's diag3 variant is in git history, commit 0770b8a), checks v2 against v1 with padding
 // inside the block and on a non-PD block, and times the other chain kernels alone.
 #define GAPLAC_STAMPS 1
 #include "../gaplac_amd/csrc/gaplac_kernels.hip"
@@ -17,10 +17,6 @@ __global__ __launch_bounds__(256) void diag_v1(double* Ag, int64_t lda, int64_t 
 __global__ __launch_bounds__(512) void diag_v2(double* Ag, int64_t lda, int64_t N, int64_t g0, double* Dinv, EvalResult* res) {
   __shared__ double smem[DIAG2_SMEM];
   potrf_diag2_body<0>(smem, Ag, lda, N, g0, Dinv, res);
-}
-__global__ __launch_bounds__(512) void diag_v3(double* Ag, int64_t lda, int64_t N, int64_t g0, double* Dinv, EvalResult* res) {
-  __shared__ double smem[DIAG3_SMEM];
-  potrf_diag3_body<0>(smem, Ag, lda, N, g0, Dinv, res);
 }
 int main() {
   const int nt = 4, Np = nt * NB;
@@ -55,15 +51,14 @@ int main() {
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
     if (v == 1) diag_v1<<<1, 256>>>(A, Np, N, 0, Dinv, res);
-    else if (v == 2) diag_v2<<<1, 512>>>(A, Np, N, 0, Dinv, res);
-    else diag_v3<<<1, 512>>>(A, Np, N, 0, Dinv, res);
+    else diag_v2<<<1, 512>>>(A, Np, N, 0, Dinv, res);
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(ms, e0, e1));
     CK(hipMemcpy(out.data(), A, out.size() * 8, hipMemcpyDeviceToHost));
     CK(hipMemcpy(dinv.data(), Dinv, dinv.size() * 8, hipMemcpyDeviceToHost));
     return 0;
   };
-  for (int v = 1; v <= 3; ++v) {
+  for (int v = 1; v <= 2; ++v) {
     for (int rep = 0; rep < 4; ++rep) {
       float ms;
       if (run(v, h, 1 << 30, &ms)) return 1;
@@ -84,14 +79,6 @@ int main() {
         for (int i = 0; i < j; ++i) upper = std::fmax(upper, std::fabs(out[(size_t)j * Np + i]));
       printf("diag v%d: %.1f us (event)  max|L-Lcpu| %.2e  max|Dinv L - I| %.2e  upper %.1e  info %llx err %u\n", v, ms * 1e3,
              errL, errD, upper, (unsigned long long)hr.info, hr.err);
-      if (rep == 3 && v == 3) {  // per panel s: the pivot wave's sweep, then to the next panel
-        unsigned long long st[128]; CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof st));
-        printf("  v3 load %llu\n", st[0] - st[20]);
-        for (int s = 0; s < 8; ++s)
-          printf("  v3 s=%d: sweep %5llu  to next panel %5llu\n", s, st[2 + 2 * s] - st[1 + 2 * s],
-                 (s < 7 ? st[3 + 2 * s] : st[17]) - st[2 + 2 * s]);
-        printf("  v3 last store %llu total %llu cycles\n", st[19] - st[17], st[19] - st[20]);
-      }
       if (rep == 3 && v <= 2) {  // per panel s, phase 2 of each wave (cycles, s_memtime)
         unsigned long long st[128]; CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof st));
         printf("  v%d load %llu\n", v, st[0] - st[20]);
@@ -119,15 +106,15 @@ int main() {
     for (int j = 0; j < Np; ++j)
       for (int i = 0; i < Np; ++i)
         if ((i >= Npad || j >= Npad) && i != j) hp[(size_t)j * Np + i] = (i == Npad && j < Npad) ? 0.3 * std::sin(j) : 0.0;
-    std::vector<double> o[4], d[4];
-    EvalResult hv[4];
-    for (int v = 1; v <= 3; ++v) {
+    std::vector<double> o[3], d[3];
+    EvalResult hv[3];
+    for (int v = 1; v <= 2; ++v) {
       if (run(v, hp, Npad, &ms)) return 1;
       o[v] = out;
       d[v] = dinv;
       CK(hipMemcpy(&hv[v], res, sizeof hv[v], hipMemcpyDeviceToHost));
     }
-    for (int v = 2; v <= 3; ++v) {
+    for (int v = 2; v <= 2; ++v) {
       double dl = 0, dd = 0;
       for (int j = 0; j < NB; ++j)
         for (int i = j; i < NB; ++i) dl = std::fmax(dl, std::fabs(o[v][(size_t)j * Np + i] - o[1][(size_t)j * Np + i]));
@@ -137,7 +124,7 @@ int main() {
     }
   }
   // non-PD: zero the block's (37,37) pivot region -> info must be 38 in both
-  for (int v = 1; v <= 3; ++v) {
+  for (int v = 1; v <= 2; ++v) {
     std::vector<double> hb = h;
     for (int i = 0; i < Np; ++i) { hb[(size_t)37 * Np + i] = 0; hb[(size_t)i * Np + 37] = 0; }
     float ms;
