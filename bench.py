@@ -26,7 +26,12 @@ Every rank asserts world size == --gpus and that its device exists; on a 1-GPU b
 With --gpus > 1 rank 0 also measures BASELINE configs[3] (N=65536) spread over all ranks
 (extra.dist) and checks its logpdf against the single-GPU evaluation of the same input in
 the same run (extra.dist.parity_vs_single, bar 1e-9 relative); a failed or non-matching
-dist line makes the process exit non-zero after the JSON line is printed.
+dist line makes the process exit non-zero (4) after the JSON line is printed. The leg runs
+under its own deadline (--dist-deadline, 240 s, well inside the driver's limit and the
+process group's 600 s collective timeout): a leg that hangs (a collective that never
+completes) becomes an error in the line instead of a job killed with no line at all;
+rank 0 prints the replicas line with dist_ok false and the process ends with status 4
+without waiting for the hung collective (bounded_leg).
 
 Prints ONE JSON line (rank 0).
 """
@@ -40,6 +45,7 @@ import platform
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -141,6 +147,42 @@ def load_traffic(name=TRAFFIC_FILE):
 
 
 DIST_PARITY_BAR = 1e-9  # relative, north_star's fp64 bar
+DIST_DEADLINE_S = 240.0  # the configs[3] leg's own deadline (--dist-deadline)
+NONROOT_GRACE_S = 60.0   # other ranks wait this much longer, so rank 0 prints first
+
+
+def bounded_leg(rank: int, fn, deadline_s: float, device=None):
+    """Run one collective leg (fn) on a worker thread under a deadline: (result, expired).
+
+    A leg that does not finish in deadline_s (rank 0; the other ranks NONROOT_GRACE_S
+    later, so that rank 0 reports first) returns ({"error": ...}, True) and leaves its
+    thread behind, blocked in whatever collective hung: the caller must then end the
+    process with os._exit (a clean shutdown would wait for that collective). An exception
+    in fn is returned as {"error": ...} on rank 0 and re-raised on the others (the launcher
+    then stops the job, non-zero). device: the thread's torch device (torch keeps the
+    current device per thread)."""
+    box = {}
+
+    def target():
+        try:
+            if device is not None:
+                import torch
+                torch.cuda.set_device(device)
+            box["value"] = fn()
+        except BaseException as e:  # reported below
+            box["error"] = e
+
+    th = threading.Thread(target=target, name="bounded-leg", daemon=True)
+    th.start()
+    th.join(deadline_s if rank == 0 else deadline_s + NONROOT_GRACE_S)
+    if th.is_alive():
+        return {"error": f"deadline: the leg did not finish within {deadline_s:.0f} s (a collective that never "
+                         f"completed?); not waited for", "deadline_s": deadline_s}, True
+    if "error" in box:
+        if rank != 0:
+            raise box["error"]
+        return {"error": repr(box["error"])[:400]}, False
+    return box["value"], False
 
 
 def _free_port() -> int:
@@ -215,23 +257,46 @@ def init_rank(args):
 
 def main_launcher_check(args):
     """--mode launcher-check: the rank side of the launcher without a GPU (gloo). Every
-    rank checks its env against --gpus, all-reduces its rank, and rank 0 prints one JSON
-    line; --fail-rank r makes rank r exit 3 (tests the launcher's failure path)."""
+    rank checks its env against --gpus, all-reduces its rank, runs a stand-in collective
+    leg through bounded_leg (the configs[3] leg's wrapper), and rank 0 prints one JSON
+    line; --fail-rank r makes rank r exit 3 (tests the launcher's failure path);
+    --hang-rank r makes rank r never join the leg's collective, so the leg hangs on every
+    other rank (tests that a hang ends as a printed line with dist_ok false, status 4)."""
     rank, world, _ = rank_env(args)
     import torch
     import torch.distributed as dist
     if rank == args.fail_rank:
         raise SystemExit(3)
-    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=60))
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
     assert dist.get_world_size() == world
     t = torch.tensor([float(rank)], dtype=torch.float64)
     dist.all_reduce(t)
     ranks = [None] * world
     dist.all_gather_object(ranks, {"rank": rank, "pid": os.getpid()})
+
+    def leg():
+        if rank == args.hang_rank:
+            time.sleep(1e6)  # never joins: the others block in the all_reduce below
+        u = torch.ones(1, dtype=torch.float64)
+        dist.all_reduce(u)
+        return {"value": float(u.item()), "parity_ok": True}
+
+    t0 = time.perf_counter()
+    dist_line, expired = bounded_leg(rank, leg, args.dist_deadline)
     if rank == 0:
-        print(json.dumps({"metric": "launcher-check", "n_gpus": world, "rank_sum": float(t.item()),
-                          "pids": [r["pid"] for r in ranks]}), flush=True)
+        out = {"metric": "launcher-check", "n_gpus": world, "rank_sum": float(t.item()),
+               "pids": [r["pid"] for r in ranks], "extra": {"dist": dist_line},
+               "dist_leg_s": round(time.perf_counter() - t0, 3)}
+        out["dist_ok"] = "error" not in dist_line and bool(dist_line.get("parity_ok"))
+        print(json.dumps(out), flush=True)
+        if not out["dist_ok"]:
+            print(f"bench: stand-in dist leg FAILED: {dist_line.get('error')}", file=sys.stderr, flush=True)
+    if expired:
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(4)  # never wait for the hung collective
     dist.destroy_process_group()
+    return 0 if rank != 0 or out["dist_ok"] else 4
 
 
 def main():
@@ -261,7 +326,10 @@ def main():
     ap.add_argument("--spw", type=int, default=4, help="dist mode: super-panel width in 128-column tiles")
     ap.add_argument("--no-dist", action="store_true",
                     help="replicas mode with --gpus > 1: skip the configs[3] distributed extra line")
+    ap.add_argument("--dist-deadline", type=float, default=DIST_DEADLINE_S,
+                    help="seconds the configs[3] leg (--gpus > 1) may take before it is reported as failed")
     ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # launcher-check only
+    ap.add_argument("--hang-rank", type=int, default=-1, help=argparse.SUPPRESS)  # launcher-check only
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
     if args.gpus < 1:
@@ -368,16 +436,21 @@ def main():
     # BASELINE configs[3] across the job's GPUs (N=65536, one evaluation spread over all
     # ranks, panel broadcasts over RCCL): an extra line beside the replicas headline.
     dist_line = None
+    dist_expired = False
     if world > 1 and not args.no_dist:
         ctx.close()  # free the N=16384 workspace before the 65536 one
         single_lp = n65536["last_logpdf"] if n65536 else None
-        dist_line = measure_config3_dist(rank, world, local_rank, torch, dist, single_lp=single_lp)
+        dist_line, dist_expired = bounded_leg(
+            rank, lambda: measure_config3_dist(rank, world, local_rank, torch, dist, single_lp=single_lp),
+            args.dist_deadline, device=local_rank)
 
     total_evals = args.steps * world
     value = total_evals / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
     if rank != 0:
+        if dist_expired:
+            os._exit(4)  # the leg's collective never completed: do not wait for it
         if world > 1:
             dist.destroy_process_group()
         return
@@ -482,6 +555,9 @@ def main():
             print(f"bench: configs[3] distributed line FAILED: {why}", file=sys.stderr, flush=True)
             rc = 4
     print(json.dumps(out), flush=True)
+    if dist_expired:
+        sys.stderr.flush()
+        os._exit(rc)  # the leg's thread is still blocked in a collective: do not wait for it
     if world > 1:
         dist.destroy_process_group()
     return rc

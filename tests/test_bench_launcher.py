@@ -65,3 +65,29 @@ def test_launch_ranks_return_codes(monkeypatch):
     assert bench.launch_ranks(2, ["--gpus", "2", "--mode", "launcher-check"], need_gpus=False) == 0
     assert bench.launch_ranks(2, ["--gpus", "2", "--mode", "launcher-check", "--fail-rank", "0"],
                               need_gpus=False) == 3
+
+
+@pytest.mark.parametrize("hang_rank", [1, 0])
+def test_hung_dist_leg_prints_line_and_exits_4(hang_rank):
+    """VERDICT r05 #2b: a configs[3] leg that hangs (here: one rank never joins the leg's
+    collective) must end as a printed line with dist_ok false and status 4, well inside the
+    driver's limit, instead of a job killed with no line (bench.bounded_leg)."""
+    import time
+    t0 = time.perf_counter()
+    p = _run(["--gpus", "3", "--mode", "launcher-check", "--hang-rank", str(hang_rank), "--dist-deadline", "15"])
+    el = time.perf_counter() - t0
+    assert p.returncode == 4, (p.returncode, p.stderr[-2000:])
+    lines = [json.loads(s) for s in p.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = lines[0]
+    assert d["dist_ok"] is False
+    assert "deadline" in d["extra"]["dist"]["error"]
+    assert d["rank_sum"] == 3.0  # the rest of the line is intact
+    assert el < 200, el
+
+
+def test_dist_leg_ok_line():
+    p = _run(["--gpus", "2", "--mode", "launcher-check", "--dist-deadline", "60"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = [json.loads(s) for s in p.stdout.splitlines() if s.startswith("{")][0]
+    assert d["dist_ok"] is True and d["extra"]["dist"]["value"] == 2.0
