@@ -338,6 +338,11 @@ int accumulate_slots(gaplac_ctx* ctx, const std::vector<gaplac_ctx::Slot>& slots
         const KTime& t = ctx->hkt[i];
         if (t.end < t.start || t.start == ~0ull) continue;
         const double ms = (double)(t.end - t.start) * 1e-5;
+#if defined(GAPLAC_CLOCK) && GAPLAC_CLOCK
+        if (t.clk_rt > 0)  // diagnostic build: the clock each bulk launch held
+            std::fprintf(stderr, "clk slot %zu kind %d %.3f ms %.3f GHz\n", i, slots[i].kind, ms,
+                         (double)t.clk_mt / (double)t.clk_rt * 0.1);
+#endif
         t0 = std::min(t0, t.start);
         t1 = std::max(t1, t.end);
         switch (slots[i].kind) {
@@ -406,7 +411,14 @@ int accumulate_slots(gaplac_ctx* ctx, const std::vector<gaplac_ctx::Slot>& slots
 // the previous columns of its own super-panel). Columns of SP p+1 receive SP p-1 in
 // R(p-1) and SP p in the lookahead col_update; within a step the streams touch disjoint
 // tile columns. Events ping-pong (p & 1).
+// GAPLAC_CHAIN_SKIP (-D, timing diagnostics only: the result is void): 1 = the super-panel
+// chain's column updates, diagonal blocks and TRSMs are not launched, 2 = nor the
+// lookahead; what the evaluation costs without the chain's CU share and latency.
+#ifndef GAPLAC_CHAIN_SKIP
+#define GAPLAC_CHAIN_SKIP 0
+#endif
 int factor_superpanel(gaplac_ctx* ctx, hipStream_t sp, int64_t N, int64_t lda, int nt, int c0, int c1) {
+    if (GAPLAC_CHAIN_SKIP >= 1 && !ctx->dry) return 0;
     for (int c = c0; c < c1; ++c) {
         double* Acol = ctx->A + (int64_t)c * NB * lda;
         if (c > c0)
@@ -533,6 +545,13 @@ static bool pair_defer(const gaplac_ctx* ctx, const std::vector<int>& spc, int n
 // 65 all columns cost +4%, 40 of them +1.5%), else the last GAPLAC_QUAD_LAST.
 static int tail_quad_last(bool sim, int T) { return sim && T <= 40 ? TAIL_TMAX : GAPLAC_QUAD_LAST; }
 
+// Deep-task width of a single evaluation's tail: 4 columns (K = 512), or 8 (K = 1024) for
+// tails of at least GAPLAC_GW8_T tile columns (-D; A/B switch).
+#ifndef GAPLAC_GW8_T
+#define GAPLAC_GW8_T 1000
+#endif
+static int tail_gw(int T) { return T >= GAPLAC_GW8_T ? 8 : 4; }
+
 int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     hipStream_t sm = ctx->s_main;
     hipStream_t sp = ctx->serial ? sm : ctx->s_panel;
@@ -584,8 +603,9 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
                 HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_gram2, 0));  // rest of the Gram built
             const int c2 = spc[(size_t)p + 2];
             const int mla = nt - c1;
-            if (ctx->la_tiles_m > 0 && mla >= ctx->la_tiles_m && c2 - c1 == W && ctx->band_off.size() > (size_t)mla &&
-                !ctx->xr_mode) {
+            if (GAPLAC_CHAIN_SKIP >= 2 && !ctx->dry) {
+            } else if (ctx->la_tiles_m > 0 && mla >= ctx->la_tiles_m && c2 - c1 == W && ctx->band_off.size() > (size_t)mla &&
+                       !ctx->xr_mode) {
                 // the lookahead as whole 128x128 tiles (the band list of SP p+1's columns):
                 // less CU time than the quadrant kernel while the trailing matrix is large
                 BulkArgs ba{ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0},
@@ -703,14 +723,14 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             if (ctx->dry) {  // gaplac_plan_check: the task list's dependency order
                 std::vector<uint32_t> host;
                 const bool sim = (ctx->tail_sim > 0 || (ctx->tail_sim < 0 && T < 80)) && X == 0;
-                build_tail_tasks(T, host, nullptr, 4, 4, tail_quad_last(sim, T), false, GAPLAC_SINGLE_GROUP, X, sim ? 1 : 0);
+                build_tail_tasks(T, host, nullptr, tail_gw(T), 4, tail_quad_last(sim, T), false, GAPLAC_SINGLE_GROUP, X, sim ? 1 : 0);
                 std::string why;
                 if (!check_tail_tasks(T, host, &why, X)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
             }
             if ((ctx->ttasks_T != T || ctx->ttasks_X != X) && !ctx->dry) {
                 std::vector<uint32_t> host;
                 const bool sim = (ctx->tail_sim > 0 || (ctx->tail_sim < 0 && T < 80)) && X == 0;
-                build_tail_tasks(T, host, nullptr, 4, 4, tail_quad_last(sim, T), false, GAPLAC_SINGLE_GROUP, X, sim ? 1 : 0);
+                build_tail_tasks(T, host, nullptr, tail_gw(T), 4, tail_quad_last(sim, T), false, GAPLAC_SINGLE_GROUP, X, sim ? 1 : 0);
                 if (sim)
                     sim_order_tail_tasks(T, host, std::max(1, ctx->ncu / std::max(1, ctx->tail_share)));
                 int rc;

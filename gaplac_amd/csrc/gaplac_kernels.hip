@@ -1510,9 +1510,41 @@ __device__ __forceinline__ void tile_syrk_body(const BulkArgs& a, int b) {
 
 // One tile per workgroup, 189 VGPRs (208 with register staging): two resident bulk
 // workgroups leave 134 registers per SIMD lane, more than the 96 a quadrant chain kernel needs.
+// Diagnostic build only (-DGAPLAC_CLOCK=1): each workgroup of the bulk tile kernels adds
+// its shader cycles (s_memtime) and 100 MHz ticks (s_memrealtime) to its launch's KTime
+// slot; the host prints the clock held per launch (MI355X_MICROARCH.md 'DVFS give-back'
+// item 6). Never compiled into the library.
+#ifndef GAPLAC_CLOCK
+#define GAPLAC_CLOCK 0
+#endif
+struct ClkStamp {
+    unsigned long long mt = 0, rt = 0;
+    __device__ __forceinline__ void begin(const KTime* kt) {
+        if (GAPLAC_CLOCK && kt && threadIdx.x == 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            mt = __builtin_amdgcn_s_memtime();
+            rt = __builtin_amdgcn_s_memrealtime();
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    __device__ __forceinline__ void end(KTime* kt) {
+        if (GAPLAC_CLOCK && kt && threadIdx.x == 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            const unsigned long long m1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            atomicAdd(&kt->clk_mt, m1 - mt);
+            atomicAdd(&kt->clk_rt, r1 - rt);
+        }
+    }
+};
+
 __global__ __launch_bounds__(256, 2) void tile_syrk_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
+    ClkStamp ck;
+    ck.begin(kt);
     tile_syrk_body(a, (int)blockIdx.x);
+    ck.end(kt);
     kt_end(kt);
 }
 
@@ -1521,7 +1553,10 @@ __global__ __launch_bounds__(256, 2) void tile_syrk_kernel(BulkArgs a, KTime* __
 // bulk launches (tile_syrk_kernel, the roofline kernel) apart.
 __global__ __launch_bounds__(256, 2) void tile_band_kernel(BulkArgs a, KTime* __restrict__ kt) {
     kt_begin(kt);
+    ClkStamp ck;
+    ck.begin(kt);
     tile_syrk_body(a, (int)blockIdx.x);
+    ck.end(kt);
     kt_end(kt);
 }
 
@@ -1719,6 +1754,7 @@ __global__ void kt_reset_kernel(KTime* kt, int n) {
     if (i < n) {
         kt[i].start = ~0ull;
         kt[i].end = 0ull;
+        kt[i].clk_mt = kt[i].clk_rt = 0ull;
     }
 }
 
