@@ -30,6 +30,7 @@ struct gaplac_ctx {
     hipEvent_t ev_xinit = nullptr, ev_xdone = nullptr;
     hipEvent_t ev_xc[2] = {}, ev_xr[2] = {};  // extra rows: SP chain done (s_extra), SP rest done (s_xrest)
     hipEvent_t ev_P[2] = {}, ev_R[2] = {}, ev_gram = nullptr, ev_gram2 = nullptr;
+    hipEvent_t ev_split[2] = {}, ev_rest[2] = {};  // split bulk updates (factor_and_reduce), ping-pong
     double* A = nullptr;
     size_t A_elems = 0;
     double* Dinv = nullptr;  // per diagonal block: 8 inverses of its 16x16 sub-blocks
@@ -340,8 +341,9 @@ int accumulate_slots(gaplac_ctx* ctx, const std::vector<gaplac_ctx::Slot>& slots
         const double ms = (double)(t.end - t.start) * 1e-5;
 #if defined(GAPLAC_CLOCK) && GAPLAC_CLOCK
         if (t.clk_rt > 0)  // diagnostic build: the clock each bulk launch held
-            std::fprintf(stderr, "clk slot %zu kind %d %.3f ms %.3f GHz\n", i, slots[i].kind, ms,
-                         (double)t.clk_mt / (double)t.clk_rt * 0.1);
+            std::fprintf(stderr, "clk slot %zu kind %d %.3f ms %.3f GHz, %llu workgroups, %.0f cycles each\n", i,
+                         slots[i].kind, ms, (double)t.clk_mt / (double)t.clk_rt * 0.1, t.clk_n,
+                         (double)t.clk_mt / (double)std::max(1ull, t.clk_n));
 #endif
         t0 = std::min(t0, t.start);
         t1 = std::max(t1, t.end);
@@ -552,6 +554,29 @@ static int tail_quad_last(bool sim, int T) { return sim && T <= 40 ? TAIL_TMAX :
 #endif
 static int tail_gw(int T) { return T >= GAPLAC_GW8_T ? 8 : 4; }
 
+// Split bulk updates (GAPLAC_SPLIT, -D): plain evaluations whose
+// super-panel phase defers in pairs (depth 2); a triangle launch is split only when its
+// rest keeps at least SPLIT_REST_MIN tile columns.
+#ifndef GAPLAC_SPLIT
+#define GAPLAC_SPLIT 1
+#endif
+constexpr int SPLIT_REST_MIN = 16;
+#ifndef GAPLAC_SPLIT_MINCOLS
+#define GAPLAC_SPLIT_MINCOLS 32
+#endif
+#ifndef GAPLAC_SPLIT_DEPTH
+#define GAPLAC_SPLIT_DEPTH 2  // deferral depths the split applies to (the head is depth x W columns)
+#endif
+static bool split_wanted(const gaplac_ctx* ctx, int nt) {
+    const int depth = ctx->pair_depth > 0 ? ctx->pair_depth : nt >= 256 ? 4 : 2;
+    const std::vector<int> spc = superpanel_starts(ctx, nt);  // (a short super-panel phase: not worth it)
+    return GAPLAC_SPLIT && ctx->xr_mode == 0 && !ctx->serial && depth <= GAPLAC_SPLIT_DEPTH &&
+           !whole_in_tail(ctx, nt) && spc.back() >= GAPLAC_SPLIT_MINCOLS;
+}
+static bool split_bulk(const gaplac_ctx* ctx, int nt) {
+    return split_wanted(ctx, nt) && (ctx->s_xrest != nullptr || ctx->dry);
+}
+
 int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     hipStream_t sm = ctx->s_main;
     hipStream_t sp = ctx->serial ? sm : ctx->s_panel;
@@ -559,6 +584,20 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     const std::vector<int> spc = superpanel_starts(ctx, nt);
     const int nsp = (int)spc.size() - 1;
     int frc;
+    // Split bulk updates (split_bulk): a bulk update's first 2W tile columns
+    // (what the next steps' bands read) stay on s_main, the rest goes to s_xrest, so the
+    // next steps' small band launches run beside it instead of after it. rest_from: first
+    // tile column of the rest still in flight there; every later launch that reaches it
+    // waits for ev_rest first (on its own stream).
+    const bool split = split_bulk(ctx, nt);
+    hipStream_t sr = ctx->s_xrest;
+    int rest_from = nt + 1, nsplit = 0;
+    auto wait_rest = [&](hipStream_t st, int col_end) {
+        if (col_end <= rest_from) return 0;
+        HIPQ(ctx, hipStreamWaitEvent(st, ctx->ev_rest[(nsplit - 1) & 1], 0));
+        if (st == sm) rest_from = nt + 1;  // s_main is past it for good (s_panel waits behind s_main's marks)
+        return 0;
+    };
     if (nsp > 0) {
         HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_gram, 0));  // first W tile columns built
         if ((frc = factor_superpanel(ctx, sp, N, lda, nt, spc[0], spc[1]))) return frc;
@@ -567,8 +606,29 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
     // bulk trailing update of the triangle of tile columns >= j0 with the panel pn (K = kd)
     auto bulk_tri = [&](int j0, const Panel& pn, int kdep) -> int {
         if (j0 >= nt) return 0;
-        const int m = nt - j0;
-        BulkArgs ba{ctx->A, lda, pn, ctx->tiles + ctx->tile_off[(size_t)m], m * (m + 1) / 2, kdep, j0, j0,
+        wait_rest(sm, nt);
+        int jr = j0;  // first tile column of the triangle launch (after the head)
+        hipStream_t st = sm;
+        const int hw = (ctx->pair_depth > 0 ? ctx->pair_depth : nt >= 256 ? 4 : 2) * W;  // head width
+        if (split && nt - j0 >= hw + SPLIT_REST_MIN && ctx->band_off.size() > (size_t)(nt - j0)) {
+            // what s_main holds so far (this step's panel wait, earlier updates) before the rest
+            HIPQ(ctx, hipEventRecord(ctx->ev_split[nsplit & 1], sm));
+            // head: tile columns [j0, j0 + hw) as band launches (whole tiles) on s_main
+            for (int b0 = j0; b0 < j0 + hw; b0 += W) {
+                const int mbd = nt - b0;
+                BulkArgs bb{ctx->A, lda, pn, ctx->tiles + ctx->band_off[(size_t)mbd], W * mbd - W * (W - 1) / 2, kdep,
+                            b0, b0, ColMap{1, 0, W}};
+                bb.max_r = mbd - 1;
+                bb.max_c = W - 1;
+                bb.whole = 1;
+                launch_bulk(sm, bb, slot(ctx, 5, 0));
+            }
+            jr = j0 + hw;
+            st = sr;
+            HIPQ(ctx, hipStreamWaitEvent(sr, ctx->ev_split[nsplit & 1], 0));
+        }
+        const int m = nt - jr;
+        BulkArgs ba{ctx->A, lda, pn, ctx->tiles + ctx->tile_off[(size_t)m], m * (m + 1) / 2, kdep, jr, jr,
                     ColMap{1, 0, W}};
         const bool small = syrk_is_small(ba.ntiles);
         const double fl = syrk_flops(m) * (kdep / NB), by = syrk_bytes(m, kdep);
@@ -582,12 +642,17 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
                 HIPQ(ctx, hipEventCreate(&e));
                 ctx->evpool.push_back(e);
             }
-            HIPQ(ctx, hipEventRecord(ctx->evpool[e0], sm));
+            HIPQ(ctx, hipEventRecord(ctx->evpool[e0], st));
         }
-        launch_bulk(sm, ba, kt);
+        launch_bulk(st, ba, kt);
         if (ev) {
-            HIPQ(ctx, hipEventRecord(ctx->evpool[e0 + 1], sm));
+            HIPQ(ctx, hipEventRecord(ctx->evpool[e0 + 1], st));
             ctx->evpairs.push_back({e0, fl, by, 0});
+        }
+        if (st == sr) {
+            HIPQ(ctx, hipEventRecord(ctx->ev_rest[nsplit & 1], sr));
+            ++nsplit;
+            rest_from = jr;
         }
         return 0;
     };
@@ -602,6 +667,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             else
                 HIPQ(ctx, hipStreamWaitEvent(sp, ctx->ev_gram2, 0));  // rest of the Gram built
             const int c2 = spc[(size_t)p + 2];
+            wait_rest(sp, c2);  // (SP p+1's columns in a split update's rest still in flight)
             const int mla = nt - c1;
             if (GAPLAC_CHAIN_SKIP >= 2 && !ctx->dry) {
             } else if (ctx->la_tiles_m > 0 && mla >= ctx->la_tiles_m && c2 - c1 == W && ctx->band_off.size() > (size_t)mla &&
@@ -634,6 +700,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         // a band [b0, b1) with the panel columns pc .. c1-1
         auto band = [&](int b0, int b1, int pc) {
             if (b1 <= b0) return;
+            wait_rest(sm, b1);
             const Panel pn{ctx->A + (int64_t)pc * NB * lda, lda, 0};
             const int kb = (c1 - pc) * NB, mbd = nt - b0;
             if (b1 - b0 == W && ctx->band_off.size() > (size_t)mbd) {
@@ -707,6 +774,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             }
         }
     }
+    wait_rest(sm, nt);  // every split update's rest before the tail
     if (spc[(size_t)nsp] < nt) {
         const int ts = spc[(size_t)nsp], T = nt - ts;
         // the posterior's cross-covariance rows: factored along inside the tail
@@ -936,6 +1004,13 @@ int ensure_workspace(gaplac_ctx* ctx, int64_t N) {
     int rc;
     HIPCK(ctx, hipSetDevice(ctx->device));
     if ((rc = ensure(ctx, &ctx->A, &ctx->A_elems, (size_t)(Np + (int64_t)NB * ctx->xr_tiles) * Np))) return rc;
+    if (split_wanted(ctx, nt) && !ctx->s_xrest) {
+        // the split bulk updates' second stream (factor_and_reduce): the extra rows' stream
+        // of a gradient / posterior context, idle in a plain evaluation
+        int least = 0, greatest = 0;
+        HIPCK(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIPCK(ctx, hipStreamCreateWithPriority(&ctx->s_xrest, hipStreamNonBlocking, least));
+    }
     if (ctx->xr_mode && !ctx->s_extra) {
         // created on first use only: a plain logpdf context keeps two streams, so the
         // batch lanes (2 contexts) fit the 4 hardware queues a process gets by default. A
@@ -1400,7 +1475,14 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
         return fail("priority range", e);
     if ((e = hipStreamCreateWithPriority(&ctx->s_panel, hipStreamNonBlocking, greatest)) != hipSuccess)
         return fail("stream", e);
-    if ((e = hipStreamCreateWithPriority(&ctx->s_main, hipStreamNonBlocking, least)) != hipSuccess)
+    // s_main one level above the split updates' rest stream (s_xrest, least) where the
+    // device has three levels (MI355X: 1 / 0 / -1): the bands the chain waits for take the
+    // freed CU slots first (A/B switch GAPLAC_MAIN_MID)
+#ifndef GAPLAC_MAIN_MID
+#define GAPLAC_MAIN_MID 1
+#endif
+    const int main_prio = GAPLAC_MAIN_MID && least - greatest >= 2 ? least - 1 : least;
+    if ((e = hipStreamCreateWithPriority(&ctx->s_main, hipStreamNonBlocking, main_prio)) != hipSuccess)
         return fail("stream", e);
     for (int q = 0; q < 2; ++q) {
         if ((e = hipEventCreateWithFlags(&ctx->ev_P[q], hipEventDisableTiming)) != hipSuccess)
@@ -1414,6 +1496,12 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
     }
     if ((e = hipEventCreateWithFlags(&ctx->ev_gram, hipEventDisableTiming)) != hipSuccess)
         return fail("event", e);
+    for (int q = 0; q < 2; ++q) {
+        if ((e = hipEventCreateWithFlags(&ctx->ev_split[q], hipEventDisableTiming)) != hipSuccess)
+            return fail("event", e);
+        if ((e = hipEventCreateWithFlags(&ctx->ev_rest[q], hipEventDisableTiming)) != hipSuccess)
+            return fail("event", e);
+    }
     if ((e = hipEventCreateWithFlags(&ctx->ev_gram2, hipEventDisableTiming)) != hipSuccess)
         return fail("event", e);
     if ((e = hipEventCreateWithFlags(&ctx->ev_xinit, hipEventDisableTiming)) != hipSuccess)
@@ -1462,6 +1550,10 @@ int gaplac_ctx_destroy(gaplac_ctx* ctx) {
     }
     if (ctx->ev_gram) (void)hipEventDestroy(ctx->ev_gram);
     if (ctx->ev_gram2) (void)hipEventDestroy(ctx->ev_gram2);
+    for (int q = 0; q < 2; ++q) {
+        if (ctx->ev_split[q]) (void)hipEventDestroy(ctx->ev_split[q]);
+        if (ctx->ev_rest[q]) (void)hipEventDestroy(ctx->ev_rest[q]);
+    }
     if (ctx->ev_xinit) (void)hipEventDestroy(ctx->ev_xinit);
     if (ctx->ev_xdone) (void)hipEventDestroy(ctx->ev_xdone);
     if (ctx->A) (void)hipFree(ctx->A);

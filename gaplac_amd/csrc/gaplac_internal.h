@@ -45,7 +45,7 @@ struct KTime {
     unsigned long long end;    // max over waves (init 0)
     // diagnostic build only (-DGAPLAC_CLOCK): per-workgroup shader cycles and 100 MHz ticks
     // of the bulk tile kernels, summed (the clock the chip held: DESIGN.md §3.8)
-    unsigned long long clk_mt, clk_rt;
+    unsigned long long clk_mt, clk_rt, clk_n;
 };
 
 // Where global tile column bj of the lower triangle is stored. Single-GPU layout: the

@@ -1535,6 +1535,7 @@ struct ClkStamp {
             __builtin_amdgcn_s_waitcnt(0xC07F);
             atomicAdd(&kt->clk_mt, m1 - mt);
             atomicAdd(&kt->clk_rt, r1 - rt);
+            atomicAdd(&kt->clk_n, 1ull);
         }
     }
 };
@@ -1754,7 +1755,7 @@ __global__ void kt_reset_kernel(KTime* kt, int n) {
     if (i < n) {
         kt[i].start = ~0ull;
         kt[i].end = 0ull;
-        kt[i].clk_mt = kt[i].clk_rt = 0ull;
+        kt[i].clk_mt = kt[i].clk_rt = kt[i].clk_n = 0ull;
     }
 }
 

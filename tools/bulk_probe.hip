@@ -109,12 +109,14 @@ int main(int argc, char** argv) {
         KTime* dk;
         CK(hipMalloc(&dk, 3 * sizeof(KTime)));
         launch_kt_reset(0, dk, 3);
+        for (int r = 0; r < 30; ++r) launch_bulk(0, a, nullptr);  // the clock the sustained load holds
         for (int r = 0; r < 3; ++r) launch_bulk(0, a, dk + r);
         KTime hk[3];
         CK(hipMemcpy(hk, dk, sizeof hk, hipMemcpyDeviceToHost));
         for (int r = 0; r < 3; ++r)
-            printf("  clock launch %d: %.3f ms %.3f GHz\n", r, (hk[r].end - hk[r].start) * 1e-5,
-                   (double)hk[r].clk_mt / (double)hk[r].clk_rt * 0.1);
+            printf("  clock launch %d: %.3f ms %.3f GHz, %llu workgroups, %.0f cycles each\n", r,
+                   (hk[r].end - hk[r].start) * 1e-5, (double)hk[r].clk_mt / (double)hk[r].clk_rt * 0.1, hk[r].clk_n,
+                   (double)hk[r].clk_mt / (double)(hk[r].clk_n ? hk[r].clk_n : 1));
         CK(hipFree(dk));
     }
 #endif
