@@ -1475,14 +1475,7 @@ int gaplac_ctx_create(int device, gaplac_ctx** out) {
         return fail("priority range", e);
     if ((e = hipStreamCreateWithPriority(&ctx->s_panel, hipStreamNonBlocking, greatest)) != hipSuccess)
         return fail("stream", e);
-    // s_main one level above the split updates' rest stream (s_xrest, least) where the
-    // device has three levels (MI355X: 1 / 0 / -1): the bands the chain waits for take the
-    // freed CU slots first (A/B switch GAPLAC_MAIN_MID)
-#ifndef GAPLAC_MAIN_MID
-#define GAPLAC_MAIN_MID 1
-#endif
-    const int main_prio = GAPLAC_MAIN_MID && least - greatest >= 2 ? least - 1 : least;
-    if ((e = hipStreamCreateWithPriority(&ctx->s_main, hipStreamNonBlocking, main_prio)) != hipSuccess)
+    if ((e = hipStreamCreateWithPriority(&ctx->s_main, hipStreamNonBlocking, least)) != hipSuccess)
         return fail("stream", e);
     for (int q = 0; q < 2; ++q) {
         if ((e = hipEventCreateWithFlags(&ctx->ev_P[q], hipEventDisableTiming)) != hipSuccess)

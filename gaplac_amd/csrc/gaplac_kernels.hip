@@ -2056,11 +2056,16 @@ __device__ __forceinline__ double dk_ou(double p, double xi, double xj, const do
 // in place (wt = 2 off the diagonal, 1 on it, 0 outside the lower triangle / past N); then
 // one pass per term over the 64 weights of a lane, each term kind a loop of its own (the
 // code stays small: a fully unrolled term x element nest overflowed the instruction cache).
-// The k-loop's LDS staging buffer holds the tile's coordinates, alpha and the exp table
-// (checked for every GAPLAC_KB: with KB = 8 they fill it exactly); the per-wave sums have
-// their own small array.
+// The k-loop's LDS staging buffer holds the tile's coordinates, alpha, the exp table and the
+// per-wave sums (checked at compile time). With GAPLAC_KB = 8 the sums do not fit and get a
+// small array of their own; with the default KB = 16 they stay in the staging buffer (an
+// extra __shared__ array there cost the gradient 1.8 ms).
 static_assert(sizeof(MmaLds) >= (2 * GAPLAC_MAX_TERMS * NB + 2 * NB + 256) * sizeof(double),
               "cinv_contract_kernel's coordinates, alpha and exp table must fit the staging LDS");
+#if GAPLAC_KB == 16
+static_assert(sizeof(MmaLds) >= (2 * GAPLAC_MAX_TERMS * NB + 2 * NB + 256 + 4 * (GAPLAC_MAX_TERMS + 1)) * sizeof(double),
+              "cinv_contract_kernel's per-wave sums must fit the staging LDS");
+#endif
 __global__ __launch_bounds__(256, 2) void cinv_contract_kernel(const double* __restrict__ A, int64_t lda, int64_t Np,
                                                                int64_t N, const double* __restrict__ X, int64_t ldx,
                                                                const double* __restrict__ alpha,
@@ -2093,7 +2098,11 @@ __global__ __launch_bounds__(256, 2) void cinv_contract_kernel(const double* __r
         double* const ar = xc + GAPLAC_MAX_TERMS * NB;  // alpha of the rows, then of the columns
         double* const ac = ar + NB;
         double* const tbl = ac + NB;                    // exp table
-        __shared__ double red[4 * (GAPLAC_MAX_TERMS + 1)];  // red[w * (T + 1) + t]
+#if GAPLAC_KB == 16
+        double* const red = tbl + 256;  // red[w * (T + 1) + t]
+#else
+        __shared__ double red[4 * (GAPLAC_MAX_TERMS + 1)];
+#endif
         const int64_t r0 = (int64_t)I * NB, c0 = (int64_t)J * NB;
         for (int idx = tid; idx < T * NB; idx += 256) {
             const int t = idx / NB, q = idx % NB;
