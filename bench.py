@@ -463,7 +463,10 @@ def main():
         traffic, traffic_src = load_traffic()
         roofline = {
             "bound": "mfma",
-            "kernel": "tile_syrk_kernel (bulk trailing update, 128x128 tiles, K=512 or 1024 (paired), LDS-DMA staged, fp64 MFMA 16x16x4)",
+            "kernel": "tile_syrk_kernel (bulk trailing update, 128x128 tiles, K=512 or 1024 (paired), LDS-DMA staged, "
+                      "fp64 MFMA 16x16x4); since round 6 each triangle launch runs beside the next steps' band launches "
+                      "(split bulk updates, DESIGN.md §3.8), so its launch time includes the GPU share the bands take: "
+                      "bulk_phase below is the same code's throughput over the time it is in flight",
             "achieved": round(achieved, 3),
             "peak": PEAK_F64_TFLOPS,
             "unit": "TFLOP/s",
@@ -474,10 +477,19 @@ def main():
             "flops_per_launch": flops_per_launch,
             "avg_launch_ms": st_ev["syrk_ms"] / st_ev["syrk_launches"],
             "launches": st_ev["syrk_launches"],
-            "timing": "hipEvents recorded on the launching stream (s_main) around every tile_syrk_kernel launch, "
+            "timing": "hipEvents recorded on the launching stream around every tile_syrk_kernel launch, "
                       "in a pass of the same steps right after the (uninstrumented) timed region; cf. "
                       "profiles/*kernel_stats.csv (rocprofv3 --kernel-trace --stats of the same command)",
         }
+        if st_ev.get("bulk_union_ms", 0) > 0:
+            bph = st_ev["bulk_flops"] / (st_ev["bulk_union_ms"] / 1e3) / 1e12
+            roofline["bulk_phase"] = {
+                "kernels": "tile_syrk_kernel + tile_band_kernel (the same tile_syrk_body: triangle updates, bands, "
+                           "split heads, whole-tile lookaheads) over the super-panel phase",
+                "achieved": round(bph, 3), "frac": round(bph / PEAK_F64_TFLOPS, 4),
+                "flops": st_ev["bulk_flops"], "launches": st_ev["bulk_launches"],
+                "union_ms": st_ev["bulk_union_ms"],
+                "timing": "union of the launches' hipEvent intervals (each on its own stream), same pass"}
     eval_flops = N ** 3 / 3.0 + N ** 2
     eval_tflops = eval_flops * (value / world) / 1e12
     extra = {

@@ -99,6 +99,9 @@ class Stats(ctypes.Structure):
         ("contract_ms", c_double),
         ("tail_launches", c_int64),
         ("tail_ms", c_double),
+        ("bulk_flops", c_double),
+        ("bulk_launches", c_int64),
+        ("bulk_union_ms", c_double),
     ]
 
 

@@ -330,6 +330,14 @@ double syrk_bytes(int m, int kd) {
     return tiles * NB * NB * 8.0 * 2.0 + (double)m * NB * kd * 8.0;
 }
 
+// Algorithmic flops of a band launch: the W tile columns of an mbd-row trailing matrix
+// (rows r >= c), K = kd: W diagonal tiles (lower triangle incl. diagonal), the rest whole.
+double band_flops(int mbd, int W, int kd) {
+    const int w = std::min(W, mbd);
+    const double tiles = (double)w * mbd - (double)w * (w - 1) / 2.0;
+    return (tiles - w) * 2.0 * NB * NB * kd + (double)w * NB * (NB + 1) * kd;
+}
+
 // Fold the device timestamps of the given slots into ctx->stats (ticks: 100 MHz).
 int accumulate_slots(gaplac_ctx* ctx, const std::vector<gaplac_ctx::Slot>& slots) {
     if (slots.empty()) return 0;
@@ -603,6 +611,27 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
         if ((frc = factor_superpanel(ctx, sp, N, lda, nt, spc[0], spc[1]))) return frc;
         HIPQ(ctx, hipEventRecord(ctx->ev_P[0], sp));
     }
+    // profiling mode 2: hipEvents around a band-type bulk launch (whole-tile bands, heads and
+    // lookaheads: kind 5) on its stream, for the bulk phase's union of launch intervals
+    auto band_launch = [&](hipStream_t st, const BulkArgs& bb, int mbd) {
+        const bool ev = ctx->prof_mode == 2 && bb.whole && !ctx->xr_mode;
+        size_t e0 = 0;
+        if (ev) {
+            e0 = 2 * ctx->evpairs.size();
+            while (ctx->evpool.size() < e0 + 2) {
+                hipEvent_t e;
+                HIPQ(ctx, hipEventCreate(&e));
+                ctx->evpool.push_back(e);
+            }
+            HIPQ(ctx, hipEventRecord(ctx->evpool[e0], st));
+        }
+        launch_bulk(st, bb, slot(ctx, 5, 0));
+        if (ev) {
+            HIPQ(ctx, hipEventRecord(ctx->evpool[e0 + 1], st));
+            ctx->evpairs.push_back({e0, band_flops(mbd, W, bb.kdepth), 0.0, 5});
+        }
+        return 0;
+    };
     // bulk trailing update of the triangle of tile columns >= j0 with the panel pn (K = kd)
     auto bulk_tri = [&](int j0, const Panel& pn, int kdep) -> int {
         if (j0 >= nt) return 0;
@@ -621,7 +650,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
                 bb.max_r = mbd - 1;
                 bb.max_c = W - 1;
                 bb.whole = 1;
-                launch_bulk(sm, bb, slot(ctx, 5, 0));
+                band_launch(sm, bb, mbd);
             }
             jr = j0 + hw;
             st = sr;
@@ -680,7 +709,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
                 ba.max_r = mla - 1;
                 ba.max_c = W - 1;
                 ba.whole = 1;
-                launch_bulk(sp, ba, slot(ctx, 5, 0));
+                band_launch(sp, ba, mla);
             } else {
                 launch_col_update(sp, ctx->A, lda, Panel{ctx->A + (int64_t)c0 * NB * lda, lda, 0}, nt, c1, c1,
                                   c2 - c1, kd, slot(ctx, 5, 0));
@@ -710,7 +739,7 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
                 ba.max_r = mbd - 1;
                 ba.max_c = W - 1;
                 ba.whole = mbd >= ctx->band_tiles_m ? 1 : 0;
-                launch_bulk(sm, ba, slot(ctx, 5, 0));
+                band_launch(sm, ba, mbd);
             } else {
                 launch_col_update(sm, ctx->A, lda, pn, nt, b0, b0, b1 - b0, kb, slot(ctx, 5, 0));
             }
@@ -2218,7 +2247,9 @@ int gaplac_get_stats(gaplac_ctx* ctx, gaplac_stats* out) {
     if (!ctx || !out) return GAPLAC_E_ARG;
     if (!ctx->evpairs.empty()) {  // fold the event-timed bulk launches in
         HIPCK(ctx, hipSetDevice(ctx->device));
-        HIPCK(ctx, hipStreamSynchronize(ctx->s_main));
+        HIPCK(ctx, hipDeviceSynchronize());  // (events on s_main, s_panel and the split's s_xrest)
+        std::vector<std::pair<double, double>> iv;  // bulk-type launch intervals, ms after the first event
+        const hipEvent_t ref = ctx->evpool[ctx->evpairs.front().i0];
         for (const auto& p : ctx->evpairs) {
             float ms = 0.f;
             HIPCK(ctx, hipEventElapsedTime(&ms, ctx->evpool[p.i0], ctx->evpool[p.i0 + 1]));
@@ -2227,11 +2258,30 @@ int gaplac_get_stats(gaplac_ctx* ctx, gaplac_stats* out) {
                 ctx->stats.cinv_launches += 1;
                 continue;
             }
+            float t0 = 0.f;
+            HIPCK(ctx, hipEventElapsedTime(&t0, ref, ctx->evpool[p.i0]));
+            iv.push_back({(double)t0, (double)t0 + ms});
+            ctx->stats.bulk_flops += p.flops;
+            ctx->stats.bulk_launches += 1;
+            if (p.kind == 5) continue;  // bands, heads, lookaheads: the union only
             ctx->stats.syrk_ms += ms;
             ctx->stats.syrk_flops += p.flops;
             ctx->stats.syrk_bytes += p.bytes;
             ctx->stats.syrk_launches += 1;
         }
+        // union of the intervals: the time some bulk-type launch was in flight
+        std::sort(iv.begin(), iv.end());
+        double cs = -1.0, ce = -1.0;
+        for (const auto& x : iv) {
+            if (x.first > ce) {
+                if (ce > cs) ctx->stats.bulk_union_ms += ce - cs;
+                cs = x.first;
+                ce = x.second;
+            } else {
+                ce = std::max(ce, x.second);
+            }
+        }
+        if (ce > cs) ctx->stats.bulk_union_ms += ce - cs;
         ctx->evpairs.clear();
     }
     *out = ctx->stats;

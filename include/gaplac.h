@@ -216,6 +216,12 @@ typedef struct gaplac_stats {
     /* persistent tail (tail_kernel: the last tile columns as one dataflow launch) */
     int64_t tail_launches;
     double  tail_ms;
+    /* profiling mode 2: every bulk-type launch of the super-panel phase (triangle updates,
+       bands, split heads, whole-tile lookaheads; they overlap since round 6): summed
+       algorithmic flops, launches, and the union of their event intervals */
+    double  bulk_flops;
+    int64_t bulk_launches;
+    double  bulk_union_ms;
 } gaplac_stats;
 int gaplac_set_profiling(gaplac_ctx* ctx, int mode);
 int gaplac_get_stats(gaplac_ctx* ctx, gaplac_stats* out);

@@ -81,3 +81,24 @@ def test_grad_unfused(base, N):
     scale = np.abs(dp).max() + 1.0
     assert np.max(np.abs(np.asarray(dp2) - np.asarray(dp))) <= 1e-10 * scale, (dp2, dp)
     assert abs(dn2 - dn) <= 1e-10 * (abs(dn) + 1.0), (dn2, dn)
+
+
+def test_split_bulk_profiling_stats(base):
+    """Profiling mode 2 with the split bulk updates: the triangle launches
+    (syrk_*) and every bulk-type launch of the super-panel phase (bulk_*, overlapping since
+    the split) are event-timed; the union of their intervals is at most their summed time
+    and at least the longest launch, and the evaluation is unchanged by the events."""
+    N = 16384
+    X, v = inputs(N, seed=6)
+    ref = base.logpdf(X, TERMS, 0.1, v, full=True)
+    base.reset_stats()
+    base.set_profiling(2)
+    got = base.logpdf(X, TERMS, 0.1, v, full=True)
+    base.set_profiling(0)
+    st = base.stats()
+    base.reset_stats()
+    assert got == ref
+    assert st["syrk_launches"] > 0 and st["bulk_launches"] > st["syrk_launches"]
+    assert st["bulk_flops"] > st["syrk_flops"] > 0
+    assert 0 < st["bulk_union_ms"] < 40.0
+    assert st["bulk_union_ms"] >= st["syrk_ms"] / st["syrk_launches"]
