@@ -604,12 +604,12 @@ def measure_config1(ctx, torch, steps: int = 8):
                          "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / PEAK_F64_TFLOPS, 4)}}
 
 
-def measure_config3_single(local_rank: int, torch, steps: int = 2):
+def measure_config3_single(local_rank: int, torch, steps: int = 2, inputs=None):
     """BASELINE configs[3]'s workload (SqExp(:x; l=1.5), N=65536, seed 3) as ONE evaluation
     on ONE GPU: the north_star's 64k point and the 1-GPU base of the configs[3]
     strong-scaling curve. Its own context (34 GB workspace), freed afterwards."""
     from gaplac_amd.backend import Context
-    x, v = CF.config3_inputs()
+    x, v = CF.config3_inputs() if inputs is None else inputs
     N = x.shape[0]
     dx = torch.from_numpy(x).to("cuda")
     dvv = torch.from_numpy(v).to("cuda")
@@ -684,7 +684,7 @@ def measure_config4(local_rank: int, torch, steps: int = 2):
 
 
 def measure_config3_dist(rank: int, world: int, local_rank: int, torch, dist, steps: int = 3,
-                         single_lp: float | None = None):
+                         single_lp: float | None = None, inputs=None):
     """BASELINE configs[3]: SqExp(:x; l=1.5), N=65536, one evaluation over all ranks of the
     job (1-D block-column cyclic Cholesky, panel broadcasts with RCCL over xGMI,
     gaplac_amd/distributed.py). Strong scaling: the work per evaluation is fixed.
@@ -693,23 +693,23 @@ def measure_config3_dist(rank: int, world: int, local_rank: int, torch, dist, st
     input (single_lp, or one evaluated here): parity_vs_single, bar DIST_PARITY_BAR.
     A failure on another rank raises (the launcher then stops the job, non-zero)."""
     try:
-        line = _config3_dist(rank, world, local_rank, torch, dist, steps)
+        line = _config3_dist(rank, world, local_rank, torch, dist, steps, inputs)
     except Exception as e:
         if rank != 0:
             raise
         return {"error": repr(e)[:400]}
     if rank == 0:
         if single_lp is None:
-            single_lp = measure_config3_single(local_rank, torch, steps=1)["last_logpdf"]
+            single_lp = measure_config3_single(local_rank, torch, steps=1, inputs=inputs)["last_logpdf"]
         rel = abs(line["last_logpdf"] - single_lp) / abs(single_lp)
         line.update(single_gpu_logpdf=single_lp, parity_vs_single=rel, parity_bar=DIST_PARITY_BAR,
                     parity_ok=bool(rel <= DIST_PARITY_BAR))
     return line
 
 
-def _config3_dist(rank: int, world: int, local_rank: int, torch, dist, steps: int):
+def _config3_dist(rank: int, world: int, local_rank: int, torch, dist, steps: int, inputs=None):
     from gaplac_amd import distributed as DI
-    x, v = CF.config3_inputs()
+    x, v = CF.config3_inputs() if inputs is None else inputs  # (inputs: tests, a smaller N)
     N = x.shape[0]
     dx = torch.from_numpy(x).to("cuda")
     dvv = torch.from_numpy(v).to("cuda")
