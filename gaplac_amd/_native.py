@@ -60,9 +60,18 @@ EXPORTED = (
     "gaplac_dist_comm_end_chunk",
     "gaplac_dist_plan_check",
     "gaplac_dist_plan",
+    "gaplac_dist_set_tail",
+    "gaplac_dist_tail_geometry",
+    "gaplac_dist_set_tail_buffer",
+    "gaplac_dist_tail_segment",
+    "gaplac_dist_tail_begin",
+    "gaplac_dist_tail_end",
+    "gaplac_dist_plan_check_tail",
+    "gaplac_dist_plan_tail",
     "gaplac_dist_replay_enable",
     "gaplac_dist_replay_chunk",
     "gaplac_dist_replay_stamps",
+    "gaplac_dist_replay_tail",
     "gaplac_dist_replay_info",
 )
 
@@ -172,10 +181,19 @@ def load() -> ctypes.CDLL:
     lib.gaplac_dist_comm_end_chunk.argtypes = [c_void_p, c_int32, c_int32]
     lib.gaplac_dist_plan_check.argtypes = [c_int32, c_int32, c_int32, c_int32, _I64P, c_char_p, c_int64]
     lib.gaplac_dist_plan.argtypes = [c_int32, c_int32, c_int32, c_int32, _I32P, c_int64, _I64P]
+    lib.gaplac_dist_set_tail.argtypes = [c_void_p, c_int32, c_int32]
+    lib.gaplac_dist_tail_geometry.argtypes = [c_void_p, c_int64, _I32P, _I64P, _I32P]
+    lib.gaplac_dist_set_tail_buffer.argtypes = [c_void_p, c_void_p, c_int64]
+    lib.gaplac_dist_tail_segment.argtypes = [c_void_p, c_int32, _VPP, _I64P, _I32P]
+    lib.gaplac_dist_tail_begin.argtypes = [c_void_p, _VPP]
+    lib.gaplac_dist_tail_end.argtypes = [c_void_p]
+    lib.gaplac_dist_plan_check_tail.argtypes = [c_int32, c_int32, c_int32, c_int32, c_int32, _I64P, c_char_p, c_int64]
+    lib.gaplac_dist_plan_tail.argtypes = [c_int32, c_int32, c_int32, c_int32, c_int32, _I32P, c_int64, _I64P]
     lib.gaplac_dist_replay_enable.argtypes = [c_void_p, c_int64]
     lib.gaplac_dist_replay_chunk.argtypes = [c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int64, c_int64,
                                              c_int64, c_int64]
     lib.gaplac_dist_replay_stamps.argtypes = [c_void_p, c_void_p, c_int64]
+    lib.gaplac_dist_replay_tail.argtypes = [c_void_p, c_void_p, c_int32, c_int64, c_double, c_int64]
     lib.gaplac_dist_replay_info.argtypes = [c_void_p, c_int32, c_int32, _I64P, _I32P, _I32P]
     for name in EXPORTED:
         getattr(lib, name).restype = getattr(lib, name).restype or c_int

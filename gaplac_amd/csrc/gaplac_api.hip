@@ -562,6 +562,20 @@ static int tail_quad_last(bool sim, int T) { return sim && T <= 40 ? TAIL_TMAX :
 #endif
 static int tail_gw(int T) { return T >= GAPLAC_GW8_T ? 8 : 4; }
 
+}  // namespace
+namespace gaplac {
+// The single-evaluation tail list of T tile columns (X extra tile rows), as eval_device
+// launches it; also the distributed root's gathered tail (gaplac_dist.hip). tail_sim as
+// gaplac_ctx::tail_sim; workers: the persistent grid the simulated order plans for.
+void build_single_tail_list(int T, int X, int tail_sim, int workers, std::vector<uint32_t>& out) {
+    const bool sim = (tail_sim > 0 || (tail_sim < 0 && T < 80)) && X == 0;
+    out.clear();
+    build_tail_tasks(T, out, nullptr, tail_gw(T), 4, tail_quad_last(sim, T), false, GAPLAC_SINGLE_GROUP, X, sim ? 1 : 0);
+    if (sim && workers > 0) sim_order_tail_tasks(T, out, workers);
+}
+}  // namespace gaplac
+namespace {
+
 // Split bulk updates (GAPLAC_SPLIT, -D): plain evaluations whose
 // super-panel phase defers in pairs (depth 2); a triangle launch is split only when its
 // rest keeps at least SPLIT_REST_MIN tile columns.
@@ -819,17 +833,13 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
             }
             if (ctx->dry) {  // gaplac_plan_check: the task list's dependency order
                 std::vector<uint32_t> host;
-                const bool sim = (ctx->tail_sim > 0 || (ctx->tail_sim < 0 && T < 80)) && X == 0;
-                build_tail_tasks(T, host, nullptr, tail_gw(T), 4, tail_quad_last(sim, T), false, GAPLAC_SINGLE_GROUP, X, sim ? 1 : 0);
+                build_single_tail_list(T, X, ctx->tail_sim, 0, host);
                 std::string why;
                 if (!check_tail_tasks(T, host, &why, X)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
             }
             if ((ctx->ttasks_T != T || ctx->ttasks_X != X) && !ctx->dry) {
                 std::vector<uint32_t> host;
-                const bool sim = (ctx->tail_sim > 0 || (ctx->tail_sim < 0 && T < 80)) && X == 0;
-                build_tail_tasks(T, host, nullptr, tail_gw(T), 4, tail_quad_last(sim, T), false, GAPLAC_SINGLE_GROUP, X, sim ? 1 : 0);
-                if (sim)
-                    sim_order_tail_tasks(T, host, std::max(1, ctx->ncu / std::max(1, ctx->tail_share)));
+                build_single_tail_list(T, X, ctx->tail_sim, std::max(1, ctx->ncu / std::max(1, ctx->tail_share)), host);
                 int rc;
                 if ((rc = ensure(ctx, &ctx->ttasks, &ctx->ttasks_elems, host.size()))) return rc;
                 HIPCK(ctx, hipMemcpy(ctx->ttasks, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));

@@ -69,6 +69,10 @@ struct DOp {
 // s: UPD(s) update(s) started, BAND(s) SP s+2 up to date in update(s), END(s) update(s)
 // done, PACK(s, c) chunk c packed, RECV(s, c) chunk c received (sent, on its owner).
 constexpr int ST_PER_STEP = 3 + 2 * MAXC;
+// after the nsp steps' stamps: the end of the rank's Gram, the tail gather's modelled
+// arrival (gaplac_dist_replay_tail), the end of the root's tail, the end of the replay's
+// copies of the gathered segments
+constexpr int ST_EXTRA = 4;
 inline int st_upd(int s) { return s * ST_PER_STEP; }
 inline int st_band(int s) { return s * ST_PER_STEP + 1; }
 inline int st_end(int s) { return s * ST_PER_STEP + 2; }
@@ -105,9 +109,33 @@ struct gaplac_dist {
     // geometry of the current evaluation
     int64_t N = -1, Np = 0;
     int nt = 0, nsp = 0, nloc = 0;
+    int nsteps = 0;  // distributed steps (nsp, or tstop with the tail gather)
     bool factored_any = false;
     std::vector<std::vector<DOp>> plan;
-    int plan_nt = -1;
+    int plan_nt = -1, plan_stop = -1;
+    // tail gather (gaplac_dist_set_tail): SPs tstop .. nsp-1 (the last
+    // <= tail_cols tile columns) are factored by rank tail_root's persistent tail after every
+    // rank sent it its columns of the trailing matrix (rows and columns >= tN0 = 128 W tstop)
+    int tail_cols = 0, tail_root = 0;
+    int tstop = -1;  // -1: no gather this evaluation
+    int64_t tN0 = 0, tNt = 0;
+    std::vector<int64_t> tseg_off, tseg_cnt;  // per segment (SP tstop + i) in this rank's segment buffer; 0: none
+    double* tseg = nullptr;   // segment buffer: a sender's own segments, or every segment on the root
+    size_t tseg_cap = 0;
+    bool tseg_external = false;
+    double* tmat = nullptr;   // root: the trailing matrix, tNt x tNt column-major
+    size_t tmat_elems = 0;
+    double* tDinv = nullptr;
+    size_t tDinv_elems = 0;
+    EvalResult* tres = nullptr;  // root: the tail's result (pivot indices relative to tN0)
+    EvalResult* htres = nullptr; // pinned
+    TailCtl* tctl = nullptr;
+    uint32_t* ttasks = nullptr;
+    size_t ttasks_elems = 0;
+    int ttasks_n = 0, ttasks_T = -1;
+    int ncu = 256;
+    bool tail_ended = false;
+    hipEvent_t ev_tail = nullptr;  // s_main: the last update done; s_comm: the gather's transfers enqueued
     int held_step = -1;   // alone: the step whose ops after its mark wait for the next update
     size_t held_from = 0;
     // device buffers
@@ -180,17 +208,22 @@ int dgrow(gaplac_dist* d, T** p, size_t* cap, size_t n) {
 // Does step p defer (only the bands of SPs p+2, p+3 get the group's panels)? Groups are
 // aligned (a deferral starts at a group's first step and ends at its last one at the
 // latest); pend: the group's first panel while a deferral runs, -1 otherwise.
-bool defers(int p, int pend, int nsp, int nt, int W, int D, int pair_m) {
-    if (D < 2 || pair_m <= 0 || p + 4 > nsp || nt - (p + 4) * W < pair_m) return false;
+// stop < nsp (tail gather, gaplac_dist_set_tail): steps stop .. nsp-1 never run, so step
+// stop-1 closes any open group.
+bool defers(int p, int pend, int nsp, int nt, int W, int D, int pair_m, int stop) {
+    if (D < 2 || pair_m <= 0 || p + 4 > nsp || nt - (p + 4) * W < pair_m || p + 1 >= stop) return false;
     return pend < 0 ? p % D == 0 : p % D != D - 1;
 }
 
-std::vector<std::vector<DOp>> build_plan(int nsp, int nt, int W, int D, int pair_m) {
-    std::vector<std::vector<DOp>> plan((size_t)std::max(nsp, 0));
+// Steps 0 .. stop-1 (stop = nsp: all of them). With stop < nsp (the tail gather) the last
+// step also applies its panel to SP stop, in place of factor(stop)'s lookahead, so that
+// every SP >= stop ends with panels 0 .. stop-1: the trailing matrix the gather moves.
+std::vector<std::vector<DOp>> build_plan(int nsp, int nt, int W, int D, int pair_m, int stop) {
+    std::vector<std::vector<DOp>> plan((size_t)std::max(stop, 0));
     int pend = -1, dcol = nsp;  // SPs >= dcol lack every panel from pend on
-    for (int p = 0; p < nsp; ++p) {
+    for (int p = 0; p < stop; ++p) {
         std::vector<DOp>& ops = plan[(size_t)p];
-        const bool defer = defers(p, pend, nsp, nt, W, D, pair_m);
+        const bool defer = defers(p, pend, nsp, nt, W, D, pair_m, stop);
         auto first = [&](int g) { return pend >= 0 && g >= dcol ? pend : p; };
         if (p + 2 < nsp) ops.push_back({OP_BAND, p + 2, first(p + 2), p});
         ops.push_back({OP_MARK, p + 2, p, p});
@@ -206,14 +239,16 @@ std::vector<std::vector<DOp>> build_plan(int nsp, int nt, int W, int D, int pair
         } else if (p + 3 < nsp) {
             ops.push_back({OP_SUF, p + 3, p, p});
         }
+        if (p + 1 == stop && stop < nsp) ops.push_back({OP_BAND, p + 1, p, p});
     }
     return plan;
 }
 
 // Every SP g gets panels 0 .. g-1 exactly once and in order (the update ops of steps
 // <= g-2, before step g-2's mark, then the lookahead with panel g-1 in factor(g)); every op
-// of step p reads panels of p's group only, ending at p.
-bool check_plan(const std::vector<std::vector<DOp>>& plan, int nsp, int D, std::string* why) {
+// of step p reads panels of p's group only, ending at p. With stop < nsp: every SP >= stop
+// ends with panels 0 .. stop-1 (SP stop gets panel stop-1 from the last step's own band).
+bool check_plan(const std::vector<std::vector<DOp>>& plan, int nsp, int D, int stop, std::string* why) {
     std::vector<int> next((size_t)nsp, 0);  // next panel SP g must receive
     char buf[256];
     auto fail = [&](const char* fmt, int a, int b, int c) {
@@ -223,7 +258,8 @@ bool check_plan(const std::vector<std::vector<DOp>>& plan, int nsp, int D, std::
         }
         return false;
     };
-    for (int p = 0; p < nsp; ++p) {
+    if ((int)plan.size() != stop || stop < 1 || stop > nsp) return fail("plan of %d steps for stop %d of %d", (int)plan.size(), stop, nsp);
+    for (int p = 0; p < stop; ++p) {
         bool marked = false;
         for (const DOp& op : plan[(size_t)p]) {
             if (op.kind == OP_MARK) {
@@ -235,7 +271,8 @@ bool check_plan(const std::vector<std::vector<DOp>>& plan, int nsp, int D, std::
                 return fail("step %d reads panels %d..%d", p, op.pf, op.pl);
             const int g1 = op.kind == OP_BAND ? op.g + 1 : nsp;
             for (int g = op.g; g < g1; ++g) {
-                if (g <= p + 1) return fail("step %d updates SP %d (not after its lookahead) %d", p, g, 0);
+                const bool last_band = p + 1 == stop && stop < nsp && g == p + 1 && op.kind == OP_BAND && op.pf == p;
+                if (g <= p + 1 && !last_band) return fail("step %d updates SP %d (not after its lookahead) %d", p, g, 0);
                 if (g == p + 2 && marked) return fail("step %d updates SP %d after the mark%d", p, g, 0);
                 if (next[(size_t)g] != op.pf) return fail("SP %d gets panel %d, expected %d", g, op.pf, next[(size_t)g]);
                 next[(size_t)g] = op.pl + 1;
@@ -243,14 +280,14 @@ bool check_plan(const std::vector<std::vector<DOp>>& plan, int nsp, int D, std::
         }
         if (!marked) return fail("step %d has no mark%d%d", p, 0, 0);
         // factor(p+1): the lookahead applies panel p to SP p+1
-        if (p + 1 < nsp) {
+        if (p + 1 < stop) {
             if (next[(size_t)p + 1] != p) return fail("SP %d reaches its chain with panels < %d, needs %d", p + 1,
                                                       next[(size_t)p + 1], p);
             next[(size_t)p + 1] = p + 1;
         }
     }
     for (int g = 0; g < nsp; ++g)
-        if (next[(size_t)g] != g) return fail("SP %d ends with panels < %d%d", g, next[(size_t)g], 0);
+        if (next[(size_t)g] != std::min(g, stop)) return fail("SP %d ends with panels < %d%d", g, next[(size_t)g], 0);
     return true;
 }
 
@@ -288,6 +325,42 @@ int64_t chunk_count(const gaplac_dist* d, int s, int c) {
 }
 int64_t chunk_bytes_useful(const gaplac_dist* d, int s, int c) {  // rows >= the panel's first row only
     return (int64_t)chunk_cols(d, s, c) * NB * (d->Np - panel_row0(d, s)) * 8;
+}
+
+// ---- tail gather geometry ----
+// The first gathered SP for nt tile columns: the first SP whose columns all lie in the last
+// tail_cols; -1: no gather (off, or not even one distributed step would remain).
+int tail_stop_of(int nt, int W, int tail_cols) {
+    const int nsp = (nt + W - 1) / W;
+    if (tail_cols <= 0 || nt <= tail_cols) return -1;
+    const int s = (nt - tail_cols + W - 1) / W;
+    return s >= 1 && s < nsp ? s : -1;
+}
+int tail_stop(const gaplac_dist* d, int nt, int /*nsp*/) { return tail_stop_of(nt, d->W, d->tail_cols); }
+// Segment i of the gather is SP stop + i: its columns from the SP's first row down (the rows
+// above it are the trailing matrix's upper triangle), column-major with ld = rows. A rank's
+// segment buffer holds the segments it sends (the SPs it owns), the root's every segment.
+struct TailGeom {
+    int stop = -1;
+    int64_t N0 = 0, Nt = 0, elems = 0;
+    std::vector<int64_t> off, cnt;  // per segment in this rank's buffer (cnt 0: not on this rank)
+};
+int64_t tseg_rows(int64_t Nt, int W, int i) { return Nt - (int64_t)i * W * NB; }
+TailGeom tail_geom(const gaplac_dist* d, int nt, int nsp, int64_t Np) {
+    TailGeom g;
+    g.stop = tail_stop(d, nt, nsp);
+    if (g.stop < 0) return g;
+    g.N0 = (int64_t)g.stop * d->W * NB;
+    g.Nt = Np - g.N0;
+    for (int s = g.stop; s < nsp; ++s) {
+        const int i = s - g.stop;
+        const bool here = d->rank == d->tail_root || s % d->nranks == d->rank;
+        const int64_t c = (int64_t)std::min(d->W, nt - s * d->W) * NB * tseg_rows(g.Nt, d->W, i);
+        g.off.push_back(here ? g.elems : 0);
+        g.cnt.push_back(here ? c : 0);
+        if (here) g.elems += c;
+    }
+    return g;
 }
 
 // Tile lists: the Gram list (all owned lower tiles), then for every owned SP ordinal u
@@ -447,7 +520,12 @@ int gaplac_dist_create(int device, int nranks, int rank, int spw, gaplac_dist** 
     if (const char* e = std::getenv("GAPLAC_DIST_CHUNK")) d->cw = std::max(1, std::min(spw, std::atoi(e)));
     if (const char* e = std::getenv("GAPLAC_DIST_BIG")) d->big_mode = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("GAPLAC_DIST_ALONE")) d->alone = std::atoi(e) > 0;
-    std::vector<hipEvent_t*> evs = {&d->ev_gram, &d->ev_panel_done};
+    {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+            d->ncu = ncu;
+    }
+    std::vector<hipEvent_t*> evs = {&d->ev_gram, &d->ev_panel_done, &d->ev_tail};
     for (int c = 0; c < MAXC; ++c) evs.push_back(&d->ev_col[c]);
     for (int b = 0; b < 2; ++b) {
         for (int c = 0; c < MAXC; ++c) {
@@ -468,6 +546,8 @@ int gaplac_dist_create(int device, int nranks, int rank, int spw, gaplac_dist** 
         return fail("hipMalloc", e);
     if ((e = hipHostMalloc(reinterpret_cast<void**>(&d->htp), sizeof(TermPack), 0)) != hipSuccess)
         return fail("hipHostMalloc", e);
+    if ((e = hipHostMalloc(reinterpret_cast<void**>(&d->htres), sizeof(EvalResult), 0)) != hipSuccess)
+        return fail("hipHostMalloc", e);
     *out = d;
     return 0;
 }
@@ -477,7 +557,7 @@ int gaplac_dist_destroy(gaplac_dist* d) {
     (void)hipSetDevice(d->device);
     for (hipStream_t s : {d->s_main, d->s_panel, d->s_comm})
         if (s) (void)hipStreamSynchronize(s);
-    std::vector<hipEvent_t> evs = {d->ev_gram, d->ev_panel_done};
+    std::vector<hipEvent_t> evs = {d->ev_gram, d->ev_panel_done, d->ev_tail};
     for (int c = 0; c < MAXC; ++c) evs.push_back(d->ev_col[c]);
     for (int b = 0; b < 2; ++b) {
         for (int c = 0; c < MAXC; ++c) {
@@ -490,12 +570,15 @@ int gaplac_dist_destroy(gaplac_dist* d) {
     for (hipEvent_t ev : evs)
         if (ev) (void)hipEventDestroy(ev);
     for (void* p : {(void*)d->C, (void*)d->Dinv, (void*)d->tiles, (void*)d->dX, (void*)d->dv, (void*)d->dres,
-                    (void*)d->dtp, (void*)d->stamps})
+                    (void*)d->dtp, (void*)d->stamps, (void*)d->tmat, (void*)d->tDinv, (void*)d->tres, (void*)d->tctl,
+                    (void*)d->ttasks})
         if (p) (void)hipFree(p);
     if (!d->pbuf_external)
         for (double* p : d->pbuf)
             if (p) (void)hipFree(p);
+    if (!d->tseg_external && d->tseg) (void)hipFree(d->tseg);
     if (d->hres) (void)hipHostFree(d->hres);
+    if (d->htres) (void)hipHostFree(d->htres);
     if (d->htp) (void)hipHostFree(d->htp);
     for (hipStream_t s : {d->s_main, d->s_panel, d->s_comm})
         if (s) (void)hipStreamDestroy(s);
@@ -596,11 +679,44 @@ int gaplac_dist_begin(gaplac_dist* d, int64_t N, int32_t D, const double* X, int
     d->nloc = nloc;
     d->factored_any = false;
     d->held_step = -1;
-    if (d->plan_nt != nt) {
-        d->plan = build_plan(nsp, nt, d->W, d->D, d->pair_m);
+    d->tail_ended = false;
+    const TailGeom tg = tail_geom(d, nt, nsp, Np);
+    d->tstop = tg.stop;
+    d->nsteps = tg.stop < 0 ? nsp : tg.stop;
+    d->tN0 = tg.N0;
+    d->tNt = tg.Nt;
+    d->tseg_off = tg.off;
+    d->tseg_cnt = tg.cnt;
+    if (d->plan_nt != nt || d->plan_stop != d->nsteps) {
+        d->plan = build_plan(nsp, nt, d->W, d->D, d->pair_m, d->nsteps);
         std::string why;
-        if (!check_plan(d->plan, nsp, d->D, &why)) return derr(d, GAPLAC_E_ARG, "step plan: %s", why.c_str());
+        if (!check_plan(d->plan, nsp, d->D, d->nsteps, &why)) return derr(d, GAPLAC_E_ARG, "step plan: %s", why.c_str());
         d->plan_nt = nt;
+        d->plan_stop = d->nsteps;
+    }
+    if (tg.stop >= 0) {
+        if (d->tseg_external) {
+            if (d->tseg_cap < (size_t)tg.elems)
+                return derr(d, GAPLAC_E_ARG, "tail buffer holds %zu doubles, %lld needed", d->tseg_cap,
+                            (long long)tg.elems);
+        } else if ((rc = dgrow(d, &d->tseg, &d->tseg_cap, (size_t)tg.elems))) {
+            return rc;
+        }
+        if (d->rank == d->tail_root) {
+            const int T = nt - tg.stop * d->W;
+            if ((rc = dgrow(d, &d->tmat, &d->tmat_elems, (size_t)(tg.Nt * tg.Nt)))) return rc;
+            if ((rc = dgrow(d, &d->tDinv, &d->tDinv_elems, (size_t)T * DINV_PER_BLOCK))) return rc;
+            if (!d->tres) DCK(d, hipMalloc(reinterpret_cast<void**>(&d->tres), sizeof(EvalResult)));
+            if (!d->tctl) DCK(d, hipMalloc(reinterpret_cast<void**>(&d->tctl), sizeof(TailCtl)));
+            if (d->ttasks_T != T) {
+                std::vector<uint32_t> host;
+                build_single_tail_list(T, 0, -1, d->ncu, host);
+                if ((rc = dgrow(d, &d->ttasks, &d->ttasks_elems, host.size()))) return rc;
+                DCK(d, hipMemcpy(d->ttasks, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+                d->ttasks_n = (int)host.size();
+                d->ttasks_T = T;
+            }
+        }
     }
     if ((rc = dgrow(d, &d->C, &d->C_elems, (size_t)Np * nloc * NB))) return rc;
     if ((rc = dgrow(d, &d->Dinv, &d->Dinv_elems, (size_t)nloc * DINV_PER_BLOCK))) return rc;
@@ -631,11 +747,11 @@ int gaplac_dist_begin(gaplac_dist* d, int64_t N, int32_t D, const double* X, int
                          nloc - 1, nullptr);
         if ((rc = guard.check())) return rc;
     }
-    if (d->stamps && d->stamps_elems >= (size_t)nsp * ST_PER_STEP + 1) stamp(d, d->s_main, nsp * ST_PER_STEP);
+    if (d->stamps && d->stamps_elems >= (size_t)nsp * ST_PER_STEP + ST_EXTRA) stamp(d, d->s_main, nsp * ST_PER_STEP);
     DCK(d, hipEventRecord(d->ev_gram, d->s_main));
     DCK(d, hipStreamWaitEvent(d->s_panel, d->ev_gram, 0));
     DCK(d, hipGetLastError());
-    if (out_nsp) *out_nsp = nsp;
+    if (out_nsp) *out_nsp = d->nsteps;
     return 0;
 }
 
@@ -643,7 +759,7 @@ int gaplac_dist_begin(gaplac_dist* d, int64_t N, int32_t D, const double* X, int
 // then the SP's column chain, packing each chunk into the group buffer once its last
 // column is final (all on s_panel).
 int gaplac_dist_factor(gaplac_dist* d, int32_t s) {
-    if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "factor: step %d out of range", s);
+    if (!d || s < 0 || s >= d->nsteps) return derr(d, GAPLAC_E_ARG, "factor: step %d out of range", s);
     if (!owns(d, s)) return derr(d, GAPLAC_E_ARG, "factor: rank %d does not own super-panel %d", d->rank, s);
     DCK(d, hipSetDevice(d->device));
     DistGuard guard(d);
@@ -717,14 +833,14 @@ int gaplac_dist_factor(gaplac_dist* d, int32_t s) {
 }
 
 int gaplac_dist_chunks(gaplac_dist* d, int32_t s, int32_t* out_chunks) {
-    if (!d || s < 0 || s >= d->nsp || !out_chunks) return derr(d, GAPLAC_E_ARG, "chunks: step %d out of range", s);
+    if (!d || s < 0 || s >= d->nsteps || !out_chunks) return derr(d, GAPLAC_E_ARG, "chunks: step %d out of range", s);
     *out_chunks = nchunks(d, s);
     return 0;
 }
 
 // Device buffer, element count and root rank of the broadcast of chunk c of panel s.
 int gaplac_dist_panel_chunk(gaplac_dist* d, int32_t s, int32_t c, void** ptr, int64_t* count, int32_t* root) {
-    if (!d || s < 0 || s >= d->nsp || c < 0 || c >= nchunks(d, s))
+    if (!d || s < 0 || s >= d->nsteps || c < 0 || c >= nchunks(d, s))
         return derr(d, GAPLAC_E_ARG, "panel: step %d chunk %d out of range", s, c);
     if (ptr) *ptr = chunk_ptr(d, s, c);
     if (count) *count = chunk_count(d, s, c);
@@ -734,7 +850,7 @@ int gaplac_dist_panel_chunk(gaplac_dist* d, int32_t s, int32_t c, void** ptr, in
 
 // The whole panel s as one broadcast (every chunk; gaplac_dist_comm_end then releases all).
 int gaplac_dist_panel(gaplac_dist* d, int32_t s, void** ptr, int64_t* count, int32_t* root) {
-    if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "panel: step %d out of range", s);
+    if (!d || s < 0 || s >= d->nsteps) return derr(d, GAPLAC_E_ARG, "panel: step %d out of range", s);
     if (ptr) *ptr = chunk_ptr(d, s, 0);
     if (count) *count = (int64_t)sp_width(d, s) * NB * group_ld(d, s) - (panel_row0(d, s) - group_row0(d, s));
     if (root) *root = s % d->nranks;
@@ -746,7 +862,7 @@ int gaplac_dist_panel(gaplac_dist* d, int32_t s, void** ptr, int64_t* count, int
 // longer read) and return it as an opaque hipStream_t, on which the host enqueues the
 // broadcast (ncclBroadcast / RCCL).
 int gaplac_dist_comm_begin_chunk(gaplac_dist* d, int32_t s, int32_t c, void** stream) {
-    if (!d || s < 0 || s >= d->nsp || c < 0 || c >= nchunks(d, s))
+    if (!d || s < 0 || s >= d->nsteps || c < 0 || c >= nchunks(d, s))
         return derr(d, GAPLAC_E_ARG, "comm_begin: step %d chunk %d out of range", s, c);
     DCK(d, hipSetDevice(d->device));
     if (owns(d, s)) {
@@ -760,7 +876,7 @@ int gaplac_dist_comm_begin_chunk(gaplac_dist* d, int32_t s, int32_t c, void** st
 }
 
 int gaplac_dist_comm_begin(gaplac_dist* d, int32_t s, void** stream) {
-    if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "comm_begin: step %d out of range", s);
+    if (!d || s < 0 || s >= d->nsteps) return derr(d, GAPLAC_E_ARG, "comm_begin: step %d out of range", s);
     int rc = gaplac_dist_comm_begin_chunk(d, s, 0, stream);
     if (rc || !owns(d, s)) return rc;
     for (int c = 1; c < nchunks(d, s); ++c) DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_packed[s & 1][c], 0));
@@ -769,7 +885,7 @@ int gaplac_dist_comm_begin(gaplac_dist* d, int32_t s, void** stream) {
 
 // The broadcast of chunk c of panel s is enqueued on the comm stream: later readers wait for it.
 int gaplac_dist_comm_end_chunk(gaplac_dist* d, int32_t s, int32_t c) {
-    if (!d || s < 0 || s >= d->nsp || c < 0 || c >= nchunks(d, s))
+    if (!d || s < 0 || s >= d->nsteps || c < 0 || c >= nchunks(d, s))
         return derr(d, GAPLAC_E_ARG, "comm_end: step %d chunk %d out of range", s, c);
     DCK(d, hipSetDevice(d->device));
     DCK(d, hipEventRecord(d->ev_recv[s & 1][c], d->s_comm));
@@ -777,7 +893,7 @@ int gaplac_dist_comm_end_chunk(gaplac_dist* d, int32_t s, int32_t c) {
 }
 
 int gaplac_dist_comm_end(gaplac_dist* d, int32_t s) {
-    if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "comm_end: step %d out of range", s);
+    if (!d || s < 0 || s >= d->nsteps) return derr(d, GAPLAC_E_ARG, "comm_end: step %d out of range", s);
     for (int c = 0; c < nchunks(d, s); ++c) {
         int rc = gaplac_dist_comm_end_chunk(d, s, c);
         if (rc) return rc;
@@ -837,7 +953,7 @@ static int run_ops(gaplac_dist* d, int p, size_t b, size_t e, bool chain_beside)
 // step, or the last step of all) releases the group buffer.
 static int end_step(gaplac_dist* d, int p) {
     stamp(d, d->s_main, st_end(p));
-    if (p % d->D == d->D - 1 || p + 1 >= d->nsp)
+    if (p % d->D == d->D - 1 || p + 1 >= d->nsteps)
         DCK(d, hipEventRecord(d->ev_free_main[group_buf(d, p)], d->s_main));
     return 0;
 }
@@ -849,7 +965,7 @@ static int end_step(gaplac_dist* d, int p) {
 // until update(s+1) (after factor(s+2)): the chain of SP s+2, which starts at that mark,
 // then never shares the GPU with this rank's bulk updates.
 int gaplac_dist_update(gaplac_dist* d, int32_t s) {
-    if (!d || s < 0 || s >= d->nsp) return derr(d, GAPLAC_E_ARG, "update: step %d out of range", s);
+    if (!d || s < 0 || s >= d->nsteps) return derr(d, GAPLAC_E_ARG, "update: step %d out of range", s);
     DCK(d, hipSetDevice(d->device));
     const int last = nchunks(d, s) - 1;
     // the owner reads its own packed panel (its broadcast may still be running); the
@@ -857,7 +973,7 @@ int gaplac_dist_update(gaplac_dist* d, int32_t s) {
     // updates before this one on the same stream.
     DCK(d, hipStreamWaitEvent(d->s_main, owns(d, s) ? d->ev_packed[s & 1][last] : d->ev_recv[s & 1][last], 0));
     const bool alone = d->alone && d->nranks > 1;
-    const bool waits = alone && s + 1 < d->nsp && owns(d, s + 1);
+    const bool waits = alone && s + 1 < d->nsteps && owns(d, s + 1);
     if (waits) DCK(d, hipStreamWaitEvent(d->s_main, d->ev_panel_done, 0));  // factor(s+1), enqueued just before
     int rc;
     if (d->held_step >= 0) {  // update(s-1)'s ops after its mark (this rank's chain of SP s+1 is done)
@@ -869,14 +985,14 @@ int gaplac_dist_update(gaplac_dist* d, int32_t s) {
     stamp(d, d->s_main, st_upd(s));
     if (d->stamps) DCK(d, hipEventRecord(d->ev_upd[s & 1], d->s_main));
     // this rank's chain runs beside the update when it owns SP s+1 and does not wait for it
-    const bool chain_beside = s + 1 < d->nsp && owns(d, s + 1) && !waits;
+    const bool chain_beside = s + 1 < d->nsteps && owns(d, s + 1) && !waits;
     const std::vector<DOp>& ops = d->plan[(size_t)s];
     size_t mark = 0;
     while (mark < ops.size() && ops[mark].kind != OP_MARK) ++mark;
     if ((rc = run_ops(d, s, 0, std::min(mark + 1, ops.size()), chain_beside))) return rc;
     // (not with D = 1: factor(s+2) packs panel s+2 into panel s's buffer slot, which the held
     // ops still read; with D >= 2 panel s+2 lands in the other group buffer or another slot)
-    if (alone && d->D >= 2 && s + 2 < d->nsp && owns(d, s + 2)) {
+    if (alone && d->D >= 2 && s + 2 < d->nsteps && owns(d, s + 2)) {
         d->held_step = s;
         d->held_from = mark + 1;
     } else {
@@ -894,21 +1010,147 @@ int gaplac_dist_finish(gaplac_dist* d, double* out_logdet, double* out_quad, int
     DCK(d, hipSetDevice(d->device));
     if (d->held_step >= 0) return derr(d, GAPLAC_E_ARG, "finish: step %d's update is incomplete", d->held_step);
     if (d->factored_any) DCK(d, hipStreamWaitEvent(d->s_main, d->ev_panel_done, 0));
+    // the distributed SPs' columns come first in the storage (a gathered SP's columns were
+    // factored by the root's tail, whose sums are in tres)
+    int64_t ncols = 0;
+    for (int s = d->rank; s < d->nsteps; s += d->nranks) ncols += sp_width(d, s);
     {
         DistGuard guard(d);
-        launch_reduce(d->s_main, d->C, d->Np, d->N, (int64_t)d->nloc * NB, cmap(d), d->dres);
+        launch_reduce(d->s_main, d->C, d->Np, d->N, ncols * NB, cmap(d), d->dres);
         int rc;
         if ((rc = guard.check())) return rc;
     }
+    const bool troot = d->tstop >= 0 && d->rank == d->tail_root;
+    if (troot && !d->tail_ended) return derr(d, GAPLAC_E_ARG, "finish: the tail gather was not completed (tail_end)");
     DCK(d, hipMemcpyAsync(d->hres, d->dres, offsetof(EvalResult, part), hipMemcpyDeviceToHost, d->s_main));
+    if (troot) DCK(d, hipMemcpyAsync(d->htres, d->tres, offsetof(EvalResult, part), hipMemcpyDeviceToHost, d->s_main));
     DCK(d, hipStreamSynchronize(d->s_main));
     DCK(d, hipStreamSynchronize(d->s_panel));
     DCK(d, hipStreamSynchronize(d->s_comm));
-    const EvalResult r = *d->hres;
+    EvalResult r = *d->hres;
+    if (troot) {
+        const EvalResult& t = *d->htres;
+        r.err |= t.err;
+        r.logdet += t.logdet;
+        r.quad += t.quad;
+        if (t.info != ~0ull) r.info = std::min(r.info, t.info + (unsigned long long)d->tN0);  // global (j + 1)
+    }
     if (r.err) return derr(d, GAPLAC_E_HIP, "in-kernel wait expired (code %u)", r.err);
     if (out_logdet) *out_logdet = r.logdet;
     if (out_quad) *out_quad = r.quad;
     if (out_info) *out_info = r.info == ~0ull ? 0 : (int64_t)r.info;
+    return 0;
+}
+
+// ---- tail gather ----
+
+// tail_cols > 0: the SPs in the last tail_cols tile columns are gathered onto rank root and
+// factored there by the persistent tail; 0 = off. Before begin.
+int gaplac_dist_set_tail(gaplac_dist* d, int32_t tail_cols, int32_t root) {
+    if (!d) return GAPLAC_E_ARG;
+    if (tail_cols < 0 || tail_cols > TAIL_TMAX || root < 0 || root >= d->nranks)
+        return derr(d, GAPLAC_E_ARG, "set_tail: %d tile columns onto rank %d", tail_cols, root);
+    d->tail_cols = tail_cols;
+    d->tail_root = root;
+    d->plan_stop = -1;
+    return 0;
+}
+
+// For order N (before begin): gather segments (0: no gather), the doubles this rank's
+// segment buffer needs, and the distributed steps begin will return.
+int gaplac_dist_tail_geometry(gaplac_dist* d, int64_t N, int32_t* nseg, int64_t* buf_elems, int32_t* nsteps) {
+    if (!d || N < 1) return derr(d, GAPLAC_E_ARG, "bad tail geometry query");
+    int64_t Np;
+    int32_t nt, nsp;
+    gaplac_dist_geometry(d, N, &Np, &nt, &nsp, nullptr, nullptr);
+    const TailGeom g = tail_geom(d, nt, nsp, Np);
+    if (nseg) *nseg = g.stop < 0 ? 0 : nsp - g.stop;
+    if (buf_elems) *buf_elems = g.elems;
+    if (nsteps) *nsteps = g.stop < 0 ? nsp : g.stop;
+    return 0;
+}
+
+// Optional caller-owned segment buffer (e.g. a tensor of the collective library's binding),
+// >= buf_elems doubles; NULL returns to a library-owned one.
+int gaplac_dist_set_tail_buffer(gaplac_dist* d, void* buf, int64_t capacity) {
+    if (!d) return GAPLAC_E_ARG;
+    DCK(d, hipSetDevice(d->device));
+    if (!d->tseg_external && d->tseg) (void)hipFree(d->tseg);
+    d->tseg = buf && capacity > 0 ? static_cast<double*>(buf) : nullptr;
+    d->tseg_cap = d->tseg ? (size_t)capacity : 0;
+    d->tseg_external = d->tseg != nullptr;
+    return 0;
+}
+
+// Segment i of the current evaluation's gather (SP tstop + i): this rank's buffer for it
+// (NULL when the rank neither sends nor receives it), doubles, and the sending rank.
+int gaplac_dist_tail_segment(gaplac_dist* d, int32_t i, void** buf, int64_t* count, int32_t* src) {
+    if (!d || d->tstop < 0 || i < 0 || i >= d->nsp - d->tstop)
+        return derr(d, GAPLAC_E_ARG, "tail_segment %d: no such segment", i);
+    const size_t k = (size_t)i;
+    if (buf) *buf = d->tseg_cnt[k] ? d->tseg + d->tseg_off[k] : nullptr;
+    if (count) *count = d->tseg_cnt[k] ? d->tseg_cnt[k] : 0;
+    if (src) *src = (d->tstop + i) % d->nranks;
+    return 0;
+}
+
+// After the last step's update: this rank's segments are packed on the comm stream, which
+// is returned; the host enqueues the gather there (sends of this rank's segments to the
+// root, the root's receives: ncclSend / ncclRecv in one group). The root's own segments are
+// packed in place and not sent.
+int gaplac_dist_tail_begin(gaplac_dist* d, void** stream) {
+    if (!d || d->tstop < 0) return derr(d, GAPLAC_E_ARG, "tail_begin: no tail gather in this evaluation");
+    if (d->held_step >= 0) return derr(d, GAPLAC_E_ARG, "tail_begin: step %d's update is incomplete", d->held_step);
+    DCK(d, hipSetDevice(d->device));
+    d->tail_ended = false;
+    DCK(d, hipEventRecord(d->ev_tail, d->s_main));
+    DCK(d, hipStreamWaitEvent(d->s_comm, d->ev_tail, 0));
+    for (int s = d->tstop; s < d->nsp; ++s) {
+        if (!owns(d, s)) continue;
+        const int i = s - d->tstop;
+        const int64_t rows = tseg_rows(d->tNt, d->W, i);
+        const int lc0 = sp_local(d, s);
+        for (int k = 0; k < sp_width(d, s); ++k)
+            launch_pack(d->s_comm, d->C + (int64_t)(lc0 + k) * NB * d->Np + panel_row0(d, s), d->Np,
+                        d->tseg + d->tseg_off[(size_t)i] + (int64_t)k * NB * rows, rows, rows);
+    }
+    DCK(d, hipGetLastError());
+    if (stream) *stream = d->s_comm;
+    return 0;
+}
+
+// The gather is enqueued on the comm stream. The root unpacks the segments into the
+// trailing matrix and factors it with the single-GPU persistent tail (tail_kernel) on
+// s_main; its logdet / quad / first failing pivot join the root's partial sums in finish.
+int gaplac_dist_tail_end(gaplac_dist* d) {
+    if (!d || d->tstop < 0) return derr(d, GAPLAC_E_ARG, "tail_end: no tail gather in this evaluation");
+    DCK(d, hipSetDevice(d->device));
+    d->tail_ended = true;
+    if (d->rank != d->tail_root) return 0;
+    DCK(d, hipEventRecord(d->ev_tail, d->s_comm));
+    DCK(d, hipStreamWaitEvent(d->s_main, d->ev_tail, 0));
+    LaunchGuard g;
+    g.base = d->tmat;
+    g.elems = d->tNt * d->tNt;
+    GuardScope scope(&g);
+    hipStream_t sm = d->s_main;
+    for (int s = d->tstop; s < d->nsp; ++s) {
+        const int i = s - d->tstop;
+        const int64_t rows = tseg_rows(d->tNt, d->W, i), r0 = (int64_t)i * d->W * NB;
+        for (int k = 0; k < sp_width(d, s); ++k)
+            launch_pack(sm, d->tseg + d->tseg_off[(size_t)i] + (int64_t)k * NB * rows, rows,
+                        d->tmat + (r0 + (int64_t)k * NB) * d->tNt + r0, d->tNt, rows);
+    }
+    const int T = d->nt - d->tstop * d->W;
+    const int64_t tN = d->N - d->tN0;
+    launch_init_result(sm, d->tres);
+    DCK(d, hipMemsetAsync(d->tctl, 0, sizeof(TailCtl), sm));
+    TailArgs ta{d->tmat, d->tNt, tN, 0, T, d->tDinv, d->tres, d->tctl, d->ttasks, d->ttasks_n, nullptr};
+    launch_tail(sm, ta, std::min(d->ncu, d->ttasks_n), nullptr);
+    launch_reduce(sm, d->tmat, d->tNt, tN, (int64_t)T * NB, ColMap{1, 0, 1}, d->tres);
+    if (d->stamps) stamp(d, sm, d->nsp * ST_PER_STEP + 2);
+    DCK(d, hipGetLastError());
+    if (g.violations) return derr(d, GAPLAC_E_ARG, "tail launch outside the trailing matrix: %s", g.first.c_str());
     return 0;
 }
 
@@ -928,13 +1170,16 @@ int gaplac_dist_local(gaplac_dist* d, double* out, int64_t ld) {
 // gets every earlier panel exactly once, in order, before its chain; returns 0 or
 // GAPLAC_E_ARG with the first violation in msg. *out_ops: the plan's bulk launches per rank
 // count (bands + suffixes), for tests.
-int gaplac_dist_plan_check(int32_t nt, int32_t spw, int32_t depth, int32_t pair_m, int64_t* out_ops, char* msg,
-                           int64_t msglen) {
-    if (nt < 1 || spw < 1 || spw > MAXC || depth < 1 || depth > 8) return GAPLAC_E_ARG;
+int gaplac_dist_plan_check_tail(int32_t nt, int32_t spw, int32_t depth, int32_t pair_m, int32_t tail_cols,
+                                int64_t* out_ops, char* msg, int64_t msglen) {
+    if (nt < 1 || spw < 1 || spw > MAXC || depth < 1 || depth > 8 || tail_cols < 0 || tail_cols > TAIL_TMAX)
+        return GAPLAC_E_ARG;
     const int nsp = (nt + spw - 1) / spw;
-    const auto plan = build_plan(nsp, nt, spw, depth, pair_m);
+    const int ts = tail_stop_of(nt, spw, tail_cols);
+    const int stop = ts < 0 ? nsp : ts;
+    const auto plan = build_plan(nsp, nt, spw, depth, pair_m, stop);
     std::string why;
-    const bool ok = check_plan(plan, nsp, depth, &why);
+    const bool ok = check_plan(plan, nsp, depth, stop, &why);
     if (out_ops) {
         int64_t n = 0;
         for (const auto& ops : plan)
@@ -947,15 +1192,24 @@ int gaplac_dist_plan_check(int32_t nt, int32_t spw, int32_t depth, int32_t pair_
     return ok ? 0 : GAPLAC_E_ARG;
 }
 
+int gaplac_dist_plan_check(int32_t nt, int32_t spw, int32_t depth, int32_t pair_m, int64_t* out_ops, char* msg,
+                           int64_t msglen) {
+    return gaplac_dist_plan_check_tail(nt, spw, depth, pair_m, 0, out_ops, msg, msglen);
+}
+
 // The step plan itself (host-only): per op (step, kind, g, pf, pl) as 5 int32 into out
 // (cap ints); *out_n = number of ops. kind: 0 band of SP g, 1 every SP >= g, 2 mark.
-int gaplac_dist_plan(int32_t nt, int32_t spw, int32_t depth, int32_t pair_m, int32_t* out, int64_t cap,
-                     int64_t* out_n) {
-    if (nt < 1 || spw < 1 || spw > MAXC || depth < 1 || depth > 8 || !out_n) return GAPLAC_E_ARG;
+// tail_cols as gaplac_dist_set_tail's (the plan then has fewer steps than SPs).
+int gaplac_dist_plan_tail(int32_t nt, int32_t spw, int32_t depth, int32_t pair_m, int32_t tail_cols, int32_t* out,
+                          int64_t cap, int64_t* out_n) {
+    if (nt < 1 || spw < 1 || spw > MAXC || depth < 1 || depth > 8 || !out_n || tail_cols < 0 || tail_cols > TAIL_TMAX)
+        return GAPLAC_E_ARG;
     const int nsp = (nt + spw - 1) / spw;
-    const auto plan = build_plan(nsp, nt, spw, depth, pair_m);
+    const int ts = tail_stop_of(nt, spw, tail_cols);
+    const int stop = ts < 0 ? nsp : ts;
+    const auto plan = build_plan(nsp, nt, spw, depth, pair_m, stop);
     int64_t n = 0;
-    for (int p = 0; p < nsp; ++p)
+    for (int p = 0; p < stop; ++p)
         for (const DOp& op : plan[(size_t)p]) {
             if (out && 5 * (n + 1) <= cap) {
                 int32_t* o = out + 5 * n;
@@ -969,6 +1223,11 @@ int gaplac_dist_plan(int32_t nt, int32_t spw, int32_t depth, int32_t pair_m, int
         }
     *out_n = n;
     return 0;
+}
+
+int gaplac_dist_plan(int32_t nt, int32_t spw, int32_t depth, int32_t pair_m, int32_t* out, int64_t cap,
+                     int64_t* out_n) {
+    return gaplac_dist_plan_tail(nt, spw, depth, pair_m, 0, out, cap, out_n);
 }
 
 // ---- replay of one rank's schedule on one GPU (diagnostics) ----
@@ -988,18 +1247,18 @@ int gaplac_dist_replay_enable(gaplac_dist* d, int64_t N) {
     int32_t nsp = 0;
     gaplac_dist_geometry(d, N, nullptr, nullptr, &nsp, nullptr, nullptr);
     int rc;
-    if ((rc = dgrow(d, &d->stamps, &d->stamps_elems, (size_t)nsp * ST_PER_STEP + 1))) return rc;
+    if ((rc = dgrow(d, &d->stamps, &d->stamps_elems, (size_t)nsp * ST_PER_STEP + ST_EXTRA))) return rc;
     DCK(d, hipMemsetAsync(d->stamps, 0, d->stamps_elems * 8, d->s_main));
     DCK(d, hipStreamSynchronize(d->s_main));
     return 0;
 }
 
 int gaplac_dist_replay_stamps(gaplac_dist* d, uint64_t* out, int64_t n) {
-    if (!d || !d->stamps || !out || n < (int64_t)d->nsp * ST_PER_STEP + 1 ||
-        d->stamps_elems < (size_t)d->nsp * ST_PER_STEP + 1)
+    if (!d || !d->stamps || !out || n < (int64_t)d->nsp * ST_PER_STEP + ST_EXTRA ||
+        d->stamps_elems < (size_t)d->nsp * ST_PER_STEP + ST_EXTRA)
         return derr(d, GAPLAC_E_ARG, "stamps: bad output");
     DCK(d, hipSetDevice(d->device));
-    DCK(d, hipMemcpy(out, d->stamps, ((size_t)d->nsp * ST_PER_STEP + 1) * 8, hipMemcpyDeviceToHost));
+    DCK(d, hipMemcpy(out, d->stamps, ((size_t)d->nsp * ST_PER_STEP + ST_EXTRA) * 8, hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -1013,7 +1272,7 @@ int gaplac_dist_replay_stamps(gaplac_dist* d, uint64_t* out, int64_t n) {
 // for this rank's own panel (its send). Then comm_end_chunk(s, c).
 int gaplac_dist_replay_chunk(gaplac_dist* d, const gaplac_dist* src, int32_t s, int32_t c, int64_t f_ticks,
                              int64_t band_ticks, int64_t lat_ticks, int64_t xfer_ticks, int64_t copy_ticks) {
-    if (!d || !d->stamps || s < 0 || s >= d->nsp || c < 0 || c >= nchunks(d, s))
+    if (!d || !d->stamps || s < 0 || s >= d->nsteps || c < 0 || c >= nchunks(d, s))
         return derr(d, GAPLAC_E_ARG, "replay: step %d chunk %d (stamps %s)", s, c, d && d->stamps ? "on" : "off");
     void* st = nullptr;
     int rc;
@@ -1059,6 +1318,48 @@ int gaplac_dist_replay_chunk(gaplac_dist* d, const gaplac_dist* src, int32_t s, 
         stamp(d, d->s_comm, st_pack(s, c));  // a non-owner's PACK slot: the copy's end
     }
     return gaplac_dist_comm_end_chunk(d, s, c);
+}
+
+// Modelled tail gather on the replayed rank, in place of the host's sends / receives
+// (between tail_begin and tail_end, which this calls). Every sender's segments leave when
+// its last update is done, taken as this rank's own (every rank's s_main runs the same
+// steps), over its own link: the root's receives arrive at
+//   END(last step) + lat + max over senders of (its bytes) x ticks_per_byte
+// as copies from the owners' segment buffers (owners[q]: rank q's context of a loopback
+// run with the same gather; copy_ticks of the copies are taken off the wait). A sender's
+// own sends end at END(last step) + lat + its bytes x ticks_per_byte (stamped only).
+int gaplac_dist_replay_tail(gaplac_dist* d, const gaplac_dist* const* owners, int32_t nowners, int64_t lat_ticks,
+                            double ticks_per_byte, int64_t copy_ticks) {
+    if (!d || !d->stamps || d->tstop < 0 || !owners || nowners != d->nranks)
+        return derr(d, GAPLAC_E_ARG, "replay_tail: needs stamps, a gather and every rank's context");
+    void* st = nullptr;
+    int rc;
+    if ((rc = gaplac_dist_tail_begin(d, &st))) return rc;
+    const bool root = d->rank == d->tail_root;
+    std::vector<int64_t> bytes((size_t)d->nranks, 0);
+    for (int i = 0; i < d->nsp - d->tstop; ++i) {
+        const int src = (d->tstop + i) % d->nranks;
+        const int64_t c = (int64_t)sp_width(d, d->tstop + i) * NB * tseg_rows(d->tNt, d->W, i) * 8;
+        if (src != d->tail_root) bytes[(size_t)src] += c;
+    }
+    const int64_t sent = root ? *std::max_element(bytes.begin(), bytes.end()) : bytes[(size_t)d->rank];
+    Release r{{st_end(d->nsteps - 1), -1, -1}, {lat_ticks + (long long)(sent * ticks_per_byte) - (root ? copy_ticks : 0), 0, 0},
+              d->nsp * ST_PER_STEP + 1};
+    if (guard_launch("release_kernel")) release_kernel<<<dim3(1), dim3(64), 0, d->s_comm>>>(d->stamps, r);
+    if (root) {
+        for (int i = 0; i < d->nsp - d->tstop; ++i) {
+            const int src = (d->tstop + i) % d->nranks;
+            if (src == d->tail_root) continue;
+            const gaplac_dist* o = owners[src];
+            if (!o || o->rank != src || o->tstop != d->tstop || o->tNt != d->tNt || !o->tseg ||
+                o->tseg_cnt[(size_t)i] != d->tseg_cnt[(size_t)i])
+                return derr(d, GAPLAC_E_ARG, "replay_tail: rank %d's context has no segment %d", src, i);
+            DCK(d, hipMemcpyAsync(d->tseg + d->tseg_off[(size_t)i], o->tseg + o->tseg_off[(size_t)i],
+                                  (size_t)d->tseg_cnt[(size_t)i] * 8, hipMemcpyDeviceToDevice, d->s_comm));
+        }
+        stamp(d, d->s_comm, d->nsp * ST_PER_STEP + 3);
+    }
+    return gaplac_dist_tail_end(d);
 }
 
 // Bytes of chunk c of panel s that a broadcast must move (rows from the panel's first

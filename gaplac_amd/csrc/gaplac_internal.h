@@ -158,6 +158,9 @@ void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<s
 // The list is a topological order of the tail's dataflow that applies every update once.
 bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why, int xrows = 0);
 void launch_tail(hipStream_t s, const TailArgs& a, int grid, KTime* kt);
+// The single-evaluation tail list (gaplac_api.hip): T tile columns, X extra tile rows, the
+// simulated order per tail_sim (-1 auto: T < 80) planned for `workers` workgroups.
+void build_single_tail_list(int T, int X, int tail_sim, int workers, std::vector<uint32_t>& out);
 
 // Host-side footprint guard. Before launching, every launcher computes the
 // element range [p + lo, p + hi) its grid will touch in the column storage it is given

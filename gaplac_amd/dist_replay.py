@@ -17,7 +17,11 @@ node from a run of that rank's real work on one GPU:
   same steps at the same time, up to the 1/P shares), band(s) and F(s, c) (the owner's time
   from its inputs to chunk c packed) are MEASURED on this rank's own super-panels (every
   P-th) in the previous iteration and interpolated in s, and lat, BW model the link;
-* this rank's own panels leave at PACK(s, c) + lat + bytes / BW (its sends).
+* this rank's own panels leave at PACK(s, c) + lat + bytes / BW (its sends);
+* with the tail gather every sender's segments leave when its last update
+  ends (taken as this rank's own END) over its own link at gather_bw, so the root's
+  receives arrive at END(last) + lat + (the largest sender's bytes) / gather_bw, as copies
+  from the owners' segment buffers (gaplac_dist_replay_tail); the root then runs the tail.
 
 Iterated a few times (F and band from the previous run), the rank's evaluation time is
 the prediction; the per-step stamps show whether a step waited for the panel (comm/chain
@@ -37,10 +41,14 @@ TICK_S = 1e-8  # s_memrealtime: 100 MHz
 
 
 class ReplayModel:
-    """Link model: per broadcast chunk lat_us + bytes / (bw_GBps * 1e9)."""
+    """Link model: per broadcast chunk lat_us + bytes / (bw_GBps * 1e9); the tail gather's
+    point-to-point sends over one xGMI link each at gather_bw_GBps."""
 
-    def __init__(self, bw_GBps: float = 200.0, lat_us: float = 15.0):
-        self.bw, self.lat = float(bw_GBps), float(lat_us)
+    def __init__(self, bw_GBps: float = 200.0, lat_us: float = 15.0, gather_bw_GBps: float = 50.0):
+        self.bw, self.lat, self.gbw = float(bw_GBps), float(lat_us), float(gather_bw_GBps)
+
+    def gather_ticks_per_byte(self) -> float:
+        return 1.0 / (self.gbw * 1e9) / TICK_S
 
     def xfer_ticks(self, nbytes: int) -> int:
         return int(round(nbytes / (self.bw * 1e9) / TICK_S))
@@ -49,15 +57,18 @@ class ReplayModel:
         return int(round(self.lat * 1e-6 / TICK_S))
 
 
+ST_EXTRA = 4  # gaplac_dist.hip: Gram end, gather arrival, tail end, gather copies end
+
+
 def _stamps(r: DI.DistRank, nsp: int):
     per, maxc = c_int32(), c_int32()
     nb = c_int64()
     r._check(r.lib.gaplac_dist_replay_info(r.h, 0, 0, byref(nb), byref(per), byref(maxc)))
-    n = nsp * per.value + 1
+    n = nsp * per.value + ST_EXTRA
     out = (c_uint64 * n)()
     r._check(r.lib.gaplac_dist_replay_stamps(r.h, out, n))
     a = np.frombuffer(out, dtype=np.uint64).astype(np.int64)
-    return a[:-1].reshape(nsp, per.value), maxc.value, int(a[-1])
+    return a[:-ST_EXTRA].reshape(nsp, per.value), maxc.value, [int(x) for x in a[-ST_EXTRA:]]
 
 
 def _interp(samples: dict, nsp: int, default: float) -> np.ndarray:
@@ -70,15 +81,17 @@ def _interp(samples: dict, nsp: int, default: float) -> np.ndarray:
 
 
 def replay_rank(owners, rep: DI.DistRank, N: int, D: int, dX_ptr: int, terms, noise: float, dv_ptr: int,
-                model: ReplayModel, F=None, band=None, copy_ticks: int = 0):
+                model: ReplayModel, F=None, band=None, copy_ticks: int = 0, tail_copy_ticks: int = 0):
     """One replayed evaluation of rank rep.rank. owners[q]: the factored loopback context of
-    rank q. F[s][c], band[s]: model inputs in ticks (None: a first guess). Returns a dict of
-    the time, the stamps and the measured inputs for the next iteration."""
+    rank q (a loopback run with the same tail gather). F[s][c], band[s]: model inputs in
+    ticks (None: a first guess). Returns a dict of the time, the stamps and the measured
+    inputs for the next iteration."""
     import torch
     rep._check(rep.lib.gaplac_dist_replay_enable(rep.h, int(N)))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    nsp = rep.begin_device(N, D, dX_ptr, N, terms, noise, dv_ptr)
+    nsp = rep.begin_device(N, D, dX_ptr, N, terms, noise, dv_ptr)  # the distributed steps
+    nsp_all = rep.geometry(N)["nsp"]
     P = rep.nranks
     nch = [rep.chunks(s) for s in range(nsp)]
     if F is None:  # first guess: 0.5 ms per chunk of chain
@@ -106,9 +119,16 @@ def replay_rank(owners, rep: DI.DistRank, N: int, D: int, dX_ptr: int, terms, no
         rep.update(s)
         if s + 1 < nsp:
             release(s + 1)
+    gathered = rep.tail_segments() > 0
+    if gathered:
+        arr = (c_void_p * P)(*[o.h.value for o in owners])
+        rep._check(rep.lib.gaplac_dist_replay_tail(rep.h, arr, P, lat, model.gather_ticks_per_byte(),
+                                                   int(tail_copy_ticks)))
     ld, q, info = rep.finish()
     wall = time.perf_counter() - t0
-    st, maxc, gram_done = _stamps(rep, nsp)
+    st, maxc, extra = _stamps(rep, nsp_all)
+    gram_done, t_arrive, t_tail_end, t_copied = extra
+    st = st[:nsp]
     rep._check(rep.lib.gaplac_dist_replay_enable(rep.h, 0))
     UPD, BAND = st[:, 0], st[:, 1]
     PACK = st[:, 3:3 + maxc]
@@ -126,9 +146,19 @@ def replay_rank(owners, rep: DI.DistRank, N: int, D: int, dX_ptr: int, terms, no
         f_meas[s] = [float(PACK[s, c] - ready) for c in range(nch[s])]
     copies = [float(PACK[s, c] - RECV[s, c]) for s in range(nsp) if not rep.owns(s) for c in range(nch[s])]
     t_first = gram_done
+    tail = None
+    root = gathered and rep.rank == rep.tail_root
+    if gathered:
+        end_last = int(st[nsp - 1, 2])
+        tail = dict(steps_end_us=round((end_last - t_first) * 0.01, 1), arrive_us=round((t_arrive - t_first) * 0.01, 1))
+        if root:
+            tail.update(copies_us=round(max(0, t_copied - t_arrive) * 0.01, 1),
+                        tail_end_us=round((t_tail_end - t_first) * 0.01, 1),
+                        tail_ms=round((t_tail_end - max(t_copied, t_arrive)) * 1e-5, 3))
     return dict(wall_s=wall, nsp=nsp, nch=nch, stamps=st, maxc=maxc, f_meas=f_meas, b_meas=b_meas,
                 copy_mean=float(np.mean(copies)) if copies else 0.0, logdet_part=ld, quad_part=q, info=info,
-                last_recv=last, t_first=t_first)
+                last_recv=last, t_first=t_first, tail=tail,
+                tail_copy=max(0, t_copied - t_arrive) if root else 0)
 
 
 def next_inputs(res: dict, prev_F=None, prev_band=None):

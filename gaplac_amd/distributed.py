@@ -20,12 +20,15 @@ Transports:
                          schedule at any rank count on a single GPU)
 
 Schedule (per rank; every library call only enqueues work except finish):
-    begin; factor(0) [owner]; bcast(0)
-    for s in 0..nsp-1: factor(s+1) [owner of s+1]; update(s); bcast(s+1)
+    begin -> nsteps; factor(0) [owner]; bcast(0)
+    for s in 0..nsteps-1: factor(s+1) [owner of s+1, s+1 < nsteps]; update(s); bcast(s+1)
+    [tail gather: tail_begin; send / receive the segments; tail_end]
     finish -> partial (logdet, quad, info); combine across ranks
 bcast(s) is one broadcast per chunk of panel s (a run of its tile columns): the owner packs
 a chunk as soon as its last column is final, and the next owner's lookahead consumes it as
-it arrives.
+it arrives. With the tail gather (set_tail) the last
+super-panels are not stepped: every rank sends its columns of the trailing matrix to the
+root, which factors it with the single-GPU persistent tail (nsteps < nsp).
 """
 from __future__ import annotations
 
@@ -48,7 +51,8 @@ class DistRank:
     """One rank's state (a gaplac_dist context) on `device`."""
 
     def __init__(self, device: int, nranks: int, rank: int, spw: int = DEFAULT_SPW, depth: int = -1,
-                 chunk: int = -1, big: int = -1, big_min: int = -1, alone: int = -1):
+                 chunk: int = -1, big: int = -1, big_min: int = -1, alone: int = -1, tail: int = -1,
+                 tail_root: int = 0):
         self.lib = _native.load()
         h = c_void_p()
         rc = self.lib.gaplac_dist_create(int(device), int(nranks), int(rank), int(spw), byref(h))
@@ -57,7 +61,23 @@ class DistRank:
         self.h = h
         self.device, self.nranks, self.rank, self.spw = device, nranks, rank, spw
         self._bufs = None  # torch tensors backing the panel buffers (kept alive here)
+        self._tbuf = None  # torch tensor backing the tail-gather segment buffer
+        self._nseg = 0
+        self.tail_root = 0
         self.configure(depth, chunk, big, big_min, alone)
+        if tail >= 0:
+            self.set_tail(tail, tail_root)
+
+    def set_tail(self, cols: int, root: int = 0):
+        """Tail gather (gaplac_dist_set_tail): the super-panels in the last `cols` tile
+        columns are factored on rank `root` by the persistent tail; 0 = off."""
+        self._check(self.lib.gaplac_dist_set_tail(self.h, int(cols), int(root)))
+        self.tail_root = int(root)
+
+    def tail_geometry(self, N: int):
+        nseg, elems, nsteps = c_int32(), c_int64(), c_int32()
+        self._check(self.lib.gaplac_dist_tail_geometry(self.h, int(N), byref(nseg), byref(elems), byref(nsteps)))
+        return dict(nseg=nseg.value, elems=elems.value, nsteps=nsteps.value)
 
     def configure(self, depth: int = -1, chunk: int = -1, big: int = -1, big_min: int = -1, alone: int = -1):
         """Schedule options (gaplac_dist_configure; -1 keeps the current value): deferral
@@ -100,15 +120,19 @@ class DistRank:
         return dict(Np=Np.value, nt=nt.value, nsp=nsp.value, nloc=nloc.value, panel_elems=pel.value)
 
     def use_torch_panel_buffers(self, N: int):
-        """Back the two panel buffers with torch tensors on this rank's device (so the
-        collective library broadcasts torch tensors)."""
+        """Back the two panel buffers (and the tail gather's segment buffer) with torch
+        tensors on this rank's device (so the collective library moves torch tensors)."""
         import torch
+        dev = torch.device("cuda", self.device)
         need = self.geometry(N)["panel_elems"]
         if self._bufs is None or self._bufs[0].numel() < need:
-            dev = torch.device("cuda", self.device)
             self._bufs = [torch.empty(need, dtype=torch.float64, device=dev) for _ in range(2)]
             self._check(self.lib.gaplac_dist_set_panel_buffers(
                 self.h, c_void_p(self._bufs[0].data_ptr()), c_void_p(self._bufs[1].data_ptr()), need))
+        tneed = self.tail_geometry(N)["elems"]
+        if tneed > 0 and (self._tbuf is None or self._tbuf.numel() < tneed):
+            self._tbuf = torch.empty(tneed, dtype=torch.float64, device=dev)
+            self._check(self.lib.gaplac_dist_set_tail_buffer(self.h, c_void_p(self._tbuf.data_ptr()), tneed))
 
     def panel_tensor(self, s: int, count: int, ptr: int = None):
         """The torch view of panel s (count doubles at ptr, inside one of the two pair
@@ -133,6 +157,7 @@ class DistRank:
         nsp = c_int32()
         self._check(self.lib.gaplac_dist_begin(self.h, N, D, Xc.ctypes.data_as(c_void_p), max(N, 1), len(terms), ta,
                                                float(noise), v.ctypes.data_as(c_void_p), 0, byref(nsp)))
+        self._nseg = self.tail_geometry(N)["nseg"]
         return nsp.value
 
     def begin_device(self, N: int, D: int, dX_ptr: int, ldx: int, terms, noise: float, dv_ptr: int) -> int:
@@ -140,6 +165,7 @@ class DistRank:
         nsp = c_int32()
         self._check(self.lib.gaplac_dist_begin(self.h, N, D, c_void_p(dX_ptr), ldx, len(terms), term_array(terms),
                                                float(noise), c_void_p(dv_ptr), 1, byref(nsp)))
+        self._nseg = self.tail_geometry(N)["nseg"]
         return nsp.value
 
     def factor(self, s: int):
@@ -182,6 +208,34 @@ class DistRank:
 
     def update(self, s: int):
         self._check(self.lib.gaplac_dist_update(self.h, int(s)))
+
+    # ---- tail gather
+    def tail_segments(self) -> int:
+        """Segments of this evaluation's gather (0: none)."""
+        return self._nseg
+
+    def tail_segment(self, i: int):
+        ptr, count, src = c_void_p(), c_int64(), c_int32()
+        self._check(self.lib.gaplac_dist_tail_segment(self.h, int(i), byref(ptr), byref(count), byref(src)))
+        return ptr.value, count.value, src.value
+
+    def segment_tensor(self, i: int):
+        """The torch view of segment i in this rank's segment buffer."""
+        ptr, count, _src = self.tail_segment(i)
+        if not ptr or self._tbuf is None:
+            raise GaplacError(_native.E_ARG, f"tail segment {i} is not on rank {self.rank}")
+        off = (ptr - self._tbuf.data_ptr()) // 8
+        if off < 0 or off + count > self._tbuf.numel():
+            raise GaplacError(_native.E_ARG, f"tail segment {i} is outside the segment buffer")
+        return self._tbuf[off:off + count]
+
+    def tail_begin(self) -> int:
+        st = c_void_p()
+        self._check(self.lib.gaplac_dist_tail_begin(self.h, byref(st)))
+        return st.value or 0
+
+    def tail_end(self):
+        self._check(self.lib.gaplac_dist_tail_end(self.h))
 
     def finish(self):
         ld, q, info = c_double(), c_double(), c_int64()
@@ -251,6 +305,49 @@ class TorchTransport:
                 dist.broadcast(buf, src=src, group=self.group)
             r.comm_end_chunk(s, c)
 
+    def gather_tail(self, ranks: Sequence):
+        """The tail gather: this rank's segments to the root, or the root's receives, as one
+        batch of point-to-point ops on the library's comm stream (RCCL send / recv over
+        xGMI with the nccl backend: every sender's link runs at once). gloo's point-to-point
+        ops take host tensors, so with gloo a device segment goes through a host copy."""
+        import torch
+        import torch.distributed as dist
+        (r,) = ranks
+        n = r.tail_segments()
+        stream = r.tail_begin()
+        root = r.tail_root
+        ops = []
+        for i in range(n):
+            _ptr, _count, src = r.tail_segment(i)
+            if src == root or r.rank not in (src, root):
+                continue
+            peer = root if r.rank == src else src
+            gpeer = dist.get_global_rank(self.group, peer) if self.group is not None else peer
+            ops.append((dist.isend if r.rank == src else dist.irecv, r.segment_tensor(i), gpeer))
+        if ops:
+            t0 = ops[0][1]
+            st = torch.cuda.ExternalStream(stream, device=t0.device) if (stream and t0.is_cuda) else None
+            if st is not None and dist.get_backend(self.group) == "nccl":
+                with torch.cuda.stream(st):
+                    reqs = dist.batch_isend_irecv([dist.P2POp(op, t, peer, group=self.group) for op, t, peer in ops])
+                    for q in reqs:
+                        q.wait()
+            else:
+                if st is not None:
+                    st.synchronize()  # the packs
+                host = [t.cpu() if op is dist.isend else torch.empty(t.shape, dtype=t.dtype) for op, t, _ in ops]
+                reqs = [op(h, peer, group=self.group) for (op, _t, peer), h in zip(ops, host)]
+                for q in reqs:
+                    q.wait()
+                for (op, t, _), h in zip(ops, host):
+                    if op is dist.irecv:
+                        if st is not None:
+                            with torch.cuda.stream(st):
+                                t.copy_(h, non_blocking=False)
+                        else:
+                            t.copy_(h)
+        r.tail_end()
+
     def combine(self, parts: Sequence, device=None):
         import torch
         import torch.distributed as dist
@@ -308,6 +405,28 @@ class LoopbackTransport:
             for r in ranks:
                 r.comm_end_chunk(s, c)
 
+    def gather_tail(self, ranks: Sequence):
+        """Every sender's segments copied into the root's buffer on the root's comm stream
+        (after the sender's packs; the sender's stream then waits for the copy, so its buffer
+        is not re-packed before the copy has read it)."""
+        import torch
+        root = ranks[0].tail_root
+        rootr = next(r for r in ranks if r.rank == root)
+        streams = {r.rank: torch.cuda.ExternalStream(r.tail_begin(), device=torch.device("cuda", r.device))
+                   for r in ranks}
+        by_rank = {r.rank: r for r in ranks}
+        for i in range(rootr.tail_segments()):
+            _ptr, _count, src = rootr.tail_segment(i)
+            if src == root:
+                continue
+            st = streams[root]
+            st.wait_stream(streams[src])
+            with torch.cuda.stream(st):
+                rootr.segment_tensor(i).copy_(by_rank[src].segment_tensor(i), non_blocking=True)
+            streams[src].wait_stream(st)
+        for r in ranks:
+            r.tail_end()
+
     def combine(self, parts: Sequence, device=None):
         ld = sum(p[0] for p in parts)
         q = sum(p[1] for p in parts)
@@ -315,49 +434,53 @@ class LoopbackTransport:
         return ld, q, (min(infos) if infos else 0)
 
 
-def plan(nt: int, spw: int, depth: int, pair_m: int = 40):
-    """The library's step plan (gaplac_dist_plan, host-only): a list per step of
+def plan(nt: int, spw: int, depth: int, pair_m: int = 40, tail: int = 0):
+    """The library's step plan (gaplac_dist_plan_tail, host-only): a list per step of
     (kind, sp, first panel, last panel), kind 0 = that SP, 1 = every SP from it on, 2 = the
-    step's event once SP step+2 is up to date."""
+    step's event once SP step+2 is up to date. tail: the tail gather's tile columns (the
+    plan then has fewer steps than super-panels)."""
     lib = _native.load()
     n = c_int64()
-    rc = lib.gaplac_dist_plan(int(nt), int(spw), int(depth), int(pair_m), None, 0, byref(n))
+    rc = lib.gaplac_dist_plan_tail(int(nt), int(spw), int(depth), int(pair_m), int(tail), None, 0, byref(n))
     if rc != 0:
-        raise ArgumentError(f"gaplac_dist_plan({nt}, {spw}, {depth}) failed: {rc}")
+        raise ArgumentError(f"gaplac_dist_plan({nt}, {spw}, {depth}, tail={tail}) failed: {rc}")
     buf = (c_int32 * (5 * max(1, n.value)))()
-    lib.gaplac_dist_plan(int(nt), int(spw), int(depth), int(pair_m), buf, 5 * n.value, byref(n))
-    nsp = (nt + spw - 1) // spw
-    steps = [[] for _ in range(nsp)]
+    lib.gaplac_dist_plan_tail(int(nt), int(spw), int(depth), int(pair_m), int(tail), buf, 5 * n.value, byref(n))
+    nsteps = max((buf[5 * i] for i in range(n.value)), default=-1) + 1
+    steps = [[] for _ in range(nsteps)]
     for i in range(n.value):
         p, kind, g, pf, pl = buf[5 * i:5 * i + 5]
         steps[p].append((kind, g, pf, pl))
     return steps
 
 
-def plan_check(nt: int, spw: int, depth: int, pair_m: int = 40):
-    """gaplac_dist_plan_check: (ok, op count, message)."""
+def plan_check(nt: int, spw: int, depth: int, pair_m: int = 40, tail: int = 0):
+    """gaplac_dist_plan_check_tail: (ok, op count, message)."""
     lib = _native.load()
     ops = c_int64()
     msg = ctypes.create_string_buffer(256)
-    rc = lib.gaplac_dist_plan_check(int(nt), int(spw), int(depth), int(pair_m), byref(ops), msg, 256)
+    rc = lib.gaplac_dist_plan_check_tail(int(nt), int(spw), int(depth), int(pair_m), int(tail), byref(ops), msg, 256)
     return rc == 0, ops.value, msg.value.decode()
 
 
-def run_schedule(ranks: Sequence, transport, nsp: int):
-    """Enqueue one evaluation's factorisation on the local ranks (begin already called)."""
+def run_schedule(ranks: Sequence, transport, nsteps: int):
+    """Enqueue one evaluation's factorisation on the local ranks (begin already called and
+    returned nsteps): the distributed steps, then the tail gather when there is one."""
     for r in ranks:
         if r.owns(0):
             r.factor(0)
     transport.bcast(ranks, 0)
-    for s in range(nsp):
-        if s + 1 < nsp:
+    for s in range(nsteps):
+        if s + 1 < nsteps:
             for r in ranks:
                 if r.owns(s + 1):
                     r.factor(s + 1)
         for r in ranks:
             r.update(s)
-        if s + 1 < nsp:
+        if s + 1 < nsteps:
             transport.bcast(ranks, s + 1)
+    if ranks[0].tail_segments() > 0:
+        transport.gather_tail(ranks)
 
 
 def finish(ranks: Sequence, transport, N: int, device=None, full: bool = False):

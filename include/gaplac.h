@@ -332,6 +332,36 @@ int gaplac_dist_plan_check(int32_t nt, int32_t spw, int32_t depth, int32_t pair_
  * super-panel step+2 is up to date); *out_n = op count, out may be NULL. */
 int gaplac_dist_plan(int32_t nt, int32_t spw, int32_t depth, int32_t pair_m, int32_t* out, int64_t cap,
                      int64_t* out_n);
+/* Tail gather. tail_cols > 0: the super-panels whose columns all lie in
+ * the last tail_cols (<= 128) tile columns are not factored by the distributed steps. After
+ * the last step's update every rank sends its columns of that trailing matrix (from each
+ * super-panel's first row down) to rank `root`, which factors it with the single-GPU
+ * persistent tail; begin then returns the number of distributed steps (fewer than nsp).
+ * Per rank, after the step loop:
+ *   gaplac_dist_tail_begin(d, &stream);      packs this rank's segments on stream
+ *   for i in 0..nseg-1: gaplac_dist_tail_segment(d, i, &buf, &count, &src);
+ *       src == rank != root: ncclSend(buf, count, ncclDouble, root, comm, stream)
+ *       rank == root != src: ncclRecv(buf, count, ncclDouble, src, comm, stream)
+ *   (all inside one ncclGroupStart / ncclGroupEnd)
+ *   gaplac_dist_tail_end(d);                  the root factors the gathered matrix
+ * then finish as before (the root's partial sums include the tail's). The reference's
+ * logpdf is the same single evaluation (CLI/src/mcmc.jl:35); nothing in it is split. 0 = off
+ * (the default with one rank). Not in the reference. */
+int gaplac_dist_set_tail(gaplac_dist* d, int32_t tail_cols, int32_t root);
+/* For order N, before begin: segments of the gather (0: none), the doubles this rank's
+ * segment buffer needs, and the steps begin will return. */
+int gaplac_dist_tail_geometry(gaplac_dist* d, int64_t N, int32_t* nseg, int64_t* buf_elems,
+                              int32_t* nsteps);
+/* Optional caller-owned device segment buffer of >= buf_elems doubles (NULL: library-owned). */
+int gaplac_dist_set_tail_buffer(gaplac_dist* d, void* buf, int64_t capacity);
+int gaplac_dist_tail_segment(gaplac_dist* d, int32_t i, void** buf, int64_t* count, int32_t* src);
+int gaplac_dist_tail_begin(gaplac_dist* d, void** hip_stream);
+int gaplac_dist_tail_end(gaplac_dist* d);
+/* Host-only: the plan and its check with the tail gather of tail_cols tile columns. */
+int gaplac_dist_plan_check_tail(int32_t nt, int32_t spw, int32_t depth, int32_t pair_m, int32_t tail_cols,
+                                int64_t* out_ops, char* msg, int64_t msglen);
+int gaplac_dist_plan_tail(int32_t nt, int32_t spw, int32_t depth, int32_t pair_m, int32_t tail_cols,
+                          int32_t* out, int64_t cap, int64_t* out_n);
 /* Replay of one rank's schedule on one GPU (diagnostics): the other ranks'
  * panels arrive as copies from their (already factored) contexts on a modelled timeline.
  * replay_enable(N) before begin turns device timestamps on (0: off); replay_chunk replaces bcast's
@@ -342,6 +372,11 @@ int gaplac_dist_replay_chunk(gaplac_dist* d, const gaplac_dist* owner, int32_t s
                              int64_t f_ticks, int64_t band_ticks, int64_t lat_ticks,
                              int64_t xfer_ticks, int64_t copy_ticks);
 int gaplac_dist_replay_stamps(gaplac_dist* d, uint64_t* out, int64_t n);
+/* The tail gather on the replayed rank (in place of tail_begin / the transfers / tail_end):
+ * the root's segments from the owners' contexts of a loopback run with the same gather,
+ * released at END(last step) + lat + the largest sender's bytes x ticks_per_byte. */
+int gaplac_dist_replay_tail(gaplac_dist* d, const gaplac_dist* const* owners, int32_t nowners,
+                            int64_t lat_ticks, double ticks_per_byte, int64_t copy_ticks);
 int gaplac_dist_replay_info(gaplac_dist* d, int32_t s, int32_t c, int64_t* bytes, int32_t* per_step,
                             int32_t* maxc);
 

@@ -3,10 +3,11 @@
 It implements the same per-rank contract as gaplac_amd.distributed.DistRank (ownership,
 local column storage, group panel buffers of `depth` panels with their geometry and
 parity, broadcast chunks of `chunk` tile columns, the lookahead in factor(s+1), and the
-bulk updates of the library's own step plan, gaplac_dist_plan) with a smaller tile edge, so
-the orchestration in gaplac_amd/distributed.py (schedule order, per-chunk broadcast roots
-and counts, the combine) runs end to end under a gloo process group on CPU. Test
-infrastructure only; the Gram comes from the oracle restatement.
+bulk updates of the library's own step plan, gaplac_dist_plan_tail, and the tail gather's
+segments) with a smaller tile edge, so the orchestration in
+gaplac_amd/distributed.py (schedule order, per-chunk broadcast roots and counts, the gather,
+the combine) runs end to end under a gloo process group on CPU. Test infrastructure only;
+the Gram comes from the oracle restatement, the root's tail is a dense numpy Cholesky.
 """
 import numpy as np
 
@@ -16,12 +17,15 @@ from oracle import restatement as R
 
 class SimRank:
     def __init__(self, nranks: int, rank: int, spw: int = 2, nb: int = 16, depth: int = 2, chunk: int = None,
-                 pair_m: int = 2):
+                 pair_m: int = 2, tail: int = 0, tail_root: int = 0):
         self.nranks, self.rank, self.spw, self.nb = nranks, rank, spw, nb
         self.depth, self.cw, self.pair_m = depth, (chunk or spw), pair_m
+        self.tail, self.tail_root = tail, tail_root
         self.device = None
         self._bufs = None
+        self._tbuf = None
         self.applied = None  # per local tile column: panels applied, in order (checked by tests)
+        self.tail_part = None  # the root's (logdet, quad, info) of the gathered trailing matrix
 
     def owns(self, s):
         return s % self.nranks == self.rank
@@ -38,6 +42,88 @@ class SimRank:
         import torch
         need = self.geometry(N)["panel_elems"]
         self._bufs = [torch.zeros(need, dtype=torch.float64) for _ in range(2)]
+        self._tail_layout(N)
+        self._tbuf = torch.zeros(max(1, self._telems), dtype=torch.float64)
+
+    # ---- tail gather (gaplac_dist.hip: tail_stop_of / tail_geom)
+    def _tail_layout(self, N):
+        g = self.geometry(N)
+        nt, nsp, W, nb = g["nt"], g["nsp"], self.spw, self.nb
+        stop = -1
+        if self.tail > 0 and nt > self.tail:
+            stop = (nt - self.tail + W - 1) // W
+            if not (1 <= stop < nsp):
+                stop = -1
+        self.tstop = stop
+        self._tseg = []  # (offset, count) per segment, count 0 when not on this rank
+        self._telems = 0
+        if stop < 0:
+            return
+        self.tN0 = stop * W * nb
+        self.tNt = g["Np"] - self.tN0
+        for sp in range(stop, nsp):
+            i = sp - stop
+            here = self.rank == self.tail_root or sp % self.nranks == self.rank
+            c = min(W, nt - sp * W) * nb * (self.tNt - i * W * nb)
+            self._tseg.append((self._telems, c) if here else (0, 0))
+            if here:
+                self._telems += c
+
+    def tail_segments(self):
+        return len(self._tseg) if self.tstop >= 0 else 0
+
+    def tail_segment(self, i):
+        off, c = self._tseg[i]
+        return None, c, (self.tstop + i) % self.nranks
+
+    def segment_tensor(self, i):
+        off, c = self._tseg[i]
+        assert c > 0, (self.rank, i)
+        return self._tbuf[off:off + c]
+
+    def tail_begin(self):
+        W, nb = self.spw, self.nb
+        for i, (off, c) in enumerate(self._tseg):
+            sp = self.tstop + i
+            if not self.owns(sp):
+                continue
+            lc0 = (sp // self.nranks) * W
+            w = self._width(sp)
+            r0 = sp * W * nb
+            rows = self.tNt - i * W * nb
+            seg = self.C[r0:, lc0 * nb:(lc0 + w) * nb]  # rows x w*nb
+            self._tbuf[off:off + c] = __import__("torch").from_numpy(np.asfortranarray(seg).reshape(-1, order="F"))
+            assert seg.shape[0] == rows
+        return 0
+
+    def tail_end(self):
+        if self.rank != self.tail_root:
+            return
+        W, nb, N = self.spw, self.nb, self.N
+        Nt, N0 = self.tNt, self.tN0
+        T = np.zeros((Nt, Nt))
+        buf = self._tbuf.numpy()
+        for i, (off, c) in enumerate(self._tseg):
+            rows = Nt - i * W * nb
+            cols = c // rows
+            r0 = i * W * nb
+            T[r0:, r0:r0 + cols] = buf[off:off + c].reshape(cols, rows).T
+        info, ld, q = 0, 0.0, 0.0
+        for jj in range(Nt):
+            j = N0 + jj
+            piv = T[jj, jj]
+            if j >= N:
+                piv = 1.0
+            elif not piv > 0 and info == 0:
+                info = j + 1
+            d = np.sqrt(piv) if piv > 0 else np.nan
+            T[jj, jj] = d
+            T[jj + 1:, jj] /= d
+            T[jj + 1:, jj + 1:] -= np.outer(T[jj + 1:, jj], T[jj + 1:, jj])
+            if j < N:
+                ld += np.log(d)
+                q += T[N - N0, jj] ** 2
+        self.tail_part = (2 * ld, q, info)
 
     # ---- panel geometry (gaplac_dist.hip: group_* / chunk_*)
     def _width(self, s):
@@ -99,9 +185,12 @@ class SimRank:
             bj = self.gcol(lj)
             self.C[:, lj * nb:(lj + 1) * nb] = A[:, bj * nb:(bj + 1) * nb]
         self.info = 0
-        self.plan = DI.plan(self.nt, self.spw, self.depth, self.pair_m)
+        self.plan = DI.plan(self.nt, self.spw, self.depth, self.pair_m, self.tail)
+        self._tail_layout(N)
+        assert len(self.plan) == (self.tstop if self.tstop >= 0 else self.nsp)
         self.applied = [[] for _ in range(self.nloc)]
-        return self.nsp
+        self.tail_part = None
+        return len(self.plan)
 
     def _apply(self, q, lj0, ncols):
         """C[:, local tile cols lj0..lj0+ncols) -= panel q's contributions (rows >= column)."""
@@ -160,15 +249,25 @@ class SimRank:
 
     def finish(self):
         nb, N = self.nb, self.N
-        # every local column got every earlier panel exactly once, in order
+        stop = self.tstop if self.tstop >= 0 else self.nsp
+        # every local column got every earlier panel exactly once, in order (a gathered SP:
+        # every distributed panel)
         for lj in range(self.nloc):
             sp = self.gcol(lj) // self.spw
-            assert self.applied[lj] == list(range(sp)), (lj, self.applied[lj])
+            assert self.applied[lj] == list(range(min(sp, stop))), (lj, self.applied[lj])
         ld = q = 0.0
+        info = self.info
+        if self.tstop >= 0 and self.rank == self.tail_root:
+            assert self.tail_part is not None, "the gather was not completed"
+            ld, q, ti = self.tail_part[0] / 2, self.tail_part[1], self.tail_part[2]
+            if ti and (info == 0 or ti < info):
+                info = ti
         for lj in range(self.nloc):
+            if self.gcol(lj) // self.spw >= stop:
+                continue
             for e in range(nb):
                 j = self.gcol(lj) * nb + e
                 if j < N:
                     ld += np.log(self.C[j, lj * nb + e])
                     q += self.C[N, lj * nb + e] ** 2
-        return 2 * ld, q, self.info
+        return 2 * ld, q, info

@@ -32,6 +32,18 @@ class CpuLoopback(DI.LoopbackTransport):
                 if r.rank != root:
                     r.chunk_tensor(s, c).copy_(src)
 
+    def gather_tail(self, ranks):
+        for r in ranks:
+            r.tail_begin()
+        root = ranks[0].tail_root
+        rootr = next(r for r in ranks if r.rank == root)
+        for i in range(rootr.tail_segments()):
+            _p, _c, src = rootr.tail_segment(i)
+            if src != root:
+                rootr.segment_tensor(i).copy_(next(r for r in ranks if r.rank == src).segment_tensor(i))
+        for r in ranks:
+            r.tail_end()
+
 
 def _case(N, seed=0):
     rng = np.random.default_rng(seed)
@@ -57,6 +69,43 @@ def test_loopback_schedule_matches_oracle(world, spw, N, depth, chunk):
     assert abs(lp - rl) <= RTOL * abs(rl)
     assert abs(ld - rd) <= 1e-9 * max(1.0, abs(rd))
     assert abs(q - rq) <= 1e-9 * max(1.0, abs(rq))
+
+
+@pytest.mark.parametrize("world,spw,N,depth,chunk,tail,root", [
+    (1, 2, 150, 2, 2, 4, 0), (2, 2, 150, 2, 1, 5, 1), (3, 1, 200, 1, 1, 6, 2), (4, 2, 257, 4, 1, 8, 0),
+    (5, 3, 95, 3, 2, 3, 4), (8, 1, 40, 2, 1, 1, 0), (2, 4, 600, 4, 1, 12, 0), (3, 4, 600, 3, 3, 16, 1),
+    (8, 2, 700, 4, 2, 20, 0), (2, 3, 400, 8, 3, 7, 1), (4, 4, 700, 2, 2, 30, 3), (8, 4, 1300, 2, 2, 40, 0)])
+def test_loopback_tail_gather_matches_oracle(world, spw, N, depth, chunk, tail, root):
+    """The tail gather: the plan stops before the super-panels of the last
+    `tail` tile columns; every rank's columns of the trailing matrix go to `root`, which
+    factors them. Every distributed column got every panel once, in order; the gathered
+    ones every distributed panel; the oracle's logpdf."""
+    X, terms, v = _case(N, seed=world + tail)
+    ranks = [SimRank(world, r, spw=spw, nb=16, depth=depth, chunk=chunk, tail=tail, tail_root=root)
+             for r in range(world)]
+    lp, ld, q = DI.logpdf_dist(ranks, CpuLoopback(), X, terms, 0.1, v, full=True)
+    assert ranks[0].tstop > 0 and ranks[0].tail_segments() > 0
+    rl, rd, rq = R.logpdf(X, terms, 0.1, v)
+    assert abs(lp - rl) <= RTOL * abs(rl)
+    assert abs(ld - rd) <= 1e-9 * max(1.0, abs(rd))
+    assert abs(q - rq) <= 1e-9 * max(1.0, abs(rq))
+
+
+def test_loopback_tail_gather_non_pd_pivot_in_tail():
+    """A failing pivot inside the gathered matrix is reported as its global (j + 1)."""
+    rng = np.random.default_rng(5)
+    N = 90
+    g = rng.integers(0, 10, N).astype(float)
+    X = g[:, None]
+    v = rng.standard_normal(N)
+    terms = [(4, 0, 0.0, 0)]
+    with pytest.raises(R.PosDefException) as ref:
+        R.logpdf(X, terms, 0.0, v)
+    for tail in (2, 5):
+        ranks = [SimRank(3, r, spw=1, nb=16, tail=tail, tail_root=1) for r in range(3)]
+        with pytest.raises(PosDefException) as got:
+            DI.logpdf_dist(ranks, CpuLoopback(), X, terms, 0.0, v)
+        assert got.value.info == ref.value.info
 
 
 def test_loopback_more_ranks_than_superpanels():
@@ -135,15 +184,16 @@ class RecordingTransport(DI.TorchTransport):
         super().bcast(ranks, s)
 
 
-def _worker_defaults(rank, world, port, q, N, spw):
+def _worker_defaults(rank, world, port, q, N, spw, tail=0):
     """One rank of a gloo job at the multi-rank defaults (depth 2, chunk 2): logpdf, and the
-    broadcast sequence every rank issued, gathered on rank 0."""
+    broadcast sequence every rank issued, gathered on rank 0. tail > 0: with the tail gather
+    onto the last rank (gloo isend / irecv through TorchTransport.gather_tail)."""
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         X, terms, v = _case(N, seed=world)
-        r = SimRank(world, rank, spw=spw, nb=16, depth=2, chunk=2)
+        r = SimRank(world, rank, spw=spw, nb=16, depth=2, chunk=2, tail=tail, tail_root=world - 1)
         tr = RecordingTransport()
         lp = DI.logpdf_dist([r], tr, X, terms, 0.1, v)
         seqs = [None] * world
@@ -155,8 +205,8 @@ def _worker_defaults(rank, world, port, q, N, spw):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [4, 8])
-def test_gloo_rehearsal_multirank_defaults(world):
+@pytest.mark.parametrize("world,tail", [(4, 0), (8, 0), (4, 12), (8, 12)])
+def test_gloo_rehearsal_multirank_defaults(world, tail):
     """VERDICT r05 #2a: the configs[3] job's rank counts on CPU, through TorchTransport at
     the P > 1 defaults (deferral depth 2, broadcast chunks of 2 tile columns, so every
     panel goes out in two chunks): every rank issues the same broadcast sequence (step,
@@ -165,7 +215,7 @@ def test_gloo_rehearsal_multirank_defaults(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_defaults, args=(r, world, port, q, N, spw)) for r in range(world)]
+    procs = [ctx.Process(target=_worker_defaults, args=(r, world, port, q, N, spw, tail)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=240) for _ in procs]
@@ -182,19 +232,33 @@ def test_gloo_rehearsal_multirank_defaults(world):
             seqs = extra
     assert len(seqs) == world
     assert all(sq == seqs[0] for sq in seqs), "ranks issued different broadcast sequences"
-    nsp = (N + 1 + 15) // 16 // spw + (1 if ((N + 1 + 15) // 16) % spw else 0)
-    assert [x[:3] for x in seqs[0]] == [(s, c, s % world) for s in range(nsp) for c in range(2)]
+    nt = (N + 1 + 15) // 16
+    nsp = nt // spw + (1 if nt % spw else 0)
+    nsteps = (nt - tail + spw - 1) // spw if tail else nsp  # 8 with 12 gathered tile columns
+    assert [x[:3] for x in seqs[0]] == [(s, c, s % world) for s in range(nsteps) for c in range(2)]
 
 
 @pytest.mark.parametrize("depth", [1, 2, 3, 4, 5, 8])
 @pytest.mark.parametrize("spw", [1, 2, 4, 8])
 def test_plan_check_every_size(depth, spw):
     """gaplac_dist_plan_check over every matrix size up to 600 tile columns (N = 76800) and
-    the deferral cut-offs the library reads (GAPLAC_PAIR_M)."""
+    the deferral cut-offs the library reads (GAPLAC_PAIR_M), without and with the tail
+    gather (every SP from the stop on ends with every distributed panel)."""
     for pair_m in (0, 8, 40):
-        for nt in range(1, 601):
-            ok, ops, msg = DI.plan_check(nt, spw, depth, pair_m)
-            assert ok, (nt, spw, depth, pair_m, msg)
+        for tail in (0, 1, 5, 40, 80, 128):
+            for nt in range(1, 601):
+                ok, ops, msg = DI.plan_check(nt, spw, depth, pair_m, tail)
+                assert ok, (nt, spw, depth, pair_m, tail, msg)
+
+
+def test_plan_tail_stops_before_the_tail():
+    """N = 65536 (513 tile columns), W = 4, 80 gathered tile columns: 109 distributed steps
+    (super-panels 109 .. 128 = the last 77 tile columns are gathered), and the last step
+    also brings SP 109 up to date with its own panel."""
+    steps = DI.plan(513, 4, 4, 40, 80)
+    assert len(steps) == 109
+    assert (0, 109, 108, 108) in steps[-1]
+    assert len(DI.plan(513, 4, 4, 40, 0)) == 129
 
 
 def test_plan_defers_in_groups():

@@ -157,7 +157,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, tail=-1):
     try:
         import torch
         import torch.distributed as dist
@@ -165,7 +165,7 @@ def _worker(rank, world, port, q):
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         X, terms, v = _case(2500, seed=21)
-        r = DI.DistRank(0, world, rank, spw=2)
+        r = DI.DistRank(0, world, rank, spw=2, tail=tail, tail_root=world - 1)
         lp = DI.logpdf_dist([r], DI.TorchTransport(), X, terms, 0.1, v)
         r.close()
         dist.destroy_process_group()
@@ -174,12 +174,15 @@ def _worker(rank, world, port, q):
         q.put((rank, None, repr(e)))
 
 
-def test_gloo_world2_processes_share_one_gpu():
+@pytest.mark.parametrize("tail", [0, 12])
+def test_gloo_world2_processes_share_one_gpu(tail):
+    """tail 12: the tail gather through TorchTransport.gather_tail (gloo: host copies of the
+    segments), onto rank 1."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, tail)) for r in range(2)]
     for p in procs:
         p.start()
     got = [q.get(timeout=100) for _ in procs]
@@ -209,3 +212,81 @@ def test_loopback_multirank_defaults_match_single_gpu(world, spw, N, big):
         assert abs(got - ref) <= 1e-11 * abs(ref)
     for r in ranks:
         r.close()
+
+
+# ---- tail gather ----
+
+@pytest.mark.parametrize("world,spw,N,tail,root", [
+    (1, 4, 3000, 8, 0), (2, 1, 1000, 3, 1), (3, 2, 1500, 5, 2), (4, 2, 2100, 10, 0), (8, 1, 1100, 4, 5),
+    (3, 1, 700, 5, 1)])
+def test_loopback_tail_gather_matches_oracle(world, spw, N, tail, root):
+    """The super-panels of the last `tail` tile columns are gathered onto `root` and factored
+    by the persistent tail there; against the oracle at 1e-12."""
+    X, terms, v = _case(N, seed=world * 11 + tail)
+    ranks = [DI.DistRank(0, world, r, spw=spw, tail=tail, tail_root=root) for r in range(world)]
+    assert ranks[0].tail_geometry(N)["nseg"] > 0
+    lp, ld, q = DI.logpdf_dist(ranks, DI.LoopbackTransport(), X, terms, 0.1, v, full=True)
+    rl, rd, rq = R.logpdf(X, terms, 0.1, v)
+    assert abs(lp - rl) <= 1e-12 * max(1.0, abs(rl))
+    assert abs(ld - rd) <= 1e-9 * max(1.0, abs(rd))
+    assert abs(q - rq) <= 1e-9 * max(1.0, abs(rq))
+    for r in ranks:
+        r.close()
+
+
+@pytest.mark.parametrize("world,spw,N,tail,root", [
+    (4, 4, 16384, 80, 0), (8, 2, 12000, 40, 7), (2, 4, 14000, 128, 1), (8, 4, 20000, 77, 3)])
+def test_loopback_tail_gather_large_matches_single_gpu(world, spw, N, tail, root):
+    """At the P > 1 defaults (chain alone, held ops, chunks of 2, per-rank bulk kernel: every
+    rank keeps its options) with the gathered tail up to its 128-column maximum; against the
+    single-GPU path at 1e-11, twice through the same workspaces."""
+    X, terms, v = _case(N, seed=N + tail)
+    with Context(0) as ctx:
+        ref = ctx.logpdf(X, terms, 0.1, v)
+    ranks = [DI.DistRank(0, world, r, spw=spw, depth=2, chunk=2, big=1, alone=1, tail=tail, tail_root=root)
+             for r in range(world)]
+    tr = DI.LoopbackTransport(keep_options=True)
+    for _ in range(2):
+        got = DI.logpdf_dist(ranks, tr, X, terms, 0.1, v)
+        assert abs(got - ref) <= 1e-11 * abs(ref)
+    for r in ranks:
+        r.close()
+
+
+def test_loopback_tail_gather_non_pd_info_in_the_tail():
+    """A first failing pivot inside the gathered matrix (a repeated category at j = 400, tile
+    column 3 of 6, the tail = columns 3..5) comes back as its global j + 1."""
+    N = 700
+    rng = np.random.default_rng(3)
+    cats = np.concatenate([np.arange(400), rng.integers(0, 400, N - 400)]).astype(float)
+    X = cats[:, None]
+    v = rng.standard_normal(N)
+    terms = [(4, 0, 0.0, 0)]
+    with pytest.raises(R.PosDefException) as ref:
+        R.logpdf(X, terms, 0.0, v)
+    assert ref.value.info == 401
+    ranks = [DI.DistRank(0, 3, r, spw=1, tail=3, tail_root=2) for r in range(3)]
+    assert ranks[0].tail_geometry(N)["nsteps"] == 3
+    with pytest.raises(PosDefException) as got:
+        DI.logpdf_dist(ranks, DI.LoopbackTransport(), X, terms, 0.0, v)
+    assert got.value.info == 401
+
+
+def test_tail_gather_options_and_reuse():
+    """set_tail validation; the gather toggled between evaluations on the same contexts."""
+    from gaplac_amd.backend import ArgumentError
+    r = DI.DistRank(0, 2, 0, spw=2)
+    with pytest.raises(ArgumentError):
+        r.set_tail(129)
+    with pytest.raises(ArgumentError):
+        r.set_tail(8, root=2)
+    r.close()
+    X, terms, v = _case(2600, seed=4)
+    rl = R.logpdf(X, terms, 0.1, v)[0]
+    ranks = _ranks(3, 2)
+    tr = DI.LoopbackTransport()
+    for tail in (0, 6, 0, 10, 20):
+        for r in ranks:
+            r.set_tail(tail, 1)
+        lp = DI.logpdf_dist(ranks, tr, X, terms, 0.1, v)
+        assert abs(lp - rl) <= 1e-12 * abs(rl), tail

@@ -3,7 +3,10 @@ replaying one rank's schedule against a modelled link (gaplac_amd/dist_replay.py
 DESIGN.md §7.3).
 
     python tools/dist_replay.py --N 65536 --ranks 8 --local 0 7 --bw 100 200 300 \
-        --depth 2 4 --chunk 1 4 --out gpurun_out/r05_dist_replay.jsonl
+        --depth 2 4 --chunk 1 4 --tail 0 80 --out gpurun_out/r05_dist_replay.jsonl
+
+--tail: the tail gather's tile columns (0 = off), onto rank 0; each value
+gets its own loopback run (the owners' segment buffers hold that gather's segments).
 
 First an in-process loopback run of the whole job factors every rank's columns (the
 panels the replayed rank receives), then for every option set the replayed rank runs
@@ -33,6 +36,8 @@ def main():
     ap.add_argument("--chunk", type=int, nargs="+", default=[4])
     ap.add_argument("--big", type=int, nargs="+", default=[1])
     ap.add_argument("--alone", type=int, nargs="+", default=[0])
+    ap.add_argument("--tail", type=int, nargs="+", default=[0])
+    ap.add_argument("--gbw", type=float, nargs="+", default=[50.0], help="gather GB/s per sender link")
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--steps", action="store_true", help="include the per-step table")
     ap.add_argument("--single", action="store_true", help="also time the single-GPU path on the input")
@@ -71,34 +76,45 @@ def main():
             single_ms = (time.perf_counter() - t0) * 1e3
         emit(dict(kind="single", N=N, ms=single_ms, logpdf=lp_single))
 
-    # the loopback job: every rank's factored columns (the owners of the replayed panels)
-    t0 = time.perf_counter()
-    owners = [DI.DistRank(0, a.ranks, r, spw=4) for r in range(a.ranks)]
-    lp_loop = DI.logpdf_dist_device(owners, DI.LoopbackTransport(), N, 1, dx.data_ptr(), N, terms, CF.NOISE_VAR,
-                                    dv.data_ptr())
-    parts = {r.rank: r.finish() for r in owners}
-    emit(dict(kind="loopback", N=N, ranks=a.ranks, logpdf=lp_loop, s=time.perf_counter() - t0))
+    for tail in a.tail:
+        # the loopback job: every rank's factored columns (the owners of the replayed panels)
+        t0 = time.perf_counter()
+        owners = [DI.DistRank(0, a.ranks, r, spw=4, tail=tail) for r in range(a.ranks)]
+        lp_loop = DI.logpdf_dist_device(owners, DI.LoopbackTransport(), N, 1, dx.data_ptr(), N, terms, CF.NOISE_VAR,
+                                        dv.data_ptr())
+        parts = {r.rank: r.finish() for r in owners}
+        emit(dict(kind="loopback", N=N, ranks=a.ranks, tail=tail, logpdf=lp_loop, s=time.perf_counter() - t0))
+        replays(a, owners, parts, tail, N, dx, dv, terms, single_ms, emit)
+        for r in owners:
+            r.close()
 
+
+def replays(a, owners, parts, tail, N, dx, dv, terms, single_ms, emit):
+    from gaplac_amd import configs as CF
+    from gaplac_amd import distributed as DI
+    from gaplac_amd import dist_replay as RP
     for rank, depth, chunk, big, alone in itertools.product(a.local, a.depth, a.chunk, a.big, a.alone):
-        rep = DI.DistRank(0, a.ranks, rank, spw=4, depth=depth, chunk=chunk, big=big, alone=alone)
-        for bw in a.bw:
-            model = RP.ReplayModel(bw_GBps=bw, lat_us=a.lat)
+        rep = DI.DistRank(0, a.ranks, rank, spw=4, depth=depth, chunk=chunk, big=big, alone=alone, tail=tail)
+        for bw, gbw in itertools.product(a.bw, a.gbw if tail else a.gbw[:1]):
+            model = RP.ReplayModel(bw_GBps=bw, lat_us=a.lat, gather_bw_GBps=gbw)
             F = band = None
-            copy = 0
+            copy = tcopy = 0
             hist = []
             res = None
             for it in range(a.iters):
                 res = RP.replay_rank(owners, rep, N, 1, dx.data_ptr(), terms, CF.NOISE_VAR, dv.data_ptr(), model,
-                                     F=F, band=band, copy_ticks=copy)
+                                     F=F, band=band, copy_ticks=copy, tail_copy_ticks=tcopy)
                 hist.append(round(res["wall_s"] * 1e3, 2))
                 F, band = RP.next_inputs(res)
                 copy = int(res["copy_mean"])
+                tcopy = int(res["tail_copy"])
             ld0, q0, _ = parts[rank]
             rows = RP.step_table(res, a.ranks, rank)
             idle = [r["main_idle_us"] for r in rows]
             f_own = {s: [round(t * 0.01, 1) for t in v] for s, v in res["f_meas"].items()}
             d = dict(kind="replay", N=N, ranks=a.ranks, rank=rank, depth=depth, chunk=chunk, big=big, alone=alone, bw_GBps=bw,
-                     lat_us=a.lat, iters_ms=hist, predicted_ms=hist[-1],
+                     lat_us=a.lat, tail=tail, gather_bw_GBps=gbw if tail else None, tail_stamps=res["tail"],
+                     iters_ms=hist, predicted_ms=hist[-1],
                      speedup_vs_single=(single_ms / hist[-1]) if single_ms else None,
                      logdet_part_equal=res["logdet_part"] == ld0, quad_part_equal=res["quad_part"] == q0,
                      logdet_part_rel=abs(res["logdet_part"] - ld0) / max(1e-300, abs(ld0)),
@@ -111,8 +127,6 @@ def main():
                 d["steps"] = rows
             emit(d)
         rep.close()
-    for r in owners:
-        r.close()
 
 
 if __name__ == "__main__":
