@@ -193,7 +193,7 @@ def load() -> ctypes.CDLL:
     lib.gaplac_dist_replay_chunk.argtypes = [c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int64, c_int64,
                                              c_int64, c_int64]
     lib.gaplac_dist_replay_stamps.argtypes = [c_void_p, c_void_p, c_int64]
-    lib.gaplac_dist_replay_tail.argtypes = [c_void_p, c_void_p, c_int32, c_int64, c_double, c_int64]
+    lib.gaplac_dist_replay_tail.argtypes = [c_void_p, c_void_p, c_int32, c_int64, c_double, c_int64, c_int64]
     lib.gaplac_dist_replay_info.argtypes = [c_void_p, c_int32, c_int32, _I64P, _I32P, _I32P]
     for name in EXPORTED:
         getattr(lib, name).restype = getattr(lib, name).restype or c_int

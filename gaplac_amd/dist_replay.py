@@ -81,11 +81,14 @@ def _interp(samples: dict, nsp: int, default: float) -> np.ndarray:
 
 
 def replay_rank(owners, rep: DI.DistRank, N: int, D: int, dX_ptr: int, terms, noise: float, dv_ptr: int,
-                model: ReplayModel, F=None, band=None, copy_ticks: int = 0, tail_copy_ticks: int = 0):
+                model: ReplayModel, F=None, band=None, copy_ticks: int = 0, tail_copy_ticks: int = 0,
+                senders_end_us: float = 0.0):
     """One replayed evaluation of rank rep.rank. owners[q]: the factored loopback context of
     rank q (a loopback run with the same tail gather). F[s][c], band[s]: model inputs in
-    ticks (None: a first guess). Returns a dict of the time, the stamps and the measured
-    inputs for the next iteration."""
+    ticks (None: a first guess). senders_end_us: the root's gather waits for the latest
+    sender's last update, from that rank's replay (its tail["steps_end_us"]; 0: this rank's
+    own). Returns a dict of the time, the stamps and the measured inputs for the next
+    iteration."""
     import torch
     rep._check(rep.lib.gaplac_dist_replay_enable(rep.h, int(N)))
     torch.cuda.synchronize()
@@ -123,7 +126,7 @@ def replay_rank(owners, rep: DI.DistRank, N: int, D: int, dX_ptr: int, terms, no
     if gathered:
         arr = (c_void_p * P)(*[o.h.value for o in owners])
         rep._check(rep.lib.gaplac_dist_replay_tail(rep.h, arr, P, lat, model.gather_ticks_per_byte(),
-                                                   int(tail_copy_ticks)))
+                                                   int(tail_copy_ticks), int(round(senders_end_us * 100))))
     ld, q, info = rep.finish()
     wall = time.perf_counter() - t0
     st, maxc, extra = _stamps(rep, nsp_all)

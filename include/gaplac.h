@@ -374,9 +374,12 @@ int gaplac_dist_replay_chunk(gaplac_dist* d, const gaplac_dist* owner, int32_t s
 int gaplac_dist_replay_stamps(gaplac_dist* d, uint64_t* out, int64_t n);
 /* The tail gather on the replayed rank (in place of tail_begin / the transfers / tail_end):
  * the root's segments from the owners' contexts of a loopback run with the same gather,
- * released at END(last step) + lat + the largest sender's bytes x ticks_per_byte. */
+ * released at max(END(last step), Gram end + senders_end) + lat + the largest sender's
+ * bytes x ticks_per_byte (senders_end: the latest sender's last update end in its own
+ * replay, relative to its Gram end; 0 = this rank's own END). */
 int gaplac_dist_replay_tail(gaplac_dist* d, const gaplac_dist* const* owners, int32_t nowners,
-                            int64_t lat_ticks, double ticks_per_byte, int64_t copy_ticks);
+                            int64_t lat_ticks, double ticks_per_byte, int64_t copy_ticks,
+                            int64_t senders_end);
 int gaplac_dist_replay_info(gaplac_dist* d, int32_t s, int32_t c, int64_t* bytes, int32_t* per_step,
                             int32_t* maxc);
 

@@ -7,6 +7,9 @@ DESIGN.md §7.3).
 
 --tail: the tail gather's tile columns (0 = off), onto rank 0; each value
 gets its own loopback run (the owners' segment buffers hold that gather's segments).
+--job: replay every rank (the gather's root last, its gather released after the latest
+sender's last update from the other replays) and emit the job's prediction (the max over
+ranks) per tail length, with the first value of every option list.
 
 First an in-process loopback run of the whole job factors every rank's columns (the
 panels the replayed rank receives), then for every option set the replayed rank runs
@@ -40,6 +43,7 @@ def main():
     ap.add_argument("--gbw", type=float, nargs="+", default=[50.0], help="gather GB/s per sender link")
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--steps", action="store_true", help="include the per-step table")
+    ap.add_argument("--job", action="store_true", help="every rank, and the job's prediction")
     ap.add_argument("--single", action="store_true", help="also time the single-GPU path on the input")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -84,9 +88,56 @@ def main():
                                         dv.data_ptr())
         parts = {r.rank: r.finish() for r in owners}
         emit(dict(kind="loopback", N=N, ranks=a.ranks, tail=tail, logpdf=lp_loop, s=time.perf_counter() - t0))
-        replays(a, owners, parts, tail, N, dx, dv, terms, single_ms, emit)
+        if a.job:
+            job(a, owners, parts, tail, N, dx, dv, terms, emit)
+        else:
+            replays(a, owners, parts, tail, N, dx, dv, terms, single_ms, emit)
         for r in owners:
             r.close()
+
+
+def _replay(a, owners, rank, tail, N, dx, dv, terms, model, senders_end_us=0.0):
+    from gaplac_amd import configs as CF
+    from gaplac_amd import distributed as DI
+    from gaplac_amd import dist_replay as RP
+    rep = DI.DistRank(0, a.ranks, rank, spw=4, depth=a.depth[0], chunk=a.chunk[0], big=a.big[0], alone=a.alone[0],
+                      tail=tail)
+    F = band = None
+    copy = tcopy = 0
+    hist = []
+    for it in range(a.iters):
+        res = RP.replay_rank(owners, rep, N, 1, dx.data_ptr(), terms, CF.NOISE_VAR, dv.data_ptr(), model, F=F,
+                             band=band, copy_ticks=copy, tail_copy_ticks=tcopy, senders_end_us=senders_end_us)
+        hist.append(round(res["wall_s"] * 1e3, 2))
+        F, band = RP.next_inputs(res)
+        copy = int(res["copy_mean"])
+        tcopy = int(res["tail_copy"])
+    rows = RP.step_table(res, a.ranks, rank)
+    rep.close()
+    return res, hist, rows
+
+
+def job(a, owners, parts, tail, N, dx, dv, terms, emit):
+    """Every rank replayed; the root (rank 0) last, its gather released after the latest
+    sender's last update."""
+    from gaplac_amd import dist_replay as RP
+    model = RP.ReplayModel(bw_GBps=a.bw[0], lat_us=a.lat, gather_bw_GBps=a.gbw[0])
+    ranks = list(range(1, a.ranks)) + [0]
+    per = {}
+    senders_end = 0.0
+    for rank in ranks:
+        res, hist, rows = _replay(a, owners, rank, tail, N, dx, dv, terms, model,
+                                  senders_end_us=senders_end if rank == 0 else 0.0)
+        ld0, q0, _ = parts[rank]
+        per[rank] = dict(predicted_ms=hist[-1], iters_ms=hist, steps_end_ms=round(rows[-1]["upd_end_us"] / 1e3, 3),
+                         parts_equal=bool(res["logdet_part"] == ld0 and res["quad_part"] == q0), tail=res["tail"])
+        if rank != 0 and tail:
+            senders_end = max(senders_end, res["tail"]["steps_end_us"])
+    pred = max(v["predicted_ms"] for v in per.values())
+    emit(dict(kind="job", N=N, ranks=a.ranks, tail=tail, bw_GBps=a.bw[0], gather_bw_GBps=a.gbw[0] if tail else None,
+              depth=a.depth[0], chunk=a.chunk[0], big=a.big[0], alone=a.alone[0], predicted_ms=pred,
+              slowest=max(per, key=lambda r: per[r]["predicted_ms"]), senders_end_ms=round(senders_end / 1e3, 3),
+              per_rank=per))
 
 
 def replays(a, owners, parts, tail, N, dx, dv, terms, single_ms, emit):
