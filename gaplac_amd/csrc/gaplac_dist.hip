@@ -134,6 +134,7 @@ struct gaplac_dist {
     size_t ttasks_elems = 0;
     int ttasks_n = 0, ttasks_T = -1;
     int ncu = 256;
+    int tail_sim = -1;  // GAPLAC_TAIL_SIM, as the single-GPU path reads it
     bool tail_ended = false;
     hipEvent_t ev_tail = nullptr;  // s_main: the last update done; s_comm: the gather's transfers enqueued
     int held_step = -1;   // alone: the step whose ops after its mark wait for the next update
@@ -520,6 +521,7 @@ int gaplac_dist_create(int device, int nranks, int rank, int spw, gaplac_dist** 
     if (const char* e = std::getenv("GAPLAC_DIST_CHUNK")) d->cw = std::max(1, std::min(spw, std::atoi(e)));
     if (const char* e = std::getenv("GAPLAC_DIST_BIG")) d->big_mode = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("GAPLAC_DIST_ALONE")) d->alone = std::atoi(e) > 0;
+    if (const char* e = std::getenv("GAPLAC_TAIL_SIM")) d->tail_sim = e[0] == '0' ? 0 : 1;
     {
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
@@ -710,7 +712,7 @@ int gaplac_dist_begin(gaplac_dist* d, int64_t N, int32_t D, const double* X, int
             if (!d->tctl) DCK(d, hipMalloc(reinterpret_cast<void**>(&d->tctl), sizeof(TailCtl)));
             if (d->ttasks_T != T) {
                 std::vector<uint32_t> host;
-                build_single_tail_list(T, 0, -1, d->ncu, host);
+                build_single_tail_list(T, 0, d->tail_sim, d->ncu, host);
                 if ((rc = dgrow(d, &d->ttasks, &d->ttasks_elems, host.size()))) return rc;
                 DCK(d, hipMemcpy(d->ttasks, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
                 d->ttasks_n = (int)host.size();
@@ -1322,14 +1324,15 @@ int gaplac_dist_replay_chunk(gaplac_dist* d, const gaplac_dist* src, int32_t s, 
 
 // Modelled tail gather on the replayed rank, in place of the host's sends / receives
 // (between tail_begin and tail_end, which this calls). Every sender's segments leave when
-// its last update is done, taken as this rank's own (every rank's s_main runs the same
-// steps), over its own link: the root's receives arrive at
-//   END(last step) + lat + max over senders of (its bytes) x ticks_per_byte
-// as copies from the owners' segment buffers (owners[q]: rank q's context of a loopback
-// run with the same gather; copy_ticks of the copies are taken off the wait). A sender's
-// own sends end at END(last step) + lat + its bytes x ticks_per_byte (stamped only).
+// its last update is done, over its own link: the root's receives arrive at
+//   max(END(last step), Gram end + senders_end) + lat + max over senders of (bytes) x ticks_per_byte
+// where senders_end is the latest sender's last update end, from that rank's own replay,
+// relative to its Gram end (0: taken as this rank's own END), as copies from the owners'
+// segment buffers (owners[q]: rank q's context of a loopback run with the same gather;
+// copy_ticks of the copies are taken off the wait). A sender's own sends end at
+// END(last step) + lat + its bytes x ticks_per_byte (stamped only).
 int gaplac_dist_replay_tail(gaplac_dist* d, const gaplac_dist* const* owners, int32_t nowners, int64_t lat_ticks,
-                            double ticks_per_byte, int64_t copy_ticks) {
+                            double ticks_per_byte, int64_t copy_ticks, int64_t senders_end) {
     if (!d || !d->stamps || d->tstop < 0 || !owners || nowners != d->nranks)
         return derr(d, GAPLAC_E_ARG, "replay_tail: needs stamps, a gather and every rank's context");
     void* st = nullptr;
@@ -1343,8 +1346,9 @@ int gaplac_dist_replay_tail(gaplac_dist* d, const gaplac_dist* const* owners, in
         if (src != d->tail_root) bytes[(size_t)src] += c;
     }
     const int64_t sent = root ? *std::max_element(bytes.begin(), bytes.end()) : bytes[(size_t)d->rank];
-    Release r{{st_end(d->nsteps - 1), -1, -1}, {lat_ticks + (long long)(sent * ticks_per_byte) - (root ? copy_ticks : 0), 0, 0},
-              d->nsp * ST_PER_STEP + 1};
+    const long long xfer = lat_ticks + (long long)(sent * ticks_per_byte) - (root ? copy_ticks : 0);
+    Release r{{st_end(d->nsteps - 1), root && senders_end > 0 ? d->nsp * ST_PER_STEP : -1, -1},
+              {xfer, senders_end + xfer, 0}, d->nsp * ST_PER_STEP + 1};
     if (guard_launch("release_kernel")) release_kernel<<<dim3(1), dim3(64), 0, d->s_comm>>>(d->stamps, r);
     if (root) {
         for (int i = 0; i < d->nsp - d->tstop; ++i) {
