@@ -714,6 +714,7 @@ def _config3_dist(rank: int, world: int, local_rank: int, torch, dist, steps: in
     dx = torch.from_numpy(x).to("cuda")
     dvv = torch.from_numpy(v).to("cuda")
     r = DI.DistRank(local_rank, world, rank, spw=DI.DEFAULT_SPW)
+    layout = "snake" if world > 1 and r.owner(world) == world - 1 else "round-robin"
     tr = DI.TorchTransport(device=torch.device("cuda", local_rank), timing=True)
 
     def one():
@@ -743,7 +744,8 @@ def _config3_dist(rank: int, world: int, local_rank: int, torch, dist, steps: in
             "value": steps / el, "unit": "evals/s", "ms_per_eval": el / steps * 1e3, "scaling": "strong",
             "ranks_seen": len(allt), "bcast_ms_per_eval_per_rank": bc, "last_logpdf": lp,
             "achieved_tflops_per_gpu": round(tf, 3), "frac_of_fp64_peak": round(tf / PEAK_F64_TFLOPS, 4),
-            "transport": "torch.distributed nccl (RCCL) broadcast on the library's comm stream"}
+            "transport": "torch.distributed nccl (RCCL) broadcast on the library's comm stream",
+            "layout": layout, "tail_gather": "off (DESIGN.md §7.4)"}
 
 
 def cpu_grad_baseline(N: int):

@@ -61,6 +61,8 @@ EXPORTED = (
     "gaplac_dist_plan_check",
     "gaplac_dist_plan",
     "gaplac_dist_set_tail",
+    "gaplac_dist_set_layout",
+    "gaplac_dist_owner",
     "gaplac_dist_tail_geometry",
     "gaplac_dist_set_tail_buffer",
     "gaplac_dist_tail_segment",
@@ -182,6 +184,8 @@ def load() -> ctypes.CDLL:
     lib.gaplac_dist_plan_check.argtypes = [c_int32, c_int32, c_int32, c_int32, _I64P, c_char_p, c_int64]
     lib.gaplac_dist_plan.argtypes = [c_int32, c_int32, c_int32, c_int32, _I32P, c_int64, _I64P]
     lib.gaplac_dist_set_tail.argtypes = [c_void_p, c_int32, c_int32]
+    lib.gaplac_dist_set_layout.argtypes = [c_void_p, c_int32]
+    lib.gaplac_dist_owner.argtypes = [c_void_p, c_int32, _I32P]
     lib.gaplac_dist_tail_geometry.argtypes = [c_void_p, c_int64, _I32P, _I64P, _I32P]
     lib.gaplac_dist_set_tail_buffer.argtypes = [c_void_p, c_void_p, c_int64]
     lib.gaplac_dist_tail_segment.argtypes = [c_void_p, c_int32, _VPP, _I64P, _I32P]

@@ -1,9 +1,10 @@
 // Distributed evaluation (BASELINE configs[3]): one rank of a 1-D
 // block-column cyclic Cholesky of the (N+1)-augmented covariance.
 //
-// Distribution. Super-panels (SP) of W 128-wide tile columns are dealt round-robin: SP s
-// belongs to rank s % nranks. A rank stores only its own tile columns (all Np rows,
-// column-major, ldc = Np), in order (ColMap in gaplac_internal.h). Because the Gram is
+// Distribution. Super-panels (SP) of W 128-wide tile columns are dealt in rounds of nranks:
+// SP s belongs to rank s % nranks, or with the snake layout (gaplac_dist_set_layout) to
+// nranks - 1 - s % nranks in odd rounds. A rank stores only its own tile columns (all Np
+// rows, column-major, ldc = Np), in order (ColMap in gaplac_internal.h). Because the Gram is
 // symmetric, a rank's block columns of the lower triangle are the block rows of the upper:
 // each rank builds exactly the Gram tiles it owns, with no redistribution.
 //
@@ -95,6 +96,7 @@ struct gaplac_dist {
     int big_mode = 1;  // GAPLAC_DIST_BIG: 0 never, 1 per rank (no chain beside the launch), 2 by launch size
     int big_min = 2048;  // (gaplac_dist_configure) tiles of a launch for the per-rank choice
     int alone = 0;     // GAPLAC_DIST_ALONE: the owner of SP s+1 starts update(s) after its chain
+    int snake = 0;     // gaplac_dist_set_layout: boustrophedon dealing of the SPs
     hipStream_t s_main = nullptr, s_panel = nullptr, s_comm = nullptr;
     hipEvent_t ev_gram = nullptr, ev_panel_done = nullptr;
     // ev_recv / ev_packed per panel parity and chunk; ev_step[s & 1]: update(s) brought SP
@@ -292,11 +294,15 @@ bool check_plan(const std::vector<std::vector<DOp>>& plan, int nsp, int D, int s
     return true;
 }
 
-ColMap cmap(const gaplac_dist* d) { return ColMap{d->nranks, d->rank, d->W}; }
+ColMap cmap(const gaplac_dist* d) { return ColMap{d->nranks, d->rank, d->W, d->snake}; }
+int owner(const gaplac_dist* d, int s) {
+    const int r = s % d->nranks;
+    return d->snake && ((s / d->nranks) & 1) ? d->nranks - 1 - r : r;
+}
 int sp_first(const gaplac_dist* d, int s) { return s * d->W; }
 int sp_width(const gaplac_dist* d, int s) { return std::min(d->W, d->nt - s * d->W); }
 int sp_local(const gaplac_dist* d, int s) { return (s / d->nranks) * d->W; }  // first local column
-bool owns(const gaplac_dist* d, int s) { return s % d->nranks == d->rank; }
+bool owns(const gaplac_dist* d, int s) { return owner(d, s) == d->rank; }
 int64_t panel_row0(const gaplac_dist* d, int s) { return (int64_t)sp_first(d, s) * NB; }
 // group buffer of panel s: (s / D) & 1; its origin row is that of the group's first panel
 int group_buf(const gaplac_dist* d, int s) { return (s / d->D) & 1; }
@@ -355,7 +361,7 @@ TailGeom tail_geom(const gaplac_dist* d, int nt, int nsp, int64_t Np) {
     g.Nt = Np - g.N0;
     for (int s = g.stop; s < nsp; ++s) {
         const int i = s - g.stop;
-        const bool here = d->rank == d->tail_root || s % d->nranks == d->rank;
+        const bool here = d->rank == d->tail_root || owns(d, s);
         const int64_t c = (int64_t)std::min(d->W, nt - s * d->W) * NB * tseg_rows(g.Nt, d->W, i);
         g.off.push_back(here ? g.elems : 0);
         g.cnt.push_back(here ? c : 0);
@@ -501,6 +507,9 @@ int gaplac_dist_create(int device, int nranks, int rank, int spw, gaplac_dist** 
     d->cw = nranks > 1 ? std::min(2, spw) : spw;
     d->alone = nranks > 1 ? 1 : 0;
     d->big_mode = nranks == 1 ? 2 : 1;
+    // the snake layout evens out the ranks (whole-job replay at N = 65536 over 8:
+    // 246.7 -> 240.9 ms); the tail gather stays off by default
+    d->snake = nranks > 1 ? 1 : 0;
     auto fail = [&](const char* what, hipError_t e) {
         std::fprintf(stderr, "gaplac_dist_create: %s: %s\n", what, hipGetErrorString(e));
         gaplac_dist_destroy(d);
@@ -588,6 +597,24 @@ int gaplac_dist_destroy(gaplac_dist* d) {
     return 0;
 }
 
+// Super-panel layout, before begin: snake = 1 deals the SPs boustrophedon (rank r owns SP
+// u P + r in even rounds u and u P + P - 1 - r in odd ones), 0 round-robin.
+int gaplac_dist_set_layout(gaplac_dist* d, int32_t snake) {
+    if (!d || snake < 0 || snake > 1) return derr(d, GAPLAC_E_ARG, "set_layout: %d", snake);
+    if (d->snake != snake) {
+        d->snake = snake;
+        d->lists_N = -1;
+    }
+    return 0;
+}
+
+// Owner rank of super-panel s under the current layout.
+int gaplac_dist_owner(gaplac_dist* d, int32_t s, int32_t* out_rank) {
+    if (!d || s < 0 || !out_rank) return GAPLAC_E_ARG;
+    *out_rank = owner(d, s);
+    return 0;
+}
+
 // Schedule options (the environment's GAPLAC_DIST_* are the defaults): depth = panels per
 // deferral group (1 = none), chunk = tile columns per broadcast chunk, big = bulk kernel
 // choice (0 never the large-launch kernel, 1 per rank: launches of >= big_min tiles with no
@@ -647,7 +674,8 @@ int gaplac_dist_geometry(gaplac_dist* d, int64_t N, int64_t* Np, int32_t* nt, in
     const int t = (int)(np / NB);
     const int ns = (t + d->W - 1) / d->W;
     int nl = 0;
-    for (int s = d->rank; s < ns; s += d->nranks) nl += std::min(d->W, t - s * d->W);
+    for (int s = 0; s < ns; ++s)
+        if (owns(d, s)) nl += std::min(d->W, t - s * d->W);
     if (Np) *Np = np;
     if (nt) *nt = t;
     if (nsp) *nsp = ns;
@@ -846,7 +874,7 @@ int gaplac_dist_panel_chunk(gaplac_dist* d, int32_t s, int32_t c, void** ptr, in
         return derr(d, GAPLAC_E_ARG, "panel: step %d chunk %d out of range", s, c);
     if (ptr) *ptr = chunk_ptr(d, s, c);
     if (count) *count = chunk_count(d, s, c);
-    if (root) *root = s % d->nranks;
+    if (root) *root = owner(d, s);
     return 0;
 }
 
@@ -855,7 +883,7 @@ int gaplac_dist_panel(gaplac_dist* d, int32_t s, void** ptr, int64_t* count, int
     if (!d || s < 0 || s >= d->nsteps) return derr(d, GAPLAC_E_ARG, "panel: step %d out of range", s);
     if (ptr) *ptr = chunk_ptr(d, s, 0);
     if (count) *count = (int64_t)sp_width(d, s) * NB * group_ld(d, s) - (panel_row0(d, s) - group_row0(d, s));
-    if (root) *root = s % d->nranks;
+    if (root) *root = owner(d, s);
     return 0;
 }
 
@@ -906,10 +934,10 @@ int gaplac_dist_comm_end(gaplac_dist* d, int32_t s) {
 // The ops [b, e) of step p's plan on s_main (chain_beside: this rank's chain runs beside
 // them, so the large-launch kernel is not taken).
 static int run_ops(gaplac_dist* d, int p, size_t b, size_t e, bool chain_beside) {
-    // owned-SP ordinal of the first owned SP >= g
+    // owned-SP ordinal of the first owned SP >= g (this rank owns one SP per round)
     auto ord_from = [&](int g) {
-        const int rel = g - d->rank;
-        return rel <= 0 ? 0 : (rel + d->nranks - 1) / d->nranks;
+        const int u = g / d->nranks;  // SP of ordinal u: cmap.global(u W) / W, in round u
+        return cmap(d).global(u * d->W) / d->W >= g ? u : u + 1;
     };
     auto launch = [&](const uint32_t* tiles, int cnt, const Panel& pn, int kd) -> int {
         if (cnt <= 0) return 0;
@@ -1015,7 +1043,8 @@ int gaplac_dist_finish(gaplac_dist* d, double* out_logdet, double* out_quad, int
     // the distributed SPs' columns come first in the storage (a gathered SP's columns were
     // factored by the root's tail, whose sums are in tres)
     int64_t ncols = 0;
-    for (int s = d->rank; s < d->nsteps; s += d->nranks) ncols += sp_width(d, s);
+    for (int s = 0; s < d->nsteps; ++s)
+        if (owns(d, s)) ncols += sp_width(d, s);
     {
         DistGuard guard(d);
         launch_reduce(d->s_main, d->C, d->Np, d->N, ncols * NB, cmap(d), d->dres);
@@ -1092,7 +1121,7 @@ int gaplac_dist_tail_segment(gaplac_dist* d, int32_t i, void** buf, int64_t* cou
     const size_t k = (size_t)i;
     if (buf) *buf = d->tseg_cnt[k] ? d->tseg + d->tseg_off[k] : nullptr;
     if (count) *count = d->tseg_cnt[k] ? d->tseg_cnt[k] : 0;
-    if (src) *src = (d->tstop + i) % d->nranks;
+    if (src) *src = owner(d, d->tstop + i);
     return 0;
 }
 
@@ -1288,7 +1317,8 @@ int gaplac_dist_replay_chunk(gaplac_dist* d, const gaplac_dist* src, int32_t s, 
             r.add[1] = xfer_ticks;
         }
     } else {
-        if (!src || src->Np != d->Np || src->W != d->W || src->nranks != d->nranks || src->rank != s % d->nranks)
+        if (!src || src->Np != d->Np || src->W != d->W || src->nranks != d->nranks || src->rank != owner(d, s) ||
+            src->snake != d->snake)
             return derr(d, GAPLAC_E_ARG, "replay: source context is not the owner of panel %d", s);
         const long long wait = f_ticks + lat_ticks + xfer_ticks - copy_ticks;
         if (s == 0) {  // the owner's chain starts after its Gram (taken as long as this rank's)
@@ -1341,7 +1371,7 @@ int gaplac_dist_replay_tail(gaplac_dist* d, const gaplac_dist* const* owners, in
     const bool root = d->rank == d->tail_root;
     std::vector<int64_t> bytes((size_t)d->nranks, 0);
     for (int i = 0; i < d->nsp - d->tstop; ++i) {
-        const int src = (d->tstop + i) % d->nranks;
+        const int src = owner(d, d->tstop + i);
         const int64_t c = (int64_t)sp_width(d, d->tstop + i) * NB * tseg_rows(d->tNt, d->W, i) * 8;
         if (src != d->tail_root) bytes[(size_t)src] += c;
     }
@@ -1352,7 +1382,7 @@ int gaplac_dist_replay_tail(gaplac_dist* d, const gaplac_dist* const* owners, in
     if (guard_launch("release_kernel")) release_kernel<<<dim3(1), dim3(64), 0, d->s_comm>>>(d->stamps, r);
     if (root) {
         for (int i = 0; i < d->nsp - d->tstop; ++i) {
-            const int src = (d->tstop + i) % d->nranks;
+            const int src = owner(d, d->tstop + i);
             if (src == d->tail_root) continue;
             const gaplac_dist* o = owners[src];
             if (!o || o->rank != src || o->tstop != d->tstop || o->tNt != d->tNt || !o->tseg ||

@@ -50,14 +50,20 @@ struct KTime {
 
 // Where global tile column bj of the lower triangle is stored. Single-GPU layout: the
 // identity (nranks = 1). 1-D block-column cyclic distribution over nranks: super-panels of
-// W tile columns are dealt round-robin, super-panel s to rank s % nranks, and a rank keeps
-// its super-panels contiguously in order, so local tile column lj holds global column
-//   bj = ((lj / W) * nranks + rank) * W + lj % W.
+// W tile columns are dealt in rounds of nranks, one per rank, and a rank keeps its
+// super-panels contiguously in order, so local tile column lj (round u = lj / W) holds
+//   bj = (u * nranks + r(u)) * W + lj % W,   r(u) = rank, or with snake (boustrophedon)
+// dealing nranks - 1 - rank in odd rounds (every rank then alternates
+// between early and late super-panels of a round).
 // Rows are never redistributed: every storage column keeps global row indices.
 struct ColMap {
     int nranks, rank, W;
+    int snake = 0;
     __host__ __device__ __forceinline__ int global(int lj) const {
-        return nranks == 1 ? lj : ((lj / W) * nranks + rank) * W + lj % W;
+        if (nranks == 1) return lj;
+        const int u = lj / W;
+        const int r = (snake && (u & 1)) ? nranks - 1 - rank : rank;
+        return (u * nranks + r) * W + lj % W;
     }
 };
 

@@ -107,7 +107,7 @@ def replay_rank(owners, rep: DI.DistRank, N: int, D: int, dX_ptr: int, terms, no
         for c in range(nch[s]):
             nbytes = c_int64()
             rep._check(rep.lib.gaplac_dist_replay_info(rep.h, s, c, byref(nbytes), None, None))
-            src = owners[s % P].h if not rep.owns(s) else None
+            src = owners[rep.owner(s)].h if not rep.owns(s) else None
             rep._check(rep.lib.gaplac_dist_replay_chunk(rep.h, src, s, c, int(F[s][c]), int(band[s]), lat,
                                                         model.xfer_ticks(nbytes.value), int(copy_ticks)))
 
@@ -182,7 +182,7 @@ def next_inputs(res: dict, prev_F=None, prev_band=None):
     return F, band
 
 
-def step_table(res: dict, P: int, rank: int):
+def step_table(res: dict, P: int, rank: int, owner=None):
     """Per step: the panel's arrival (last chunk), this rank's update start and end, and
     how long its s_main sat idle waiting for the panel (> 0: the step was chain / link
     bound on this rank; 0: the panel was there before the stream got to it)."""
@@ -193,7 +193,8 @@ def step_table(res: dict, P: int, rank: int):
     for s in range(res["nsp"]):
         arr = int(res["last_recv"][s]) - t0
         upd, end = int(st[s, 0]) - t0, int(st[s, 2]) - t0
-        rows.append(dict(s=s, owner=s % P, own=(s % P == rank), arrival_us=arr * 0.01, upd_start_us=upd * 0.01,
+        o = owner(s) if owner else s % P
+        rows.append(dict(s=s, owner=o, own=(o == rank), arrival_us=arr * 0.01, upd_start_us=upd * 0.01,
                          upd_end_us=end * 0.01, main_idle_us=max(0, upd - (prev_end - t0 if s else 0)) * 0.01))
         prev_end = end + t0
     return rows

@@ -8,6 +8,9 @@ super-panel from its owner; the result needs one allreduce of (logdet, quad) and
 the failing-pivot index. The compute lives in libgaplac_hip.so (gaplac_dist_* in
 include/gaplac.h); this module sequences the steps and issues the collectives.
 
+With the snake layout (set_layout) SP s belongs to rank world-1-s%world in
+odd rounds of world super-panels; owner(s) asks the library.
+
 Reference semantics are those of gaplac_logpdf (AbstractGPs.logpdf(FiniteGP, v) at
 CLI/src/mcmc.jl:35 and CLI/src/select.jl:49-50): the same value to <= 1e-9 relative,
 PosDefException(info) on a non-positive pivot.
@@ -52,7 +55,7 @@ class DistRank:
 
     def __init__(self, device: int, nranks: int, rank: int, spw: int = DEFAULT_SPW, depth: int = -1,
                  chunk: int = -1, big: int = -1, big_min: int = -1, alone: int = -1, tail: int = -1,
-                 tail_root: int = 0):
+                 tail_root: int = 0, snake: int = -1):
         self.lib = _native.load()
         h = c_void_p()
         rc = self.lib.gaplac_dist_create(int(device), int(nranks), int(rank), int(spw), byref(h))
@@ -67,6 +70,23 @@ class DistRank:
         self.configure(depth, chunk, big, big_min, alone)
         if tail >= 0:
             self.set_tail(tail, tail_root)
+        if snake >= 0:
+            self.set_layout(snake)
+
+    def set_layout(self, snake: int):
+        """gaplac_dist_set_layout: 1 = snake (boustrophedon) dealing of the super-panels."""
+        self._check(self.lib.gaplac_dist_set_layout(self.h, int(snake)))
+
+    def owner(self, s: int) -> int:
+        r = c_int32()
+        self._check(self.lib.gaplac_dist_owner(self.h, int(s), byref(r)))
+        return r.value
+
+    def global_col(self, lj: int) -> int:
+        """Global tile column of local tile column lj (ColMap::global)."""
+        u, e = divmod(lj, self.spw)
+        s = next(u * self.nranks + k for k in range(self.nranks) if self.owner(u * self.nranks + k) == self.rank)
+        return s * self.spw + e
 
     def set_tail(self, cols: int, root: int = 0):
         """Tail gather (gaplac_dist_set_tail): the super-panels in the last `cols` tile
@@ -110,7 +130,7 @@ class DistRank:
         raise GaplacError(rc, msg)
 
     def owns(self, s: int) -> bool:
-        return s % self.nranks == self.rank
+        return self.owner(s) == self.rank
 
     def geometry(self, N: int):
         Np, pel = c_int64(), c_int64()
@@ -388,7 +408,7 @@ class LoopbackTransport:
 
     def bcast(self, ranks: Sequence, s: int):
         import torch
-        root = s % ranks[0].nranks
+        root = ranks[0].panel_chunk(s, 0)[2]
         rootr = next(r for r in ranks if r.rank == root)
         for c in range(rootr.chunks(s)):
             streams = {r.rank: torch.cuda.ExternalStream(r.comm_begin_chunk(s, c), device=torch.device("cuda", r.device))

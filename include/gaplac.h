@@ -261,13 +261,14 @@ int gaplac_plan_check_schedule(int64_t N, int32_t spw, int32_t depth, int32_t pa
  * would dispatch here when the job runs on several GPUs.
  *
  * Per rank, per evaluation (every call only enqueues, except finish):
- *   gaplac_dist_begin(...)                         -> nsp
- *   if (0 % nranks == rank) gaplac_dist_factor(d, 0)
+ *   gaplac_dist_begin(...)                         -> nsteps (nsp without the tail gather)
+ *   if (owner(0) == rank) gaplac_dist_factor(d, 0)         (owner: gaplac_dist_owner)
  *   bcast(0)
- *   for s in 0..nsp-1:
- *       if (s+1 < nsp && (s+1) % nranks == rank) gaplac_dist_factor(d, s+1)
+ *   for s in 0..nsteps-1:
+ *       if (s+1 < nsteps && owner(s+1) == rank) gaplac_dist_factor(d, s+1)
  *       gaplac_dist_update(d, s)
- *       if (s+1 < nsp) bcast(s+1)
+ *       if (s+1 < nsteps) bcast(s+1)
+ *   [the tail gather, when set: see gaplac_dist_set_tail]
  *   gaplac_dist_finish(d, &logdet_part, &quad_part, &info_part)
  *   allreduce: logdet = sum, quad = sum, info = min over nonzero; then
  *   logpdf = -(N*log(2*pi) + logdet + quad) / 2   (NaN / PosDefException if info > 0)
@@ -309,6 +310,13 @@ int gaplac_dist_begin(gaplac_dist* d, int64_t N, int32_t D, const double* X, int
  * alone 1; with one rank: chunk = spw, big 2, alone 0. */
 int gaplac_dist_configure(gaplac_dist* d, int32_t depth, int32_t chunk, int32_t big, int32_t big_min,
                           int32_t alone);
+/* Super-panel layout, before begin: snake = 1 deals the super-panels boustrophedon (rank r
+ * owns super-panel u*nranks + r in even rounds u, u*nranks + nranks-1-r in odd ones), which
+ * evens out the ranks' trailing-update work; 0 = round-robin. Default: 1
+ * with several ranks. owner: the rank that owns super-panel s (factors it and roots its
+ * broadcast). */
+int gaplac_dist_set_layout(gaplac_dist* d, int32_t snake);
+int gaplac_dist_owner(gaplac_dist* d, int32_t s, int32_t* out_rank);
 int gaplac_dist_factor(gaplac_dist* d, int32_t s);   /* owner of super-panel s only */
 int gaplac_dist_chunks(gaplac_dist* d, int32_t s, int32_t* out_chunks);
 int gaplac_dist_panel_chunk(gaplac_dist* d, int32_t s, int32_t c, void** buf, int64_t* count,
@@ -332,7 +340,7 @@ int gaplac_dist_plan_check(int32_t nt, int32_t spw, int32_t depth, int32_t pair_
  * super-panel step+2 is up to date); *out_n = op count, out may be NULL. */
 int gaplac_dist_plan(int32_t nt, int32_t spw, int32_t depth, int32_t pair_m, int32_t* out, int64_t cap,
                      int64_t* out_n);
-/* Tail gather. tail_cols > 0: the super-panels whose columns all lie in
+/* Tail gather (off by default). tail_cols > 0: the super-panels whose columns all lie in
  * the last tail_cols (<= 128) tile columns are not factored by the distributed steps. After
  * the last step's update every rank sends its columns of that trailing matrix (from each
  * super-panel's first row down) to rank `root`, which factors it with the single-GPU

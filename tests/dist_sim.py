@@ -17,25 +17,29 @@ from oracle import restatement as R
 
 class SimRank:
     def __init__(self, nranks: int, rank: int, spw: int = 2, nb: int = 16, depth: int = 2, chunk: int = None,
-                 pair_m: int = 2, tail: int = 0, tail_root: int = 0):
+                 pair_m: int = 2, tail: int = 0, tail_root: int = 0, snake: int = 0):
         self.nranks, self.rank, self.spw, self.nb = nranks, rank, spw, nb
         self.depth, self.cw, self.pair_m = depth, (chunk or spw), pair_m
-        self.tail, self.tail_root = tail, tail_root
+        self.tail, self.tail_root, self.snake = tail, tail_root, snake
         self.device = None
         self._bufs = None
         self._tbuf = None
         self.applied = None  # per local tile column: panels applied, in order (checked by tests)
         self.tail_part = None  # the root's (logdet, quad, info) of the gathered trailing matrix
 
+    def owner(self, s):  # gaplac_dist.hip owner()
+        r = s % self.nranks
+        return self.nranks - 1 - r if self.snake and (s // self.nranks) % 2 else r
+
     def owns(self, s):
-        return s % self.nranks == self.rank
+        return self.owner(s) == self.rank
 
     def geometry(self, N):
         nb, W = self.nb, self.spw
         Np = (N + 1 + nb - 1) // nb * nb
         nt = Np // nb
         nsp = (nt + W - 1) // W
-        nloc = sum(min(W, nt - s * W) for s in range(self.rank, nsp, self.nranks))
+        nloc = sum(min(W, nt - s * W) for s in range(nsp) if self.owner(s) == self.rank)
         return dict(Np=Np, nt=nt, nsp=nsp, nloc=nloc, panel_elems=Np * min(self.depth * W, nt) * nb)
 
     def use_torch_panel_buffers(self, N):
@@ -63,7 +67,7 @@ class SimRank:
         self.tNt = g["Np"] - self.tN0
         for sp in range(stop, nsp):
             i = sp - stop
-            here = self.rank == self.tail_root or sp % self.nranks == self.rank
+            here = self.rank == self.tail_root or self.owns(sp)
             c = min(W, nt - sp * W) * nb * (self.tNt - i * W * nb)
             self._tseg.append((self._telems, c) if here else (0, 0))
             if here:
@@ -74,7 +78,7 @@ class SimRank:
 
     def tail_segment(self, i):
         off, c = self._tseg[i]
-        return None, c, (self.tstop + i) % self.nranks
+        return None, c, self.owner(self.tstop + i)
 
     def segment_tensor(self, i):
         off, c = self._tseg[i]
@@ -153,7 +157,7 @@ class SimRank:
         return col0 * ld + (r0 - origin), ncols * ld - (r0 - origin)
 
     def panel_chunk(self, s, c):
-        return None, self._chunk_range(s, c)[1], s % self.nranks
+        return None, self._chunk_range(s, c)[1], self.owner(s)
 
     def chunk_tensor(self, s, c):
         off, count = self._chunk_range(s, c)
@@ -170,8 +174,10 @@ class SimRank:
 
     # global tile column of local tile column lj (ColMap::global)
     def gcol(self, lj):
-        W = self.spw
-        return ((lj // W) * self.nranks + self.rank) * W + lj % W
+        W, P = self.spw, self.nranks
+        u = lj // W
+        r = P - 1 - self.rank if self.snake and u % 2 else self.rank
+        return (u * P + r) * W + lj % W
 
     def begin(self, X, terms, noise, v):
         g = self.geometry(len(v))
@@ -243,7 +249,7 @@ class SimRank:
                     self._apply_sp(g, pf, pl)
             elif kind == 1:
                 for u in range((self.nloc + W - 1) // W):
-                    sg = u * self.nranks + self.rank
+                    sg = self.gcol(u * W) // W
                     if sg >= g:
                         self._apply_sp(sg, pf, pl)
 

@@ -24,7 +24,7 @@ class CpuLoopback(DI.LoopbackTransport):
             r.use_torch_panel_buffers(N)
 
     def bcast(self, ranks, s):
-        root = s % ranks[0].nranks
+        root = ranks[0].owner(s)
         rootr = next(r for r in ranks if r.rank == root)
         for c in range(rootr.chunks(s)):
             src = rootr.chunk_tensor(s, c)
@@ -58,12 +58,13 @@ def _case(N, seed=0):
 @pytest.mark.parametrize("world,spw,N,depth,chunk", [
     (1, 2, 150, 2, 2), (2, 2, 150, 2, 1), (3, 1, 200, 1, 1), (4, 2, 257, 4, 1), (5, 3, 95, 3, 2), (8, 1, 40, 2, 1),
     (2, 4, 600, 4, 1), (3, 4, 600, 3, 3), (8, 2, 700, 4, 2), (2, 3, 400, 8, 3)])
-def test_loopback_schedule_matches_oracle(world, spw, N, depth, chunk):
-    """Every rank count / deferral depth / chunk width: the library's step plan applied by
-    the numpy rank double gives every column every panel once, in order (SimRank.finish),
-    and the oracle's logpdf."""
+@pytest.mark.parametrize("snake", [0, 1])
+def test_loopback_schedule_matches_oracle(world, spw, N, depth, chunk, snake):
+    """Every rank count / deferral depth / chunk width, round-robin and snake layouts: the
+    library's step plan applied by the numpy rank double gives every column every panel
+    once, in order (SimRank.finish), and the oracle's logpdf."""
     X, terms, v = _case(N, seed=world)
-    ranks = [SimRank(world, r, spw=spw, nb=16, depth=depth, chunk=chunk) for r in range(world)]
+    ranks = [SimRank(world, r, spw=spw, nb=16, depth=depth, chunk=chunk, snake=snake) for r in range(world)]
     lp, ld, q = DI.logpdf_dist(ranks, CpuLoopback(), X, terms, 0.1, v, full=True)
     rl, rd, rq = R.logpdf(X, terms, 0.1, v)
     assert abs(lp - rl) <= RTOL * abs(rl)
@@ -75,13 +76,14 @@ def test_loopback_schedule_matches_oracle(world, spw, N, depth, chunk):
     (1, 2, 150, 2, 2, 4, 0), (2, 2, 150, 2, 1, 5, 1), (3, 1, 200, 1, 1, 6, 2), (4, 2, 257, 4, 1, 8, 0),
     (5, 3, 95, 3, 2, 3, 4), (8, 1, 40, 2, 1, 1, 0), (2, 4, 600, 4, 1, 12, 0), (3, 4, 600, 3, 3, 16, 1),
     (8, 2, 700, 4, 2, 20, 0), (2, 3, 400, 8, 3, 7, 1), (4, 4, 700, 2, 2, 30, 3), (8, 4, 1300, 2, 2, 40, 0)])
-def test_loopback_tail_gather_matches_oracle(world, spw, N, depth, chunk, tail, root):
+@pytest.mark.parametrize("snake", [0, 1])
+def test_loopback_tail_gather_matches_oracle(world, spw, N, depth, chunk, tail, root, snake):
     """The tail gather: the plan stops before the super-panels of the last
     `tail` tile columns; every rank's columns of the trailing matrix go to `root`, which
     factors them. Every distributed column got every panel once, in order; the gathered
     ones every distributed panel; the oracle's logpdf."""
     X, terms, v = _case(N, seed=world + tail)
-    ranks = [SimRank(world, r, spw=spw, nb=16, depth=depth, chunk=chunk, tail=tail, tail_root=root)
+    ranks = [SimRank(world, r, spw=spw, nb=16, depth=depth, chunk=chunk, tail=tail, tail_root=root, snake=snake)
              for r in range(world)]
     lp, ld, q = DI.logpdf_dist(ranks, CpuLoopback(), X, terms, 0.1, v, full=True)
     assert ranks[0].tstop > 0 and ranks[0].tail_segments() > 0
@@ -184,7 +186,7 @@ class RecordingTransport(DI.TorchTransport):
         super().bcast(ranks, s)
 
 
-def _worker_defaults(rank, world, port, q, N, spw, tail=0):
+def _worker_defaults(rank, world, port, q, N, spw, tail=0, snake=0):
     """One rank of a gloo job at the multi-rank defaults (depth 2, chunk 2): logpdf, and the
     broadcast sequence every rank issued, gathered on rank 0. tail > 0: with the tail gather
     onto the last rank (gloo isend / irecv through TorchTransport.gather_tail)."""
@@ -193,7 +195,7 @@ def _worker_defaults(rank, world, port, q, N, spw, tail=0):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         X, terms, v = _case(N, seed=world)
-        r = SimRank(world, rank, spw=spw, nb=16, depth=2, chunk=2, tail=tail, tail_root=world - 1)
+        r = SimRank(world, rank, spw=spw, nb=16, depth=2, chunk=2, tail=tail, tail_root=world - 1, snake=snake)
         tr = RecordingTransport()
         lp = DI.logpdf_dist([r], tr, X, terms, 0.1, v)
         seqs = [None] * world
@@ -205,8 +207,8 @@ def _worker_defaults(rank, world, port, q, N, spw, tail=0):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,tail", [(4, 0), (8, 0), (4, 12), (8, 12)])
-def test_gloo_rehearsal_multirank_defaults(world, tail):
+@pytest.mark.parametrize("world,tail,snake", [(4, 0, 0), (8, 0, 0), (4, 12, 1), (8, 12, 1)])
+def test_gloo_rehearsal_multirank_defaults(world, tail, snake):
     """VERDICT r05 #2a: the configs[3] job's rank counts on CPU, through TorchTransport at
     the P > 1 defaults (deferral depth 2, broadcast chunks of 2 tile columns, so every
     panel goes out in two chunks): every rank issues the same broadcast sequence (step,
@@ -215,7 +217,7 @@ def test_gloo_rehearsal_multirank_defaults(world, tail):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_defaults, args=(r, world, port, q, N, spw, tail)) for r in range(world)]
+    procs = [ctx.Process(target=_worker_defaults, args=(r, world, port, q, N, spw, tail, snake)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=240) for _ in procs]
@@ -235,7 +237,8 @@ def test_gloo_rehearsal_multirank_defaults(world, tail):
     nt = (N + 1 + 15) // 16
     nsp = nt // spw + (1 if nt % spw else 0)
     nsteps = (nt - tail + spw - 1) // spw if tail else nsp  # 8 with 12 gathered tile columns
-    assert [x[:3] for x in seqs[0]] == [(s, c, s % world) for s in range(nsteps) for c in range(2)]
+    owner = SimRank(world, 0, spw=spw, snake=snake).owner
+    assert [x[:3] for x in seqs[0]] == [(s, c, owner(s)) for s in range(nsteps) for c in range(2)]
 
 
 @pytest.mark.parametrize("depth", [1, 2, 3, 4, 5, 8])

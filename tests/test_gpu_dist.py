@@ -46,9 +46,10 @@ def _ranks(world, spw):
     (1, 4, 1000), (2, 1, 1000), (2, 4, 3000), (3, 1, 129), (3, 2, 1500), (4, 1, 700),
     (4, 2, 2100), (8, 1, 1100), (8, 1, 300), (2, 2, 1), (3, 1, 127), (3, 1, 128),
 ])
-def test_loopback_matches_oracle(world, spw, N):
+@pytest.mark.parametrize("snake", [0, 1])
+def test_loopback_matches_oracle(world, spw, N, snake):
     X, terms, v = _case(N, seed=world * 7 + spw)
-    ranks = _ranks(world, spw)
+    ranks = [DI.DistRank(0, world, r, spw=spw, snake=snake) for r in range(world)]
     lp, ld, q = DI.logpdf_dist(ranks, DI.LoopbackTransport(), X, terms, 0.1, v, full=True)
     rl, rd, rq = R.logpdf(X, terms, 0.1, v)
     assert abs(lp - rl) <= RTOL * abs(rl)
@@ -57,11 +58,13 @@ def test_loopback_matches_oracle(world, spw, N):
     assert abs(q - rq) <= 1e-9 * max(1.0, abs(rq))
 
 
-def test_loopback_factor_columns_match_oracle():
-    """Each rank's stored columns are the owned columns of L (and z in row N)."""
+@pytest.mark.parametrize("snake", [0, 1])
+def test_loopback_factor_columns_match_oracle(snake):
+    """Each rank's stored columns are the owned columns of L (and z in row N), in the
+    round-robin and the snake layout."""
     N, world, spw = 900, 3, 1
     X, terms, v = _case(N, seed=2)
-    ranks = _ranks(world, spw)
+    ranks = [DI.DistRank(0, world, r, spw=spw, snake=snake) for r in range(world)]
     DI.logpdf_dist(ranks, DI.LoopbackTransport(), X, terms, 0.1, v)
     C = R.gram(X, terms, 0.1)
     L = np.linalg.cholesky(C)
@@ -70,7 +73,9 @@ def test_loopback_factor_columns_match_oracle():
         loc = r.local(N)
         g = r.geometry(N)
         for lj in range(g["nloc"]):
-            bj = ((lj // spw) * world + r.rank) * spw + lj % spw
+            bj = r.global_col(lj)
+            if not snake:
+                assert bj == ((lj // spw) * world + r.rank) * spw + lj % spw
             for e in range(128):
                 j = bj * 128 + e
                 if j >= N:
@@ -196,8 +201,9 @@ def test_gloo_world2_processes_share_one_gpu(tail):
         assert abs(lp - rl) <= 1e-12 * abs(rl)
 
 
-@pytest.mark.parametrize("world,spw,N,big", [(4, 2, 12000, 1), (4, 2, 12000, 0), (8, 2, 9000, 1)])
-def test_loopback_multirank_defaults_match_single_gpu(world, spw, N, big):
+@pytest.mark.parametrize("world,spw,N,big,snake", [(4, 2, 12000, 1, 0), (4, 2, 12000, 0, 0), (8, 2, 9000, 1, 0),
+                                                    (8, 2, 9000, 1, 1), (3, 4, 14000, 1, 1)])
+def test_loopback_multirank_defaults_match_single_gpu(world, spw, N, big, snake):
     """the P > 1 defaults (chain alone with held post-mark ops, depth 2, chunk 2,
     the per-rank bulk kernel choice) across ranks that really exchange panels: every rank
     keeps its options (LoopbackTransport(keep_options=True)); against the single-GPU path
@@ -205,7 +211,7 @@ def test_loopback_multirank_defaults_match_single_gpu(world, spw, N, big):
     X, terms, v = _case(N, seed=N + world)
     with Context(0) as ctx:
         ref = ctx.logpdf(X, terms, 0.1, v)
-    ranks = [DI.DistRank(0, world, r, spw=spw, depth=2, chunk=2, big=big, alone=1) for r in range(world)]
+    ranks = [DI.DistRank(0, world, r, spw=spw, depth=2, chunk=2, big=big, alone=1, snake=snake) for r in range(world)]
     tr = DI.LoopbackTransport(keep_options=True)
     for _ in range(2):
         got = DI.logpdf_dist(ranks, tr, X, terms, 0.1, v)
@@ -234,17 +240,17 @@ def test_loopback_tail_gather_matches_oracle(world, spw, N, tail, root):
         r.close()
 
 
-@pytest.mark.parametrize("world,spw,N,tail,root", [
-    (4, 4, 16384, 80, 0), (8, 2, 12000, 40, 7), (2, 4, 14000, 128, 1), (8, 4, 20000, 77, 3)])
-def test_loopback_tail_gather_large_matches_single_gpu(world, spw, N, tail, root):
+@pytest.mark.parametrize("world,spw,N,tail,root,snake", [
+    (4, 4, 16384, 80, 0, 0), (8, 2, 12000, 40, 7, 1), (2, 4, 14000, 128, 1, 0), (8, 4, 20000, 77, 3, 1)])
+def test_loopback_tail_gather_large_matches_single_gpu(world, spw, N, tail, root, snake):
     """At the P > 1 defaults (chain alone, held ops, chunks of 2, per-rank bulk kernel: every
     rank keeps its options) with the gathered tail up to its 128-column maximum; against the
     single-GPU path at 1e-11, twice through the same workspaces."""
     X, terms, v = _case(N, seed=N + tail)
     with Context(0) as ctx:
         ref = ctx.logpdf(X, terms, 0.1, v)
-    ranks = [DI.DistRank(0, world, r, spw=spw, depth=2, chunk=2, big=1, alone=1, tail=tail, tail_root=root)
-             for r in range(world)]
+    ranks = [DI.DistRank(0, world, r, spw=spw, depth=2, chunk=2, big=1, alone=1, tail=tail, tail_root=root,
+                         snake=snake) for r in range(world)]
     tr = DI.LoopbackTransport(keep_options=True)
     for _ in range(2):
         got = DI.logpdf_dist(ranks, tr, X, terms, 0.1, v)

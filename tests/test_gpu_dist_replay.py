@@ -18,10 +18,10 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("world,rank,depth,chunk,big,alone,tail", [
-    (4, 1, 2, 1, 1, 1, 0), (4, 3, 4, 2, 1, 0, 0), (3, 0, 1, 4, 0, 1, 0), (3, 2, 2, 2, 1, 1, 0),
-    (4, 0, 2, 2, 1, 1, 24), (4, 2, 2, 2, 1, 1, 24)])
-def test_replay_rank_matches_loopback(world, rank, depth, chunk, big, alone, tail):
+@pytest.mark.parametrize("world,rank,depth,chunk,big,alone,tail,snake", [
+    (4, 1, 2, 1, 1, 1, 0, 0), (4, 3, 4, 2, 1, 0, 0, 0), (3, 0, 1, 4, 0, 1, 0, 0), (3, 2, 2, 2, 1, 1, 0, 1),
+    (4, 0, 2, 2, 1, 1, 24, 1), (4, 2, 2, 2, 1, 1, 24, 0)])
+def test_replay_rank_matches_loopback(world, rank, depth, chunk, big, alone, tail, snake):
     """tail > 0: the tail gather onto rank 0, replayed: the root's partial
     sums (its columns and the gathered tail) equal the loopback run's, and the gathered
     segments arrive no earlier than the model says."""
@@ -33,10 +33,10 @@ def test_replay_rank_matches_loopback(world, rank, depth, chunk, big, alone, tai
     terms = [(1, 0, 1.5, 0)]
     dx = torch.from_numpy(x).to("cuda")
     dv = torch.from_numpy(v).to("cuda")
-    owners = [DI.DistRank(0, world, r, spw=4, tail=tail) for r in range(world)]
+    owners = [DI.DistRank(0, world, r, spw=4, tail=tail, snake=snake) for r in range(world)]
     DI.logpdf_dist_device(owners, DI.LoopbackTransport(), N, 1, dx.data_ptr(), N, terms, 0.1, dv.data_ptr())
     ld0, q0, info0 = owners[rank].finish()
-    rep = DI.DistRank(0, world, rank, spw=4, depth=depth, chunk=chunk, big=big, alone=alone, tail=tail)
+    rep = DI.DistRank(0, world, rank, spw=4, depth=depth, chunk=chunk, big=big, alone=alone, tail=tail, snake=snake)
     model = RP.ReplayModel(bw_GBps=50.0, lat_us=20.0)
     F = band = None
     for _ in range(2):
@@ -62,8 +62,9 @@ def test_replay_rank_matches_loopback(world, rank, depth, chunk, big, alone, tai
             tNt = g["Np"] - nsteps * 4 * 128
             sent = {}
             for i, sp in enumerate(range(nsteps, g["nsp"])):
-                if sp % world:
-                    sent[sp % world] = sent.get(sp % world, 0) + min(4, g["nt"] - sp * 4) * 128 * (tNt - i * 512) * 8
+                o = rep.owner(sp)
+                if o:
+                    sent[o] = sent.get(o, 0) + min(4, g["nt"] - sp * 4) * 128 * (tNt - i * 512) * 8
             need = (model.lat + max(sent.values()) / (model.gbw * 1e9) * 1e6) if rank == 0 else model.lat
             assert t["arrive_us"] >= t["steps_end_us"] + need - 0.05, (t, need)
             if rank == 0:

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--big", type=int, nargs="+", default=[1])
     ap.add_argument("--alone", type=int, nargs="+", default=[0])
     ap.add_argument("--tail", type=int, nargs="+", default=[0])
+    ap.add_argument("--snake", type=int, nargs="+", default=[-1], help="layout (-1: the library's default)")
     ap.add_argument("--gbw", type=float, nargs="+", default=[50.0], help="gather GB/s per sender link")
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--steps", action="store_true", help="include the per-step table")
@@ -80,14 +81,15 @@ def main():
             single_ms = (time.perf_counter() - t0) * 1e3
         emit(dict(kind="single", N=N, ms=single_ms, logpdf=lp_single))
 
-    for tail in a.tail:
+    for tail, snake in itertools.product(a.tail, a.snake):
+        a.cur_snake = snake
         # the loopback job: every rank's factored columns (the owners of the replayed panels)
         t0 = time.perf_counter()
-        owners = [DI.DistRank(0, a.ranks, r, spw=4, tail=tail) for r in range(a.ranks)]
+        owners = [DI.DistRank(0, a.ranks, r, spw=4, tail=tail, snake=snake) for r in range(a.ranks)]
         lp_loop = DI.logpdf_dist_device(owners, DI.LoopbackTransport(), N, 1, dx.data_ptr(), N, terms, CF.NOISE_VAR,
                                         dv.data_ptr())
         parts = {r.rank: r.finish() for r in owners}
-        emit(dict(kind="loopback", N=N, ranks=a.ranks, tail=tail, logpdf=lp_loop, s=time.perf_counter() - t0))
+        emit(dict(kind="loopback", N=N, ranks=a.ranks, tail=tail, snake=snake, logpdf=lp_loop, s=time.perf_counter() - t0))
         if a.job:
             job(a, owners, parts, tail, N, dx, dv, terms, emit)
         else:
@@ -101,7 +103,7 @@ def _replay(a, owners, rank, tail, N, dx, dv, terms, model, senders_end_us=0.0):
     from gaplac_amd import distributed as DI
     from gaplac_amd import dist_replay as RP
     rep = DI.DistRank(0, a.ranks, rank, spw=4, depth=a.depth[0], chunk=a.chunk[0], big=a.big[0], alone=a.alone[0],
-                      tail=tail)
+                      tail=tail, snake=a.cur_snake)
     F = band = None
     copy = tcopy = 0
     hist = []
@@ -112,7 +114,7 @@ def _replay(a, owners, rank, tail, N, dx, dv, terms, model, senders_end_us=0.0):
         F, band = RP.next_inputs(res)
         copy = int(res["copy_mean"])
         tcopy = int(res["tail_copy"])
-    rows = RP.step_table(res, a.ranks, rank)
+    rows = RP.step_table(res, a.ranks, rank, rep.owner)
     rep.close()
     return res, hist, rows
 
@@ -134,7 +136,7 @@ def job(a, owners, parts, tail, N, dx, dv, terms, emit):
         if rank != 0 and tail:
             senders_end = max(senders_end, res["tail"]["steps_end_us"])
     pred = max(v["predicted_ms"] for v in per.values())
-    emit(dict(kind="job", N=N, ranks=a.ranks, tail=tail, bw_GBps=a.bw[0], gather_bw_GBps=a.gbw[0] if tail else None,
+    emit(dict(kind="job", N=N, ranks=a.ranks, tail=tail, snake=a.cur_snake, bw_GBps=a.bw[0], gather_bw_GBps=a.gbw[0] if tail else None,
               depth=a.depth[0], chunk=a.chunk[0], big=a.big[0], alone=a.alone[0], predicted_ms=pred,
               slowest=max(per, key=lambda r: per[r]["predicted_ms"]), senders_end_ms=round(senders_end / 1e3, 3),
               per_rank=per))
@@ -145,7 +147,8 @@ def replays(a, owners, parts, tail, N, dx, dv, terms, single_ms, emit):
     from gaplac_amd import distributed as DI
     from gaplac_amd import dist_replay as RP
     for rank, depth, chunk, big, alone in itertools.product(a.local, a.depth, a.chunk, a.big, a.alone):
-        rep = DI.DistRank(0, a.ranks, rank, spw=4, depth=depth, chunk=chunk, big=big, alone=alone, tail=tail)
+        rep = DI.DistRank(0, a.ranks, rank, spw=4, depth=depth, chunk=chunk, big=big, alone=alone, tail=tail,
+                          snake=a.cur_snake)
         for bw, gbw in itertools.product(a.bw, a.gbw if tail else a.gbw[:1]):
             model = RP.ReplayModel(bw_GBps=bw, lat_us=a.lat, gather_bw_GBps=gbw)
             F = band = None
@@ -160,7 +163,7 @@ def replays(a, owners, parts, tail, N, dx, dv, terms, single_ms, emit):
                 copy = int(res["copy_mean"])
                 tcopy = int(res["tail_copy"])
             ld0, q0, _ = parts[rank]
-            rows = RP.step_table(res, a.ranks, rank)
+            rows = RP.step_table(res, a.ranks, rank, rep.owner)
             idle = [r["main_idle_us"] for r in rows]
             f_own = {s: [round(t * 0.01, 1) for t in v] for s, v in res["f_meas"].items()}
             d = dict(kind="replay", N=N, ranks=a.ranks, rank=rank, depth=depth, chunk=chunk, big=big, alone=alone, bw_GBps=bw,
