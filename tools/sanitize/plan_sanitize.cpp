@@ -8,7 +8,8 @@
 //                                interleave_tail_tasks) on its first call;
 //   gaplac_plan_check_schedule - the deferred-update accounting at every depth;
 //   gaplac_dist_plan_check     - build_plan / check_plan of the distributed schedule;
-//   gaplac_dist_plan           - the plan export.
+//   gaplac_dist_plan           - the plan export;
+//   gaplac_dist_plan_check_tail / gaplac_dist_plan_tail - the same with the tail gather.
 // Exit 0 when every check passes and no sanitizer fired (halt_on_error=1).
 #include <cstdio>
 #include <vector>
@@ -69,6 +70,20 @@ int main() {
                     const int rc = gaplac_dist_plan_check(nt, spw, depth, pair_m, &a, msg, sizeof msg);
                     EXPECT(rc == 0, "dist_plan_check nt=%d spw=%d depth=%d pair_m=%d: %s", nt, spw, depth, pair_m, msg);
                     ++checks;
+                    for (int tail : {1, 5, 48, 80, 128}) {
+                        const int rt = gaplac_dist_plan_check_tail(nt, spw, depth, pair_m, tail, &a, msg, sizeof msg);
+                        EXPECT(rt == 0, "dist_plan_check_tail nt=%d spw=%d depth=%d pair_m=%d tail=%d: %s", nt, spw,
+                               depth, pair_m, tail, msg);
+                        ++checks;
+                        if (nt % 97 == 0) {
+                            int64_t n = 0;
+                            EXPECT(gaplac_dist_plan_tail(nt, spw, depth, pair_m, tail, nullptr, 0, &n) == 0 && n > 0,
+                                   "dist_plan_tail size");
+                            std::vector<int32_t> out((size_t)(5 * n));
+                            EXPECT(gaplac_dist_plan_tail(nt, spw, depth, pair_m, tail, out.data(), 5 * n, &n) == 0,
+                                   "dist_plan_tail export");
+                        }
+                    }
                     if (nt % 97 == 0) {  // the export, sized by a first call
                         int64_t n = 0;
                         EXPECT(gaplac_dist_plan(nt, spw, depth, pair_m, nullptr, 0, &n) == 0 && n > 0, "dist_plan size");
