@@ -90,6 +90,7 @@ struct gaplac_ctx {
     uint32_t* ttasks = nullptr;  // its task list for ttasks_T tile columns
     size_t ttasks_elems = 0;
     int ttasks_T = -1, ttasks_X = 0, ttasks_n = 0;
+    bool ttasks_G = false;  // the list holds the Gram's tile tasks (gram_in_tail)
     std::string ttrace_path;     // GAPLAC_TAIL_TRACE: append per-task times of every tail launch here
     int tail_fault = -1;         // GAPLAC_TAIL_FAULT (tests only): skip this tail column's diagonal block
     unsigned long long* ttrace = nullptr;
@@ -501,6 +502,19 @@ static bool whole_in_tail(const gaplac_ctx* ctx, int nt) {
     return tail_allowed(ctx) && ctx->tailk && ctx->tail_s > 0 && nt <= TAIL_TMAX && nt <= ctx->tail_s;
 }
 
+// The Gram inside the tail (TAIL_G tasks, -D GAPLAC_TAIL_GRAM=0 turns it off): a plain
+// single evaluation whose matrix lies whole in the tail builds its Gram tiles as the tail's
+// first tasks instead of in two launches before it (N = 4096: the Gram launches, their gaps
+// and the tail's start behind them were ~50 us of the 1.15 ms evaluation).
+// Needs the tile stores' buffer offsets (< 2^31 bytes per tile column span).
+#ifndef GAPLAC_TAIL_GRAM
+#define GAPLAC_TAIL_GRAM 1
+#endif
+static bool gram_in_tail(const gaplac_ctx* ctx, int nt, int64_t lda) {
+    return GAPLAC_TAIL_GRAM && ctx->xr_mode == 0 && whole_in_tail(ctx, nt) &&
+           ((int64_t)(NB - 1) * lda + NB) * 8 < ((int64_t)1 << 31);
+}
+
 static std::vector<int> superpanel_starts(const gaplac_ctx* ctx, int nt) {
     std::vector<int> sp{0};
     // a matrix the persistent tail covers whole (plain logpdf, at most TAIL_TMAX tile
@@ -567,11 +581,12 @@ namespace gaplac {
 // The single-evaluation tail list of T tile columns (X extra tile rows), as eval_device
 // launches it; also the distributed root's gathered tail (gaplac_dist.hip). tail_sim as
 // gaplac_ctx::tail_sim; workers: the persistent grid the simulated order plans for.
-void build_single_tail_list(int T, int X, int tail_sim, int workers, std::vector<uint32_t>& out) {
+void build_single_tail_list(int T, int X, int tail_sim, int workers, std::vector<uint32_t>& out, bool gram) {
     const bool sim = (tail_sim > 0 || (tail_sim < 0 && T < 80)) && X == 0;
     out.clear();
     build_tail_tasks(T, out, nullptr, tail_gw(T), 4, tail_quad_last(sim, T), false, GAPLAC_SINGLE_GROUP, X, sim ? 1 : 0);
     if (sim && workers > 0) sim_order_tail_tasks(T, out, workers);
+    if (gram && X == 0) add_gram_tasks(T, out);
 }
 }  // namespace gaplac
 namespace {
@@ -831,26 +846,30 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
                 HIPQ(ctx, hipEventRecord(ctx->ev_xdone, ctx->s_xrest));
                 HIPQ(ctx, hipStreamWaitEvent(sm, ctx->ev_xdone, 0));
             }
+            const bool gram = ts == 0 && gram_in_tail(ctx, nt, lda);
             if (ctx->dry) {  // gaplac_plan_check: the task list's dependency order
                 std::vector<uint32_t> host;
-                build_single_tail_list(T, X, ctx->tail_sim, 0, host);
+                build_single_tail_list(T, X, ctx->tail_sim, 0, host, gram);
                 std::string why;
-                if (!check_tail_tasks(T, host, &why, X)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
+                if (!check_tail_tasks(T, host, &why, X, gram)) return set_err(ctx, GAPLAC_E_ARG, "%s", why.c_str());
             }
-            if ((ctx->ttasks_T != T || ctx->ttasks_X != X) && !ctx->dry) {
+            if ((ctx->ttasks_T != T || ctx->ttasks_X != X || ctx->ttasks_G != gram) && !ctx->dry) {
                 std::vector<uint32_t> host;
-                build_single_tail_list(T, X, ctx->tail_sim, std::max(1, ctx->ncu / std::max(1, ctx->tail_share)), host);
+                build_single_tail_list(T, X, ctx->tail_sim, std::max(1, ctx->ncu / std::max(1, ctx->tail_share)), host,
+                                       gram);
                 int rc;
                 if ((rc = ensure(ctx, &ctx->ttasks, &ctx->ttasks_elems, host.size()))) return rc;
                 HIPCK(ctx, hipMemcpy(ctx->ttasks, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
                 ctx->ttasks_T = T;
                 ctx->ttasks_X = X;
+                ctx->ttasks_G = gram;
                 ctx->ttasks_n = (int)host.size();
             }
             if (!ctx->tctl && !ctx->dry)
                 HIPCK(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->tctl), sizeof(TailCtl)));
-            HIPQ(ctx, hipMemsetAsync(ctx->tctl, 0, sizeof(TailCtl), sm));
-            const int nts = ctx->dry ? (int)(T * (T + 1) * (T + 2) / 6 + 3 * T * T + X * T * (T + 3) / 2)
+            if (!gram) HIPQ(ctx, hipMemsetAsync(ctx->tctl, 0, sizeof(TailCtl), sm));  // (gram: zeroed at the start)
+            const int nts = ctx->dry ? (int)(T * (T + 1) * (T + 2) / 6 + 3 * T * T + X * T * (T + 3) / 2 +
+                                             (gram ? T * (T + 1) / 2 : 0))
                                      : ctx->ttasks_n;
             if (!ctx->ttrace_path.empty() && !ctx->dry) {
                 int rc;
@@ -861,6 +880,12 @@ int factor_and_reduce(gaplac_ctx* ctx, int64_t N, int64_t lda, int nt) {
                         ctx->ttrace_path.empty() ? nullptr : ctx->ttrace};
             ta.fault = ctx->tail_fault;
             ta.xrows = X;
+            if (gram) {  // the inputs the Gram launches would have read (enqueue_eval_body)
+                ta.gX = ctx->dX;
+                ta.gldx = N;
+                ta.gv = ctx->dv;
+                ta.gtp = ctx->dtp;
+            }
             // batch lanes run their tails side by side: each persistent grid takes its share
             // of the CUs (one tail workgroup fills a CU's LDS), so no tail waits for another
             launch_tail(sm, ta, std::min(std::max(1, ctx->ncu / std::max(1, ctx->tail_share)), nts), slot(ctx, 10, 0));
@@ -914,7 +939,12 @@ int ensure_tile_lists(gaplac_ctx* ctx, int nt) {
 // ctx->dtp.
 int enqueue_eval_body(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt) {
     const int64_t lda = Np + (int64_t)NB * ctx->xr_tiles;
-    launch_init_result(ctx->s_main, ctx->dres);
+    const bool gram_tail = gram_in_tail(ctx, nt, lda);
+    if (gram_tail && !ctx->tctl && !ctx->dry) HIPCK(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->tctl), sizeof(TailCtl)));
+    if (gram_tail)  // the tail's counters zeroed here (factor_and_reduce then skips its memset)
+        launch_init_result_ctl(ctx->s_main, ctx->dres, ctx->tctl);
+    else
+        launch_init_result(ctx->s_main, ctx->dres);
     if (ctx->recording) launch_kt_reset(ctx->s_main, ctx->dkt, (int)ctx->kt_cap);
     // Gram in two launches: the first super-panel's tile columns, then the rest (the panel
     // chain starts on the first part while the second is still being written; the second as
@@ -923,11 +953,13 @@ int enqueue_eval_body(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt)
     const double bpt = 8.0 * NB * NB;  // bytes per tile
     const double b1 = bpt * (tri(nt) - tri(std::max(0, nt - ctx->spw))) + 8.0 * (double)N * (D + 1);
     const double b2 = bpt * tri(std::max(0, nt - ctx->spw));
-    launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 1, ctx->spw, slot(ctx, 1, b1));
-    HIPQ(ctx, hipEventRecord(ctx->ev_gram, ctx->s_main));
-    launch_gram_queue(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, ctx->spw, nt, 2, ctx->dres,
-                      slot(ctx, 1, b2));
-    HIPQ(ctx, hipEventRecord(ctx->ev_gram2, ctx->s_main));
+    if (!gram_tail) {  // (else the tail's first tasks build it)
+        launch_gram(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, 1, ctx->spw, slot(ctx, 1, b1));
+        HIPQ(ctx, hipEventRecord(ctx->ev_gram, ctx->s_main));
+        launch_gram_queue(ctx->s_main, ctx->A, lda, N, nt, ctx->dX, N, ctx->dv, ctx->dtp, ctx->spw, nt, 2, ctx->dres,
+                          slot(ctx, 1, b2));
+        HIPQ(ctx, hipEventRecord(ctx->ev_gram2, ctx->s_main));
+    }
     if (ctx->xr_mode == 1) launch_init_identity_rows(ctx->s_main, ctx->A, lda, Np, nt, ctx->spw);
     if (ctx->xr_mode == 2)
         launch_cross_gram(ctx->s_main, ctx->A, lda, Np, nt, N, ctx->xr_M, ctx->xr_tiles, ctx->dX, N, ctx->dXs,

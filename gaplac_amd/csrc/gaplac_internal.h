@@ -108,6 +108,9 @@ struct TailCtl {
     // TRSM of the sub-diagonal tile (k+1, k): per 16-row group g, the 16-column blocks of L
     // stored so far (0..8); the next diagonal tile's Q blocks consume them as they come
     unsigned sprog[TAIL_TMAX][8];
+    // Gram tile (i, j) built by its task (TAIL_G, the Gram inside the tail): its first
+    // column's tasks (k = 0) wait for it
+    unsigned gdone[TAIL_TMAX * TAIL_TMAX];
 };
 struct TailArgs {
     double* A;
@@ -131,6 +134,13 @@ struct TailArgs {
     // must come back as GAPLAC_E_HIP; -1 = off
     int fault = -1;
     int xrows = 0;  // extra tile rows below the matrix factored along (tile rows ts+T .. ts+T+xrows-1)
+    // The Gram inside the tail (single evaluations whose matrix lies whole in it, ts = 0):
+    // the list holds one TAIL_G task per lower tile, built from gX (ld gldx), gv and gtp as
+    // gram_kernel builds it; nullptr: the Gram is built before the launch
+    const double* gX = nullptr;
+    int64_t gldx = 0;
+    const double* gv = nullptr;
+    const TermPack* gtp = nullptr;
 };
 constexpr int TAIL_DSTAMPS = 20;  // start, load in LDS, per panel s: phase 2 start / end, done
 constexpr int TAIL_MODEL_SHIFT = 27;
@@ -161,12 +171,18 @@ int sim_order_tail_tasks(int T, std::vector<uint32_t>& list, int workers);
 // models' current columns are interleaved task by task (colstart from build_tail_tasks).
 void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<size_t>& colstart, int B, int lag,
                            std::vector<uint32_t>& out);
-// The list is a topological order of the tail's dataflow that applies every update once.
-bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why, int xrows = 0);
+// The list is a topological order of the tail's dataflow that applies every update once
+// (gram: it also builds every lower tile once, before the tile's first task).
+bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why, int xrows = 0, bool gram = false);
+// The Gram inside the tail: one TAIL_G task per lower tile of the T x T tile triangle
+// prepended to a list (tile (0,0) first, then D(0), then the rest column by column).
+void add_gram_tasks(int T, std::vector<uint32_t>& list);
 void launch_tail(hipStream_t s, const TailArgs& a, int grid, KTime* kt);
+// init_result_kernel's reset of res plus every word of the tail's counters ctl, one launch
+void launch_init_result_ctl(hipStream_t s, EvalResult* res, TailCtl* ctl);
 // The single-evaluation tail list (gaplac_api.hip): T tile columns, X extra tile rows, the
 // simulated order per tail_sim (-1 auto: T < 80) planned for `workers` workgroups.
-void build_single_tail_list(int T, int X, int tail_sim, int workers, std::vector<uint32_t>& out);
+void build_single_tail_list(int T, int X, int tail_sim, int workers, std::vector<uint32_t>& out, bool gram = false);
 
 // Host-side footprint guard. Before launching, every launcher computes the
 // element range [p + lo, p + hi) its grid will touch in the column storage it is given

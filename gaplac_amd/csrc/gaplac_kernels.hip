@@ -160,6 +160,14 @@ __device__ __forceinline__ double exp_nonpos(double x, const double* __restrict_
     return x < -745.2 ? 0.0 : y;
 }
 
+// threadIdx.x through an opaque copy: in the persistent kernel nothing derived from it is
+// hoisted out of the task loop (LICM would keep every body's addresses live: spills)
+__device__ __forceinline__ int otid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 // ---------------------------------------------------------------------------------
 // Gram term evaluation, specialised at compile time on the term kind and on how the term
 // combines with its group (KernelProduct inside a group, KernelSum across groups):
@@ -197,7 +205,8 @@ __device__ __forceinline__ double gram_term(double xi, double xj, double p, int6
     }
 }
 
-template <int KIND, int MODE, int CB>
+// A wave's batch: tile columns j0l + NW q, q < CB (NW: the workgroup's waves).
+template <int KIND, int MODE, int CB, int NW = 4>
 __device__ __forceinline__ void gram_batch(double (&tot0)[CB], double (&tot1)[CB],
                                            double (&pr0)[CB], double (&pr1)[CB],
                                            const double* __restrict__ xc, double2 xr, double p,
@@ -205,8 +214,8 @@ __device__ __forceinline__ void gram_batch(double (&tot0)[CB], double (&tot1)[CB
 #pragma clang fp contract(off)
 #pragma unroll
     for (int q = 0; q < CB; ++q) {
-        const double xj = xc[4 * q];
-        const int64_t j = j0 + 4 * q;
+        const double xj = xc[NW * q];
+        const int64_t j = j0 + NW * q;
         const double k0 = gram_term<KIND>(xr.x, xj, p, i0, j, etbl);
         const double k1 = gram_term<KIND>(xr.y, xj, p, i0 + 1, j, etbl);
         if constexpr (MODE == GM_SUM_FIRST) { tot0[q] = k0; tot1[q] = k1; }
@@ -218,18 +227,18 @@ __device__ __forceinline__ void gram_batch(double (&tot0)[CB], double (&tot1)[CB
     }
 }
 
-template <int KIND, int CB>
+template <int KIND, int CB, int NW = 4>
 __device__ __forceinline__ void gram_batch_mode(int mode, double (&tot0)[CB], double (&tot1)[CB],
                                                 double (&pr0)[CB], double (&pr1)[CB],
                                                 const double* __restrict__ xc, double2 xr, double p,
                                                 int64_t i0, int64_t j0, const double* __restrict__ etbl) {
     switch (mode) {
-        case GM_SUM_FIRST: gram_batch<KIND, GM_SUM_FIRST, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-        case GM_SUM: gram_batch<KIND, GM_SUM, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-        case GM_PR_FIRST: gram_batch<KIND, GM_PR_FIRST, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-        case GM_PR: gram_batch<KIND, GM_PR, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-        case GM_PR_LAST0: gram_batch<KIND, GM_PR_LAST0, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-        default: gram_batch<KIND, GM_PR_LAST, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        case GM_SUM_FIRST: gram_batch<KIND, GM_SUM_FIRST, CB, NW>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        case GM_SUM: gram_batch<KIND, GM_SUM, CB, NW>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        case GM_PR_FIRST: gram_batch<KIND, GM_PR_FIRST, CB, NW>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        case GM_PR: gram_batch<KIND, GM_PR, CB, NW>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        case GM_PR_LAST0: gram_batch<KIND, GM_PR_LAST0, CB, NW>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+        default: gram_batch<KIND, GM_PR_LAST, CB, NW>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
     }
 }
 
@@ -244,10 +253,13 @@ __device__ __forceinline__ void gram_batch_mode(int mode, double (&tot0)[CB], do
 // Workgroup = one 128x128 lower tile, 256 threads. Each lane owns two consecutive rows
 // (16-byte stores, a wave writes one 1 KiB column segment per instruction); the tile's
 // column coordinates are staged once in LDS and read as wave-wide broadcasts.
+// NW = 8: the persistent tail's 512-thread workgroup builds a tile as a task (tail_kernel,
+// TAIL_G): the same per-element arithmetic, eight waves taking every eighth column, the
+// stores with the AUX cache policy (sc1: the tail's hand-off protocol).
 // ---------------------------------------------------------------------------------
 constexpr int GRAM_LDS = 2 * GAPLAC_MAX_TERMS * NB + NB + 256;  // doubles of LDS gram_tile works in
 
-template <int CB = GRAM_CB>
+template <int CB = GRAM_CB, int NW = 4, int AUX = 0>
 __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda, int64_t N,
                                           const double* __restrict__ X, int64_t ldx,
                                           const double* __restrict__ v,
@@ -267,12 +279,14 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
     double (*xrow)[NB] = xcol + GAPLAC_MAX_TERMS;
     double* vcol = lds + 2 * GAPLAC_MAX_TERMS * NB;
     double* etbl = vcol + NB;
-    const int tid = threadIdx.x;
+    static_assert(NW == 4 || NW == 8, "gram_tile: 4 or 8 waves");
+    static_assert(NB % (NW * CB) == 0, "gram_tile: whole batches per wave");
+    const int tid = NW == 4 ? (int)threadIdx.x : otid();
     const int T = tp.T;
     // Staging: thread tid owns coordinate slot c = tid % NB of the columns (tid < NB) or
     // the rows (tid >= NB); the term index is uniform (scalar TermPack loads) and every
     // global load is issued before the first one is consumed (one latency per tile).
-    {
+    if (NW == 4 || tid < 2 * NB) {
         const int c = tid & (NB - 1);
         const bool is_row = tid >= NB;
         const int64_t j = (is_row ? r0 : c0) + c;
@@ -303,7 +317,7 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
     const int64_t i0 = r0 + 2 * lane, i1 = i0 + 1;
     __syncthreads();
 
-    // Wave w: tile columns cc = w + 4 (cb + q), in batches of CB columns. Kind and
+    // Wave w: tile columns cc = w + NW (cb + q), in batches of CB columns. Kind and
     // group position are switched on once per term and batch (uniform branches); each
     // term gives 2 CB independent evaluations for the VALU pipeline to overlap.
     // Off the diagonal a singleton Noise group is all zeros and is skipped; interior
@@ -325,6 +339,7 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
         (void*)(((uint64_t)__builtin_amdgcn_readfirstlane((unsigned)(tbase >> 32)) << 32) |
                 (uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)tbase)),
         0, use_buf ? (int)span : 0, 0x00020000);
+    static_assert(AUX == 0 || NW == 8, "gram_tile: a cache policy only for the tail's tiles");
     auto store2 = [&](int cc, double o0, double o1) {
 #ifdef GAPLAC_GRAM_NOSTORE  // tools/gram_probe: compute-only timing (never true for real data)
         if (o0 != 1.2345e300) return;
@@ -335,7 +350,7 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
             u32x4 bits;
             __builtin_memcpy(&bits, &d, 16);
             __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, 16 * lane,
-                                                   __builtin_amdgcn_readfirstlane((int)((int64_t)cc * lda * 8)), 0);
+                                                   __builtin_amdgcn_readfirstlane((int)((int64_t)cc * lda * 8)), AUX);
         } else {
             *reinterpret_cast<double2*>(Ccol + (int64_t)cc * lda + i0) = make_double2(o0, o1);
         }
@@ -359,11 +374,11 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
         }
     };
     if (all_single) {
-        for (int cb = 0; cb < NB / 4; cb += CB) {
+        for (int cb = 0; cb < NB / NW; cb += CB) {
             double tot0[CB], tot1[CB], pr0[CB], pr1[CB];
 #pragma unroll
             for (int q = 0; q < CB; ++q) tot0[q] = tot1[q] = 0.0;  // 0 + k = k
-            const int j0l = wu + 4 * cb;
+            const int j0l = wu + NW * cb;
             for (int t = 0; t < T; ++t) {
                 const int kind = tp.kind[t];
                 if (kind == GAPLAC_NOISE && !diag_tile) continue;
@@ -372,21 +387,21 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
                 const double2 xr = *reinterpret_cast<const double2*>(&xrow[t][2 * lane]);
                 const int64_t j0 = c0 + j0l;
                 switch (kind) {
-                    case GAPLAC_SQEXP: gram_batch<GAPLAC_SQEXP, GM_SUM, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                    case GAPLAC_OU: gram_batch<GAPLAC_OU, GM_SUM, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                    case GAPLAC_LINEAR: gram_batch<GAPLAC_LINEAR, GM_SUM, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                    case GAPLAC_CAT: gram_batch<GAPLAC_CAT, GM_SUM, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                    default: gram_batch<GAPLAC_NOISE, GM_SUM, CB>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                    case GAPLAC_SQEXP: gram_batch<GAPLAC_SQEXP, GM_SUM, CB, NW>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                    case GAPLAC_OU: gram_batch<GAPLAC_OU, GM_SUM, CB, NW>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                    case GAPLAC_LINEAR: gram_batch<GAPLAC_LINEAR, GM_SUM, CB, NW>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                    case GAPLAC_CAT: gram_batch<GAPLAC_CAT, GM_SUM, CB, NW>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                    default: gram_batch<GAPLAC_NOISE, GM_SUM, CB, NW>(tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
                 }
             }
             store_batch(j0l, tot0, tot1);
         }
         return;
     }
-    for (int cb = 0; cb < NB / 4; cb += CB) {
+    for (int cb = 0; cb < NB / NW; cb += CB) {
         double tot0[CB], tot1[CB], pr0[CB], pr1[CB];
         bool have_tot = false;
-        const int j0l = wu + 4 * cb;  // tile column of q = 0
+        const int j0l = wu + NW * cb;  // tile column of q = 0
         for (int t = 0; t < T; ++t) {
             const int kind = tp.kind[t];
             const bool first = t == 0 || tp.last_in_group[t - 1];
@@ -400,11 +415,11 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
             const double2 xr = *reinterpret_cast<const double2*>(&xrow[t][2 * lane]);
             const int64_t j0 = c0 + j0l;
             switch (kind) {
-                case GAPLAC_SQEXP: gram_batch_mode<GAPLAC_SQEXP, CB>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                case GAPLAC_OU: gram_batch_mode<GAPLAC_OU, CB>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                case GAPLAC_LINEAR: gram_batch_mode<GAPLAC_LINEAR, CB>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                case GAPLAC_CAT: gram_batch_mode<GAPLAC_CAT, CB>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
-                default: gram_batch_mode<GAPLAC_NOISE, CB>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                case GAPLAC_SQEXP: gram_batch_mode<GAPLAC_SQEXP, CB, NW>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                case GAPLAC_OU: gram_batch_mode<GAPLAC_OU, CB, NW>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                case GAPLAC_LINEAR: gram_batch_mode<GAPLAC_LINEAR, CB, NW>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                case GAPLAC_CAT: gram_batch_mode<GAPLAC_CAT, CB, NW>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
+                default: gram_batch_mode<GAPLAC_NOISE, CB, NW>(mode, tot0, tot1, pr0, pr1, xc, xr, p, i0, j0, etbl); break;
             }
         }
         if (!have_tot) {
@@ -809,13 +824,6 @@ __device__ __forceinline__ void potrf_diag_kernel_body(double* __restrict__ Ag, 
 // table row 1); the stand-alone kernels use AUX = 0. Offsets are in doubles, < 2^28.
 // ---------------------------------------------------------------------------------
 constexpr int GM_SC1 = 16;
-// threadIdx.x through an opaque copy: in the persistent kernel nothing derived from it is
-// hoisted out of the task loop (LICM would keep every body's addresses live: spills)
-__device__ __forceinline__ int otid() {
-    int t = threadIdx.x;
-    asm volatile("" : "+v"(t));
-    return t;
-}
 typedef unsigned gm_u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned gm_u32x4 __attribute__((ext_vector_type(4)));
 // address-space views for __builtin_amdgcn_global_load_lds (LDS-DMA)
@@ -1763,7 +1771,7 @@ void launch_kt_reset(hipStream_t s, KTime* kt, int n) {
     if (n > 0 && guard_launch("kt_reset_kernel")) kt_reset_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s>>>(kt, n);
 }
 
-__global__ void init_result_kernel(EvalResult* res) {
+__device__ __forceinline__ void init_result_kernel_body(EvalResult* res) {
     res->logpdf = 0.0;
     res->logdet = 0.0;
     res->quad = 0.0;
@@ -1771,6 +1779,7 @@ __global__ void init_result_kernel(EvalResult* res) {
     res->gram_ticket = 0u;
     res->err = 0u;
 }
+__global__ void init_result_kernel(EvalResult* res) { init_result_kernel_body(res); }
 
 // ---------------------------------------------------------------------------------
 // Gradient of logpdf: the factorisation also runs
@@ -2405,6 +2414,7 @@ __device__ __forceinline__ unsigned tail_ld(const unsigned* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 constexpr int TAIL_S_WHOLE = 2;  // S task q: the whole 128-row tile, after D(k) (else q = row half)
+constexpr int TAIL_G = 1;        // D-type task q: build Gram tile (i, j) (TailArgs::gX; waits for nothing)
 constexpr unsigned TAIL_NQ = 10;  // Q blocks per diagonal tile (= units a diagonal U adds)
 
 // task word: type (2 bits) | q (4) | k (7) | i (7) | j (7), tile indices relative to ts
@@ -2795,11 +2805,15 @@ __device__ __forceinline__ void tail_q32(const Gm<AUX>& gC, const Gm<AUX>& gP, i
 // Lane 0: wait until the task's inputs are final (bounded: 0.2 s of the 100 MHz clock).
 // Returns false when the bound expires or another task has already failed (TailCtl::err
 // set: then every later wait returns at once and the launch drains quickly).
-__device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int k, int i, int j) {
+__device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int k, int i, int j, bool gram) {
+    if (type == TK_D && q == TAIL_G) return true;
     const unsigned long long t0 = wall_clock64();
+    // the Gram inside the tail: a tile's first-column tasks (k = 0) find it built first
+    const int gt = !gram || k != 0 ? -1 : type == TK_D ? 0 : type == TK_S ? i * TAIL_TMAX : i * TAIL_TMAX + j;
     for (unsigned it = 1;; ++it) {
-        bool ok;
-        if (type == TK_D) {
+        bool ok = gt < 0 || tail_ld(&c->gdone[gt]) != 0u;
+        if (!ok) {
+        } else if (type == TK_D) {
             ok = tail_ld(&c->units[k * TAIL_TMAX + k]) >= TAIL_NQ * (unsigned)k;
         } else if (type == TK_S) {  // the block itself; D(k)'s progress inside tail_trsm_pipe
             ok = tail_ld(&c->units[i * TAIL_TMAX + k]) >= 4u * k;
@@ -2823,6 +2837,7 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int
 // The tail's diagonal blocks run potrf_diag2_body (round 3); its LDS also holds the TRSM's
 // staged L_kk and inverses (tail_trsm_stage: 36 x 256 doubles).
 static_assert(DIAG2_SMEM >= (TRSM_LBLK + NDB) * 256, "tail_kernel LDS too small for the TRSM staging");
+static_assert(DIAG2_SMEM >= GRAM_LDS, "tail_kernel LDS too small for a Gram tile");
 __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict__ kt) {
     __shared__ double smem[DIAG2_SMEM];
     __shared__ unsigned s_task;
@@ -2843,7 +2858,7 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         double* const Dinv = a.Dinv + m * a.dinv_stride;
         EvalResult* const res = a.res + m;
         if (a.trace && threadIdx.x == 0) a.trace[3 * tk] = wall_clock64();
-        if (threadIdx.x == 0 && !tail_wait(ctl, type, q, k, i, j)) {
+        if (threadIdx.x == 0 && !tail_wait(ctl, type, q, k, i, j, a.gX != nullptr)) {
             atomicOr(&ctl->err, 1u);
             atomicOr(&res->err, 2u);  // the result record itself: the host sees it whatever the exit order
         }
@@ -2852,8 +2867,11 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         const int gk = a.ts + k;
         double* colk = A + (int64_t)gk * NB * a.lda;
         // debug (GAPLAC_TAIL_FAULT): D(fault) never runs nor publishes
-        const bool faulted = type == TK_D && k == a.fault;
+        const bool faulted = type == TK_D && q == 0 && k == a.fault;
         if (faulted) {
+        } else if (type == TK_D && q == TAIL_G) {  // Gram tile (i, j), sc1 stores (ts = 0)
+            gram_tile<GRAM_CB, 8, GM_SC1>(A + (int64_t)(a.ts + j) * NB * a.lda, a.lda, a.N, a.gX, a.gldx, a.gv, a.gtp,
+                                          a.ts + i, a.ts + j, smem);
         } else if (type == TK_D) {
             if ((int64_t)gk * NB < a.N) {
                 potrf_diag2_body<GM_SC1>(smem, colk + (int64_t)gk * NB, a.lda, a.N, (int64_t)gk * NB,
@@ -2894,7 +2912,9 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0 && !faulted) {
-            if (type == TK_D) {
+            if (type == TK_D && q == TAIL_G) {
+                __hip_atomic_fetch_add(&ctl->gdone[i * TAIL_TMAX + j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (type == TK_D) {
                 __hip_atomic_fetch_add(&ctl->ddone[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else if (type == TK_S) {  // two halves per tile (or one whole-tile task): done at 2
                 __hip_atomic_fetch_add(&ctl->sdone[i * TAIL_TMAX + k], q == TAIL_S_WHOLE ? 2u : 1u, __ATOMIC_RELAXED,
@@ -2940,6 +2960,27 @@ void interleave_tail_tasks(const std::vector<uint32_t>& one, const std::vector<s
             }
         }
     }
+}
+
+// The Gram inside the tail (single evaluations whose matrix lies whole in the tail): a
+// TAIL_G task per lower tile ahead of the list, tile (0, 0) first and D(0) right behind it
+// (the chain's start waits only for its own tile), then the other tiles column by column,
+// the order in which the list's first-column tasks need them. The ~T^2/2 tile builds run on
+// the other workgroups while D(0) factors.
+void add_gram_tasks(int T, std::vector<uint32_t>& list) {
+    std::vector<uint32_t> out;
+    out.reserve(list.size() + (size_t)T * (T + 1) / 2);
+    out.push_back(tail_enc(TK_D, TAIL_G, 0, 0, 0));
+    const uint32_t d0 = tail_enc(TK_D, 0, 0, 0, 0);
+    bool have_d0 = false;
+    for (uint32_t e : list) have_d0 = have_d0 || e == d0;
+    if (have_d0) out.push_back(d0);
+    for (int j = 0; j < T; ++j)
+        for (int i = j; i < T; ++i)
+            if (i || j) out.push_back(tail_enc(TK_D, TAIL_G, 0, i, j));
+    for (uint32_t e : list)
+        if (!(have_d0 && e == d0)) out.push_back(e);
+    list.swap(out);
 }
 
 // Dequeue order of the tail's tasks (see the block comment above). Every task waits only
@@ -3216,9 +3257,10 @@ int sim_order_tail_tasks(int T, std::vector<uint32_t>& list, int workers) {
 // list order, each only once its wait condition (tail_wait) holds on the tasks before it,
 // i.e. the list is a topological order of the dataflow, and at the end every tile has
 // received every column's update exactly once, every TRSM and diagonal block has run.
-bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why, int xrows) {
+bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why, int xrows, bool gram) {
     const int R = T + xrows;  // tile rows (the extra rows below the matrix: TRSMs and updates only)
     std::vector<unsigned> units((size_t)R * T, 0), sdone((size_t)R * T, 0), ddone((size_t)T, 0);
+    std::vector<unsigned> built((size_t)T * T, 0);  // Gram tiles built by their tasks (gram)
     auto fail = [&](size_t n, const char* what) {
         char b[160];
         std::snprintf(b, sizeof b, "tail task %zu of %zu (T = %d): %s", n, list.size(), T, what);
@@ -3232,6 +3274,17 @@ bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why
         const unsigned whole = i == j ? TAIL_NQ : 4u;
         if (k >= T || i >= R || j >= T || (i >= T && (type == TK_D || type == TK_Q)))
             return fail(n, "task outside the tile range");
+        if (type == TK_D && q == TAIL_G) {
+            if (!gram || xrows) return fail(n, "a Gram tile task in a list without the Gram inside");
+            if (k != 0 || j > i) return fail(n, "a Gram tile task outside the lower tile triangle");
+            if (built[(size_t)i * T + j]++) return fail(n, "a Gram tile built twice");
+            continue;
+        }
+        // the Gram inside the tail: a tile's first-column tasks after its Gram tile
+        if (gram && k == 0) {
+            const int gi = type == TK_D ? 0 : i, gj = type == TK_D ? 0 : type == TK_S ? 0 : j;
+            if (!built[(size_t)gi * T + gj]) return fail(n, "a task before its Gram tile");
+        }
         if (type == TK_D) {
             if (q != 0) return fail(n, "a diagonal block task of an unknown kind");
             if (units[(size_t)k * T + k] != TAIL_NQ * (unsigned)k) return fail(n, "D before its tile is updated");
@@ -3258,6 +3311,8 @@ bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why
     }
     for (int j = 0; j < T; ++j) {
         if (ddone[(size_t)j] != 1u) return fail(list.size(), "a diagonal block missing or repeated");
+        for (int i = j; gram && i < T; ++i)
+            if (!built[(size_t)i * T + j]) return fail(list.size(), "a Gram tile never built");
         for (int i = j; i < R; ++i) {
             const unsigned whole = i == j ? TAIL_NQ : 4u;
             if (units[(size_t)i * T + j] != whole * (unsigned)j) return fail(list.size(), "a tile missed an update");
@@ -3611,6 +3666,21 @@ void launch_tail(hipStream_t s, const TailArgs& a, int grid, KTime* kt) {
 void launch_init_result(hipStream_t s, EvalResult* res) {
     if (!guard_launch("init_result_kernel")) return;
     init_result_kernel<<<dim3(1), dim3(1), 0, s>>>(res);
+}
+
+// The result record and the tail's counters in one launch (the Gram inside the tail: the
+// evaluation's first launch is then this one, the tail the second; a hipMemsetAsync of the
+// counters was two fill launches of ~5 us each on the N = 4096 evaluation's critical path).
+__global__ __launch_bounds__(256) void init_result_ctl_kernel(EvalResult* res, unsigned* __restrict__ ctl, int nwords) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) init_result_kernel_body(res);
+    for (int w = (int)(blockIdx.x * 256 + threadIdx.x); w < nwords; w += (int)gridDim.x * 256) ctl[w] = 0u;
+}
+
+void launch_init_result_ctl(hipStream_t s, EvalResult* res, TailCtl* ctl) {
+    if (!guard_launch("init_result_ctl_kernel")) return;
+    static_assert(sizeof(TailCtl) % sizeof(unsigned) == 0, "TailCtl: whole words");
+    init_result_ctl_kernel<<<dim3(64), dim3(256), 0, s>>>(res, reinterpret_cast<unsigned*>(ctl),
+                                                          (int)(sizeof(TailCtl) / sizeof(unsigned)));
 }
 
 }  // namespace gaplac
