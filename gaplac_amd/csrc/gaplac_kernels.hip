@@ -358,7 +358,7 @@ __device__ __forceinline__ void gram_tile(double* __restrict__ Ccol, int64_t lda
     auto store_batch = [&](int j0l, const double (&tot0)[CB], const double (&tot1)[CB]) {
 #pragma unroll
         for (int q = 0; q < CB; ++q) {
-            const int cc = j0l + 4 * q;
+            const int cc = j0l + NW * q;
             const int64_t j = c0 + cc;
             double o0 = tot0[q], o1 = tot1[q];
             if (!plain) {
@@ -2838,6 +2838,10 @@ __device__ __forceinline__ bool tail_wait(const TailCtl* c, int type, int q, int
 // staged L_kk and inverses (tail_trsm_stage: 36 x 256 doubles).
 static_assert(DIAG2_SMEM >= (TRSM_LBLK + NDB) * 256, "tail_kernel LDS too small for the TRSM staging");
 static_assert(DIAG2_SMEM >= GRAM_LDS, "tail_kernel LDS too small for a Gram tile");
+// GRAM: the variant whose list holds the Gram's tile tasks (TailArgs::gX set); the other
+// tails (batched lanes, the 16k tail) do not carry its code (its registers cost them
+// SGPR spills: select -0.8%, profiles/r07g2_gram_tail_ab.txt)
+template <bool GRAM>
 __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict__ kt) {
     __shared__ double smem[DIAG2_SMEM];
     __shared__ unsigned s_task;
@@ -2858,7 +2862,7 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         double* const Dinv = a.Dinv + m * a.dinv_stride;
         EvalResult* const res = a.res + m;
         if (a.trace && threadIdx.x == 0) a.trace[3 * tk] = wall_clock64();
-        if (threadIdx.x == 0 && !tail_wait(ctl, type, q, k, i, j, a.gX != nullptr)) {
+        if (threadIdx.x == 0 && !tail_wait(ctl, type, q, k, i, j, GRAM)) {
             atomicOr(&ctl->err, 1u);
             atomicOr(&res->err, 2u);  // the result record itself: the host sees it whatever the exit order
         }
@@ -2869,7 +2873,7 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         // debug (GAPLAC_TAIL_FAULT): D(fault) never runs nor publishes
         const bool faulted = type == TK_D && q == 0 && k == a.fault;
         if (faulted) {
-        } else if (type == TK_D && q == TAIL_G) {  // Gram tile (i, j), sc1 stores (ts = 0)
+        } else if (GRAM && type == TK_D && q == TAIL_G) {  // Gram tile (i, j), sc1 stores (ts = 0)
             gram_tile<GRAM_CB, 8, GM_SC1>(A + (int64_t)(a.ts + j) * NB * a.lda, a.lda, a.N, a.gX, a.gldx, a.gv, a.gtp,
                                           a.ts + i, a.ts + j, smem);
         } else if (type == TK_D) {
@@ -2912,7 +2916,7 @@ __global__ __launch_bounds__(512) void tail_kernel(TailArgs a, KTime* __restrict
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0 && !faulted) {
-            if (type == TK_D && q == TAIL_G) {
+            if (GRAM && type == TK_D && q == TAIL_G) {
                 __hip_atomic_fetch_add(&ctl->gdone[i * TAIL_TMAX + j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else if (type == TK_D) {
                 __hip_atomic_fetch_add(&ctl->ddone[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3660,7 +3664,10 @@ void launch_tail(hipStream_t s, const TailArgs& a, int grid, KTime* kt) {
         !guard_launch("tail_kernel", a.A, 0,
                       (int64_t)(a.nmodels - 1) * a.a_stride + tiles_end(a.lda, a.ts + a.T + a.xrows - 1, a.ts + a.T - 1)))
         return;
-    tail_kernel<<<dim3((unsigned)grid), dim3(512), 0, s>>>(a, kt);
+    if (a.gX)
+        tail_kernel<true><<<dim3((unsigned)grid), dim3(512), 0, s>>>(a, kt);
+    else
+        tail_kernel<false><<<dim3((unsigned)grid), dim3(512), 0, s>>>(a, kt);
 }
 
 void launch_init_result(hipStream_t s, EvalResult* res) {

@@ -41,11 +41,11 @@ def run(k):
 def analyse(d):
     tr = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
     tr.sort(key=lambda r: int(r["Start_Timestamp"]))
-    short = lambda n: n.split("(")[0].replace("gaplac::", "")
+    short = lambda n: n.split("(")[0].replace("gaplac::", "").removeprefix("void ").split("<")[0]
     evs, cur = [], None
     for r in tr:
         n = short(r["Kernel_Name"])
-        if n == "init_result_kernel":
+        if n in ("init_result_kernel", "init_result_ctl_kernel"):  # (the latter: Gram inside the tail)
             cur = []
         if cur is not None:
             cur.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), n))

@@ -22,7 +22,9 @@ t0 = int(ev[0]["Start_Timestamp"])
 
 def short(n):
     n = n.split("(")[0].replace("gaplac::", "")
-    return n
+    if n.startswith("void "):  # template kernels (tail_kernel<GRAM>) demangle with their return type
+        n = n[5:]
+    return n.split("<")[0]
 
 
 rows = [(int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0, r["Queue_Id"], short(r["Kernel_Name"]))
