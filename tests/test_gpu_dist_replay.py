@@ -66,7 +66,8 @@ def test_replay_rank_matches_loopback(world, rank, depth, chunk, big, alone, tai
                 if o:
                     sent[o] = sent.get(o, 0) + min(4, g["nt"] - sp * 4) * 128 * (tNt - i * 512) * 8
             need = (model.lat + max(sent.values()) / (model.gbw * 1e9) * 1e6) if rank == 0 else model.lat
-            assert t["arrive_us"] >= t["steps_end_us"] + need - 0.05, (t, need)
+            # both stamps are rounded to 0.1 us and the modelled link time to 10 ns ticks
+            assert t["arrive_us"] >= t["steps_end_us"] + need - 0.15, (t, need)
             if rank == 0:
                 assert t["tail_end_us"] > t["arrive_us"] and t["tail_ms"] > 0
         else:
