@@ -515,6 +515,13 @@ static bool gram_in_tail(const gaplac_ctx* ctx, int nt, int64_t lda) {
            ((int64_t)(NB - 1) * lda + NB) * 8 < ((int64_t)1 << 31);
 }
 
+// The term descriptor reaches ctx->dtp through the evaluation's first launch
+// (init_result_ctl_kernel, when the Gram is inside the tail) instead of a copy.
+static bool tp_by_init(const gaplac_ctx* ctx, int64_t N) {
+    const int64_t Np = round_up(N + 1, NB);
+    return gram_in_tail(ctx, (int)(Np / NB), Np + (int64_t)NB * ctx->xr_tiles);
+}
+
 static std::vector<int> superpanel_starts(const gaplac_ctx* ctx, int nt) {
     std::vector<int> sp{0};
     // a matrix the persistent tail covers whole (plain logpdf, at most TAIL_TMAX tile
@@ -942,7 +949,7 @@ int enqueue_eval_body(gaplac_ctx* ctx, int64_t N, int32_t D, int64_t Np, int nt)
     const bool gram_tail = gram_in_tail(ctx, nt, lda);
     if (gram_tail && !ctx->tctl && !ctx->dry) HIPCK(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->tctl), sizeof(TailCtl)));
     if (gram_tail)  // the tail's counters zeroed here (factor_and_reduce then skips its memset)
-        launch_init_result_ctl(ctx->s_main, ctx->dres, ctx->tctl);
+        launch_init_result_ctl(ctx->s_main, ctx->dres, ctx->tctl, *ctx->htp, ctx->dtp);
     else
         launch_init_result(ctx->s_main, ctx->dres);
     if (ctx->recording) launch_kt_reset(ctx->s_main, ctx->dkt, (int)ctx->kt_cap);
@@ -1135,7 +1142,8 @@ int eval_enqueue(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp) {
     if ((rc = ensure_workspace(ctx, N))) return rc;
     const int64_t Np = round_up(N + 1, NB);
     *ctx->htp = tp;
-    HIPCK(ctx, hipMemcpyAsync(ctx->dtp, ctx->htp, sizeof(TermPack), hipMemcpyHostToDevice, ctx->s_main));
+    if (!tp_by_init(ctx, N))
+        HIPCK(ctx, hipMemcpyAsync(ctx->dtp, ctx->htp, sizeof(TermPack), hipMemcpyHostToDevice, ctx->s_main));
     ctx->slots.clear();
     ctx->recording = false;
     return enqueue_eval(ctx, N, D, Np, (int)(Np / NB));
@@ -1166,7 +1174,8 @@ int eval_device(gaplac_ctx* ctx, int64_t N, int32_t D, const TermPack& tp, EvalR
         }
     }
     *ctx->htp = tp;
-    HIPCK(ctx, hipMemcpyAsync(ctx->dtp, ctx->htp, sizeof(TermPack), hipMemcpyHostToDevice, ctx->s_main));
+    if (!tp_by_init(ctx, N))
+        HIPCK(ctx, hipMemcpyAsync(ctx->dtp, ctx->htp, sizeof(TermPack), hipMemcpyHostToDevice, ctx->s_main));
     ctx->slots.clear();
     ctx->recording = prof;
     rc = enqueue_eval(ctx, N, D, Np, nt);

@@ -178,8 +178,9 @@ bool check_tail_tasks(int T, const std::vector<uint32_t>& list, std::string* why
 // prepended to a list (tile (0,0) first, then D(0), then the rest column by column).
 void add_gram_tasks(int T, std::vector<uint32_t>& list);
 void launch_tail(hipStream_t s, const TailArgs& a, int grid, KTime* kt);
-// init_result_kernel's reset of res plus every word of the tail's counters ctl, one launch
-void launch_init_result_ctl(hipStream_t s, EvalResult* res, TailCtl* ctl);
+// init_result_kernel's reset of res plus every word of the tail's counters ctl, one launch;
+// it also stores tp (by value) into dtp
+void launch_init_result_ctl(hipStream_t s, EvalResult* res, TailCtl* ctl, const TermPack& tp, TermPack* dtp);
 // The single-evaluation tail list (gaplac_api.hip): T tile columns, X extra tile rows, the
 // simulated order per tail_sim (-1 auto: T < 80) planned for `workers` workgroups.
 void build_single_tail_list(int T, int X, int tail_sim, int workers, std::vector<uint32_t>& out, bool gram = false);

@@ -3678,16 +3678,23 @@ void launch_init_result(hipStream_t s, EvalResult* res) {
 // The result record and the tail's counters in one launch (the Gram inside the tail: the
 // evaluation's first launch is then this one, the tail the second; a hipMemsetAsync of the
 // counters was two fill launches of ~5 us each on the N = 4096 evaluation's critical path).
-__global__ __launch_bounds__(256) void init_result_ctl_kernel(EvalResult* res, unsigned* __restrict__ ctl, int nwords) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) init_result_kernel_body(res);
+// It also stores the evaluation's term descriptor, passed by value, into dtp: that replaces the
+// descriptor's host-to-device copy, one more operation on the evaluation's stream.
+__global__ __launch_bounds__(256) void init_result_ctl_kernel(EvalResult* res, unsigned* __restrict__ ctl, int nwords,
+                                                              const TermPack tp, TermPack* __restrict__ dtp) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        init_result_kernel_body(res);
+        *dtp = tp;
+    }
     for (int w = (int)(blockIdx.x * 256 + threadIdx.x); w < nwords; w += (int)gridDim.x * 256) ctl[w] = 0u;
 }
 
-void launch_init_result_ctl(hipStream_t s, EvalResult* res, TailCtl* ctl) {
+void launch_init_result_ctl(hipStream_t s, EvalResult* res, TailCtl* ctl, const TermPack& tp, TermPack* dtp) {
     if (!guard_launch("init_result_ctl_kernel")) return;
     static_assert(sizeof(TailCtl) % sizeof(unsigned) == 0, "TailCtl: whole words");
+    static_assert(sizeof(TermPack) <= 1024, "TermPack: passed as a kernel argument");
     init_result_ctl_kernel<<<dim3(64), dim3(256), 0, s>>>(res, reinterpret_cast<unsigned*>(ctl),
-                                                          (int)(sizeof(TailCtl) / sizeof(unsigned)));
+                                                          (int)(sizeof(TailCtl) / sizeof(unsigned)), tp, dtp);
 }
 
 }  // namespace gaplac
