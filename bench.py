@@ -132,8 +132,8 @@ def cpu_baseline(N: int, budget_s: float = 25.0):
 
 # PMC traffic of the dominant kernel (tools/profile_round.sh: FETCH_SIZE / WRITE_SIZE
 # passes over the same command, corrected per MI355X_MICROARCH.md; per launch).
-TRAFFIC_FILE = os.path.join("profiles", "r06g7_traffic_syrk.json")
-TRAFFIC_FILE_CINV = os.path.join("profiles", "r06g7_traffic_cinv.json")
+TRAFFIC_FILE = os.path.join("profiles", "r06g8_traffic_syrk.json")
+TRAFFIC_FILE_CINV = os.path.join("profiles", "r06g8_traffic_cinv.json")
 
 
 def load_traffic(name=TRAFFIC_FILE):
